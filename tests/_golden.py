@@ -1,0 +1,71 @@
+"""Helpers to read the golden fixtures captured from the reference (make_golden.py)."""
+import json
+import os
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as fh:
+        return json.load(fh)
+
+
+def case_names():
+    return [c["name"] for c in manifest()["cases"]]
+
+
+class Case:
+    def __init__(self, name):
+        man = manifest()
+        self.hyper = man["hyper"]
+        self.entry = next(c for c in man["cases"] if c["name"] == name)
+        self.name = name
+        self.world = int(self.entry["world"])
+        self.steps = int(self.entry["steps"])
+        self.r = int(self.entry["r"])
+        self.mats = [(n, int(m), int(k)) for n, m, k in self.entry["mats"]]
+        with np.load(os.path.join(GOLDEN, name + ".npz")) as z:
+            self.arr = {k: z[k] for k in z.files}
+
+    @property
+    def rank_fraction(self):
+        _, m, n = self.mats[0]
+        return self.r / min(m, n)
+
+    def t(self, rank, step, key):
+        return torch.from_numpy(self.arr[f"r{rank}_s{step}_{key}"].copy())
+
+    def has(self, rank, step, key):
+        return f"r{rank}_s{step}_{key}" in self.arr
+
+    def batches(self, rank, step):
+        return self.entry["rank_meta"][rank]["steps"][step]["batches"]
+
+    def ortho_calls(self, rank, step):
+        meta = self.entry["rank_meta"][rank]["steps"][step]["ortho"]
+        out = []
+        for i, om in enumerate(meta):
+            out.append(dict(
+                p_in=self.t(rank, step, f"ortho{i}_pin"),
+                p_out=self.t(rank, step, f"ortho{i}_pout"),
+                S=self.t(rank, step, f"ortho{i}_S") if om["has_sketch"] else None,
+            ))
+        return out
+
+    def sketch_for(self, rank, step, p_in):
+        """Return the sketch the reference drew for the ortho call whose input matches p_in."""
+        best, best_err = None, float("inf")
+        for call in self.ortho_calls(rank, step):
+            if call["p_in"].shape != p_in.shape:
+                continue
+            err = (call["p_in"] - p_in).abs().max().item()
+            if err < best_err:
+                best, best_err = call, err
+        assert best is not None, "no ortho call with matching shape"
+        scale = max(p_in.abs().max().item(), 1e-30)
+        assert best_err <= 1e-4 * scale, f"closest ortho input differs by {best_err}"
+        return best["S"]
