@@ -1,0 +1,195 @@
+"""Benchmark: device-resident Dion step over the Llama-3-8B 2D gradient set, rank 64.
+
+Contract (see the task's bench section and BASELINE.json):
+  python bench.py [--gpus N --steps K --warmup W]
+  N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL); every rank
+  compresses its own full gradient set (weak scaling) and exchanges P (reduce-
+  scatter + all-gather) and R (all-reduce) over the replicate group, exactly the
+  reference's RP = N low-rank path.  One JSON line on rank 0.
+
+A step = MegatronDion.step() over all 128 matrices (32 x {qkv 6144x4096,
+proj 4096x4096, fc1 28672x4096, fc2 4096x14336 (transposed)}): M += G,
+P = M Q, RCQR, R = M^T P, fix-up, error feedback, column norm, weight update.
+G is bf16 (synthetic N(0, 1e-3^2)), M / W / Q fp32, all resident in HBM.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "grad GiB/s/GPU (device-resident) Dion-compressed, Llama-3-8B 2D weights r=64"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+LLAMA3_8B_LAYER = (("linear_qkv", 6144, 4096), ("linear_proj", 4096, 4096),
+                   ("linear_fc1", 28672, 4096), ("linear_fc2", 4096, 14336))
+
+# algorithmic HBM bytes per matrix element of each codec call (DESIGN.md "bytes per unit")
+BYTES_PER_ELEM = {"project_p": 10.0, "project_r": 4.0, "ef_apply": 16.0}
+
+
+def llama_shapes(layers):
+    return [(f"layers.{i}.{n}.weight", m, k) for i in range(layers) for n, m, k in LLAMA3_8B_LAYER]
+
+
+class TimedCodec:
+    """Wraps the HIP codec; records HIP events around each call on the launch stream."""
+
+    def __init__(self, inner):
+        self.inner = inner
+        self.name = inner.name
+        self.enabled = False
+        self.events = {}
+
+    def __getattr__(self, item):
+        fn = getattr(self.inner, item)
+        if item not in ("project_p", "orthonormalize", "project_r", "fixup_colnorm", "ef_apply"):
+            return fn
+
+        def wrapped(*args, **kwargs):
+            if not self.enabled:
+                return fn(*args, **kwargs)
+            stream = torch.cuda.current_stream()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(stream)
+            out = fn(*args, **kwargs)
+            e.record(stream)
+            elems = 0
+            if item in BYTES_PER_ELEM:
+                mats = args[1] if item == "project_p" else args[0]
+                elems = sum(int(t.numel()) for t in mats)
+            self.events.setdefault(item, []).append((s, e, elems))
+            return out
+
+        return wrapped
+
+    def summary(self):
+        out = {}
+        for k, lst in self.events.items():
+            ms = [s.elapsed_time(e) for s, e, _ in lst]
+            elems = sum(n for _, _, n in lst)
+            out[k] = {"calls": len(lst), "total_ms": sum(ms), "avg_ms": sum(ms) / len(ms), "elems": elems}
+        return out
+
+
+def cpu_baseline(sample_layers=1, steps=1):
+    """The pinned CPU oracle (`port`) on one Llama-3-8B layer, timed on this host's cores."""
+    from oracle import dion_oracle as O
+
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    gen = torch.Generator().manual_seed(99)
+    hyper = O.DionHyper(rank_fraction=1 / 64)
+    mats = []
+    for _, m, n in llama_shapes(sample_layers):
+        W = torch.randn(m, n, generator=gen) * 0.02
+        M = torch.zeros(m, n)
+        q = torch.randn(m if m < n else n, 64, generator=gen)
+        G = (torch.randn(m, n, generator=gen) * 1e-3).to(torch.bfloat16).float()
+        mats.append(O.DionMatrix(W=W, M=M, Q=q, G=G, transposed=m < n, rank_fraction=1 / 64))
+    best = float("inf")
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        for mt in mats:
+            O.dion_batch_step_local([mt], hyper)
+        best = min(best, time.perf_counter() - t0)
+    elems = sum(m * n for _, m, n in llama_shapes(sample_layers))
+    return {"value": round(elems * 2 / best / 2 ** 30, 4), "unit": "GiB/s", "cores": cores, "kind": "port",
+            "sample": f"{sample_layers} of 32 Llama-3-8B layers (qkv, proj, fc1, fc2; {elems} grad elements), "
+                      f"r=64, best of {steps} step(s), {best:.2f} s, torch CPU fp32 with {cores} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--layers", type=int, default=32, help="Llama-3-8B has 32; fewer only for debugging")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        group = dist.group.WORLD
+
+    import megatron_dion_amd as mda
+    from megatron_dion_amd.codec import HipDionCodec
+    from megatron_dion_amd.optimizer import attach_dp_routing
+
+    shapes = llama_shapes(args.layers)
+    torch.manual_seed(1234 + rank)
+    named = []
+    for name, m, n in shapes:
+        w = torch.nn.Parameter(torch.empty(m, n, device=dev).normal_(0.0, 0.02))
+        w.grad = torch.empty(m, n, device=dev).normal_(0.0, 1e-3).to(torch.bfloat16)
+        named.append((name, w))
+    codec = TimedCodec(HipDionCodec(dev))
+    opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=1 / 64,
+                           codec=codec)
+    attach_dp_routing(opt, named, replicate_group=group)
+    elems = sum(m * n for _, m, n in shapes)
+
+    for _ in range(args.warmup):
+        opt.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    codec.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        opt.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    codec.enabled = False
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * elems * 2 / (elapsed / args.steps) / 2 ** 30
+
+    summ = codec.summary()
+    dominant = max(summ, key=lambda k: summ[k]["total_ms"])
+    d = summ[dominant]
+    bytes_per_launch = BYTES_PER_ELEM.get(dominant, 0.0) * d["elems"] / d["calls"]
+    achieved = bytes_per_launch / (d["avg_ms"] * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(d["avg_ms"], 4),
+                "per_call_ms": {k: round(v["total_ms"] / args.steps, 3) for k, v in summ.items()}}
+
+    out = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic (random-init Llama-3-8B 2D weight shapes, bf16 grads N(0,1e-3^2))",
+           "config": {"workload": "llama3-8b-2d-grad-set-r64", "matrices": len(shapes), "grad_elements": elems,
+                      "rank": 64, "grad_dtype": "bf16", "state_dtype": "f32",
+                      "parallelism": f"dp{world} (replicate, low-rank P/R exchange)" if world > 1 else "dp1"},
+           "roofline": roofline}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

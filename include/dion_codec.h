@@ -1,0 +1,136 @@
+/*
+ * dion_codec.h -- C ABI of the MI355X (gfx950) Dion gradient codec.
+ *
+ * Replaces the device work of the reference's Dion hot path
+ *   /root/reference/megatron/core/optimizer/dion/runtime.py:1499-1911
+ *   (batch_dion_update_async) and the helpers it calls.
+ * Each entry point below names the reference code it stands in for.
+ *
+ * Conventions:
+ *  - every function returns DION_OK (0) or a negative DION_E_* code; the text
+ *    of the last failure on the calling thread is dion_last_error();
+ *  - no allocation and no host synchronisation inside; everything is enqueued
+ *    on `stream` (a hipStream_t; torch.cuda.current_stream().cuda_stream);
+ *  - stateless and re-entrant; the caller owns every buffer;
+ *  - one matrix per pointer (pointer arrays, host memory, `desc->batch`
+ *    entries) exactly like the reference's per-parameter tensors; the small
+ *    factors P, R are one contiguous (batch, rows, r) fp32 buffer each, like
+ *    the reference's P_batch / R_batch;
+ *  - M, W are fp32 row-major m x n (row stride ld_m / ld_w elements); G is
+ *    bf16 or fp32 row-major (ld_g); Q is fp32 n_Q x r contiguous per matrix;
+ *  - orientation follows the reference's DionParamConfig.is_transposed
+ *    (dion/state.py:304-310): transposed == 0 => P has m rows (P = M Q),
+ *    transposed == 1 => P has n rows (P = M^T Q).  m_P = transposed ? n : m,
+ *    n_Q = transposed ? m : n.
+ */
+#ifndef DION_CODEC_H_
+#define DION_CODEC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
+
+#define DION_ABI_VERSION 1
+
+#define DION_OK 0
+#define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
+#define DION_E_UNSUPPORTED (-2) /* shape or dtype outside the built kernels     */
+#define DION_E_LAUNCH (-3)      /* HIP launch failure                           */
+#define DION_E_WORKSPACE (-4)   /* workspace smaller than dion_workspace_bytes  */
+
+#define DION_DTYPE_NONE 0
+#define DION_DTYPE_F32 1
+#define DION_DTYPE_BF16 2
+
+/* operations that need scratch (argument `op` of dion_workspace_bytes) */
+#define DION_OP_PROJECT_P 1
+#define DION_OP_ORTHONORMALIZE 2
+#define DION_OP_PROJECT_R 3
+
+typedef struct DionBatchDesc {
+  int32_t batch;      /* matrices in this call (all the same shape)            */
+  int32_t m, n;       /* storage shape of every M / G / W                      */
+  int32_t r;          /* rank = columns of P, Q, R  (1..128)                   */
+  int32_t transposed; /* reference DionParamConfig.is_transposed               */
+  int32_t g_dtype;    /* DION_DTYPE_NONE (no accumulate), _F32 or _BF16        */
+  int32_t m_dtype;    /* DION_DTYPE_F32                                        */
+  int32_t w_dtype;    /* DION_DTYPE_F32                                        */
+  int64_t ld_g;       /* row strides in elements; 0 means n                    */
+  int64_t ld_m;
+  int64_t ld_w;
+} DionBatchDesc;
+
+/* ABI version of the loaded library (== DION_ABI_VERSION). */
+int dion_abi_version(void);
+
+/* Text of the last error raised on this thread ("" if none). */
+const char* dion_last_error(void);
+
+/* Scratch bytes `op` needs for `desc` (0 is a valid answer). */
+int dion_workspace_bytes(const DionBatchDesc* desc, int op, size_t* bytes);
+
+/*
+ * Pass A.  For every matrix b:  M_b += G_b (when g_dtype != NONE),
+ *   P_b = X_b Q_b  with X_b = M_b (or M_b^T when transposed), fp32 (TF32 off),
+ *   nonzero[b] |= 1 if any element of the accumulated M_b is != 0.
+ * `nonzero` must be zeroed by the caller before the call.
+ * Replaces runtime.py:1560-1566 (momentum accumulate), :1602-1616 (stack +
+ * P = M Q) and the all-zero test of kernels.py:185 (is_all_zero).
+ */
+int dion_project_p(const DionBatchDesc* desc, const void* const* G, float* const* M,
+                   const float* const* Q, float* P, uint32_t* nonzero, void* ws,
+                   size_t ws_bytes, dion_stream_t stream);
+
+/*
+ * Randomised Cholesky QR of every P_b (m_P x r), in place
+ *   (ortho.py:71-123 orthogonalize):  m_P <= r: Q factor of a Householder QR;
+ *   else R1 = qr(S P).R, P <- P R1^-1, R2 = chol_upper(P^T P), P <- P R2^-1,
+ *   with S ~ N(0, 1/k), k = ceil(oversample r / 128) * 128.
+ * `sketch` (batch x k x m_P fp32, row-major) is used when non-null (parity
+ * tests); otherwise S is generated on the fly from (seed, b, row, col) by a
+ * counter-based Gaussian generator (the reference draws an unseeded sketch,
+ * ortho.py:659-661; results are sketch-invariant up to column signs).
+ */
+int dion_orthonormalize(const DionBatchDesc* desc, float* P, const float* sketch,
+                        uint64_t seed, float oversample, void* ws, size_t ws_bytes,
+                        dion_stream_t stream);
+
+/*
+ * Pass B.  R_b = X_b^T P_b  (n_Q x r), fp32.  runtime.py:1476-1477.
+ */
+int dion_project_r(const DionBatchDesc* desc, const float* const* M, const float* P,
+                   float* R, void* ws, size_t ws_bytes, dion_stream_t stream);
+
+/*
+ * fix_all_zero_or_nan (kernels.py:157-204) + column normalisation
+ * (kernels.py:207-210, 279-290) + Q commit (runtime.py:1132), for the
+ * `desc->batch` real entries:
+ *   z = !nonzero[b];  P_b <- z ? 0 : nan_to_num(P_b);
+ *   R_b <- z ? nan_to_num(Q_b) : nan_to_num(R_b);
+ *   Q_b <- R_b / (sqrt(sum_rows R_b^2) + eps)          (Q_b is overwritten)
+ */
+int dion_fixup_colnorm(const DionBatchDesc* desc, float* P, float* R, float* const* Q,
+                       const uint32_t* nonzero, float eps, dion_stream_t stream);
+
+/*
+ * Error feedback + weight update (kernels.py:54-154, 229-276; runtime.py:1105-1113):
+ *   M_b += -(1-mu) * (P_b R_b^T  or  R_b P_b^T when transposed)
+ *   W_b  = (wd > 0 ? (1 - lr*wd) : 1) * W_b - scaled_lr * (P_b Qn_b^T or Qn_b P_b^T)
+ * Qn_b is the committed Q (output of dion_fixup_colnorm).  W may be NULL
+ * (error feedback only).  Entries with nonzero[b] == 0 keep M and only decay W.
+ */
+int dion_ef_apply(const DionBatchDesc* desc, float* const* M, float* const* W,
+                  const float* P, const float* R, const float* const* Qn,
+                  const uint32_t* nonzero, float mu, float lr, float wd, float scaled_lr,
+                  dion_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DION_CODEC_H_ */

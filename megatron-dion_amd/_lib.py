@@ -1,0 +1,108 @@
+"""ctypes binding of the C ABI in include/dion_codec.h (libdion_codec.so).
+
+The library is built in-tree by `python __graft_entry__.py` (hipcc, gfx950) and
+must be present: there is no CPU or PyTorch fallback for the codec.  A missing
+or stale library raises `DionLibraryError` at first use.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "csrc", "libdion_codec.so")
+ABI_VERSION = 1
+
+DION_OK = 0
+DION_E_INVALID = -1
+DION_E_UNSUPPORTED = -2
+DION_E_LAUNCH = -3
+DION_E_WORKSPACE = -4
+
+DTYPE_NONE = 0
+DTYPE_F32 = 1
+DTYPE_BF16 = 2
+
+OP_PROJECT_P = 1
+OP_ORTHONORMALIZE = 2
+OP_PROJECT_R = 3
+
+# every symbol include/dion_codec.h declares
+EXPORTED = (
+    "dion_abi_version",
+    "dion_last_error",
+    "dion_workspace_bytes",
+    "dion_project_p",
+    "dion_orthonormalize",
+    "dion_project_r",
+    "dion_fixup_colnorm",
+    "dion_ef_apply",
+)
+
+
+class DionLibraryError(RuntimeError):
+    pass
+
+
+class DionBatchDesc(ctypes.Structure):
+    _fields_ = [
+        ("batch", ctypes.c_int32),
+        ("m", ctypes.c_int32),
+        ("n", ctypes.c_int32),
+        ("r", ctypes.c_int32),
+        ("transposed", ctypes.c_int32),
+        ("g_dtype", ctypes.c_int32),
+        ("m_dtype", ctypes.c_int32),
+        ("w_dtype", ctypes.c_int32),
+        ("ld_g", ctypes.c_int64),
+        ("ld_m", ctypes.c_int64),
+        ("ld_w", ctypes.c_int64),
+    ]
+
+
+_P = ctypes.c_void_p
+_PP = ctypes.POINTER(ctypes.c_void_p)
+_DESC = ctypes.POINTER(DionBatchDesc)
+
+_SIGNATURES = {
+    "dion_abi_version": ([], ctypes.c_int),
+    "dion_last_error": ([], ctypes.c_char_p),
+    "dion_workspace_bytes": ([_DESC, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "dion_project_p": ([_DESC, _PP, _PP, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "dion_orthonormalize": ([_DESC, _P, _P, ctypes.c_uint64, ctypes.c_float, _P, ctypes.c_size_t, _P],
+                            ctypes.c_int),
+    "dion_project_r": ([_DESC, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "dion_fixup_colnorm": ([_DESC, _P, _P, _PP, _P, ctypes.c_float, _P], ctypes.c_int),
+    "dion_ef_apply": ([_DESC, _PP, _PP, _P, _P, _PP, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                       ctypes.c_float, _P], ctypes.c_int),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the codec library; raise if it is missing or stale."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise DionLibraryError(
+            f"[DION_HIP_LIBRARY_MISSING] {path} not found; build it with "
+            "`python __graft_entry__.py` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    for name, (args, res) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    ver = lib.dion_abi_version()
+    if ver != ABI_VERSION:
+        raise DionLibraryError(f"[DION_HIP_ABI_MISMATCH] library ABI {ver}, expected {ABI_VERSION}")
+    if path == LIB_PATH:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != DION_OK:
+        msg = load().dion_last_error().decode("utf-8", "replace")
+        raise DionLibraryError(f"[DION_HIP_ERROR] {what} failed ({rc}): {msg}")

@@ -1,0 +1,153 @@
+"""Batch assembly for the data-parallel (replicate) Dion path.
+
+Follows /root/reference/megatron/core/optimizer/distrib_dion/batches.py:
+  build_batch_key            :76-107   (shape/shard/orientation/low-rank/dtype key)
+  update-contract key        :52-73    (lr, weight_decay, wd_mult, mu, rank_fraction, r)
+  group key                  :233-242  (kernel kind, batch world size, group ranks)
+  ordering                   :115-117, :195 (sorted by repr of the key; identical on every rank)
+  chunk + pad                :903-1067 (chunks of batch_world_size; padding entries carry
+                                        zero grad/momentum/Q, dist_meta=None, the first param)
+The reference agrees the order across ranks with a (cached) all_gather_object;
+replicas of a data-parallel model hold identical parameter sets, so the locally
+sorted order is already global.  `verify_schedule_across_ranks` performs the
+same agreement check once when asked.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .types import DionBatch, DionBatchCollectives, DionBatchEntry, DionBatchGroup
+
+
+def _norm_dim(dim, has_axis: bool) -> int:
+    if dim is None and not has_axis:
+        return -1
+    if dim is None:
+        raise RuntimeError("[Dion] missing shard tensor dim for active sharded axis in batch key construction")
+    return int(dim)
+
+
+def _norm_shape(shape) -> tuple:
+    return () if shape is None else tuple(int(d) for d in shape)
+
+
+def build_batch_key(shape, cfg, dtype, *, global_shape=None, per_expert_global_shape=None,
+                    tensor_row_shard_sizes=None, row_shard_sizes=None) -> tuple:
+    key_shape = per_expert_global_shape or global_shape or shape
+    return (
+        tuple(int(d) for d in key_shape),
+        bool(cfg.has_fs_shard),
+        bool(getattr(cfg, "use_fs_shard", cfg.has_fs_shard)),
+        bool(cfg.has_tp_shard),
+        bool(getattr(cfg, "use_tp_shard", cfg.has_tp_shard)),
+        bool(cfg.is_transposed),
+        bool(cfg.use_low_rank_sync),
+        _norm_dim(cfg.tp_shard_dim, cfg.has_tp_shard),
+        _norm_dim(cfg.fs_shard_dim, cfg.has_fs_shard),
+        dtype,
+        _norm_shape(global_shape),
+        _norm_shape(per_expert_global_shape),
+        _norm_shape(tensor_row_shard_sizes),
+        _norm_shape(row_shard_sizes),
+    )
+
+
+def _contract_key(group: Optional[dict], state: Optional[dict]) -> tuple:
+    def f(name):
+        return float(group[name]) if group is not None and name in group else None
+    r = int(state.get("r", -1)) if state is not None else -1
+    return (f("lr"), f("weight_decay"), f("wd_mult"), f("mu"), f("rank_fraction"), r)
+
+
+def _ranks(group) -> tuple:
+    if group is None:
+        return ()
+    try:
+        return tuple(int(x) for x in dist.get_process_group_ranks(group))
+    except Exception:  # fake groups in unit tests
+        return tuple(getattr(group, "ranks", ()))
+
+
+def _group_key(bg: DionBatchGroup) -> tuple:
+    return (str(bg.kernel_kind), int(bg.batch_world_size), _ranks(bg.replicate_group), _ranks(bg.ortho_group),
+            _ranks(bg.q_norm_group), _ranks(bg.low_rank_replicate_group),
+            tuple(_ranks(g) for g in bg.sync_groups))
+
+
+def resolve_dp_batch_group(config, *, replicate_group, group_size: Callable) -> DionBatchGroup:
+    """DP/RP-only form of resolve_batch_group (batches.py:496-603): no TP/FS axes."""
+    if getattr(config, "use_tp_shard", False) or getattr(config, "use_fs_shard", False):
+        raise RuntimeError("[DION_UNSUPPORTED_SHARDING] TP/FS-sharded Dion params are outside the DP codec path")
+    world = group_size(replicate_group) if replicate_group is not None else 1
+    sync = (replicate_group,) if (config.use_low_rank_sync and replicate_group is not None and world > 1) else ()
+    return DionBatchGroup(kernel_kind="ddp", replicate_group=replicate_group, batch_world_size=int(world),
+                          sync_groups=sync)
+
+
+def build_dion_batches(*, dion_params: Sequence, get_replicate_group: Callable,
+                       group_size: Callable = None, batch_key_cache: Optional[dict] = None,
+                       **_unused) -> List[DionBatch]:
+    """Group, order, chunk and pad routed Dion params into DionBatch objects."""
+    group_size = group_size or (lambda g: dist.get_world_size(g))
+    replicate_group = get_replicate_group()
+    grouped: Dict[tuple, list] = {}
+    groups: Dict[tuple, DionBatchGroup] = {}
+    for sp in dion_params:
+        state = sp.optimizer_state
+        meta = sp.dist_meta
+        cfg = sp.config
+        local_shape = state.get("local_shape") or tuple(sp.param.shape)
+        global_shape = state.get("global_shape") or getattr(meta, "global_shape", None)
+        per_expert = state.get("per_expert_global_shape") or getattr(meta, "per_expert_global_shape", None)
+        bg = resolve_dp_batch_group(cfg, replicate_group=replicate_group, group_size=group_size)
+        key = (build_batch_key(local_shape, cfg, sp.grad.dtype, global_shape=global_shape,
+                               per_expert_global_shape=per_expert,
+                               tensor_row_shard_sizes=getattr(meta, "tensor_row_shard_sizes", None),
+                               row_shard_sizes=getattr(meta, "row_shard_sizes", None)),
+               _contract_key(sp.optim_group, state), _group_key(bg))
+        grouped.setdefault(key, []).append(sp)
+        groups.setdefault(key, bg)
+
+    batches: List[DionBatch] = []
+    cache_key = 0
+    for key in sorted(grouped, key=repr):
+        items = grouped[key]
+        bg = groups[key]
+        size = max(1, int(bg.batch_world_size))
+        for start in range(0, len(items), size):
+            chunk = items[start:start + size]
+            entries = []
+            for sp in chunk:
+                shape = tuple(int(d) for d in sp.optimizer_state["momentum"].shape)
+                entries.append(DionBatchEntry(
+                    param=sp.param, grad=sp.grad.view(*shape), optimizer_state=sp.optimizer_state,
+                    optim_group=sp.optim_group, config=sp.config, dist_meta=sp.dist_meta,
+                    momentum=sp.optimizer_state["momentum"].view(*shape), q_tensor=sp.optimizer_state["Q"],
+                    param_shape=shape, commit_update=sp.commit_update))
+            real = len(entries)
+            tmpl = entries[0]
+            while len(entries) < size:
+                entries.append(DionBatchEntry(
+                    param=tmpl.param, grad=torch.zeros_like(tmpl.grad), optimizer_state=None,
+                    optim_group=tmpl.optim_group, config=tmpl.config, dist_meta=None,
+                    momentum=torch.zeros_like(tmpl.momentum), q_tensor=torch.zeros_like(tmpl.q_tensor),
+                    param_shape=tmpl.param_shape))
+            batches.append(DionBatch(batch_key=key, entries=tuple(entries), real_batch_size=real,
+                                     batch_cache_key=cache_key, batch_group=bg,
+                                     batch_collectives=DionBatchCollectives()))
+            cache_key += real
+    return batches
+
+
+def verify_schedule_across_ranks(batches: Sequence[DionBatch], group) -> None:
+    """Check every rank built the same (key, real size) schedule (batches.py:185-216)."""
+    if group is None or dist.get_world_size(group) <= 1:
+        return
+    mine = [(repr(b.batch_key), int(b.real_batch_size)) for b in batches]
+    gathered: List = [None] * dist.get_world_size(group)
+    dist.all_gather_object(gathered, mine, group=group)
+    if any(g != mine for g in gathered):
+        raise RuntimeError("[DION_BATCH_KEY_MULTIPLICITY_MISMATCH] ranks built different Dion batch schedules")

@@ -1,0 +1,168 @@
+"""Device codec: thin torch-facing wrapper over the C ABI (include/dion_codec.h).
+
+`HipDionCodec` is the only compute backend of the product path.  It takes the
+reference's per-parameter tensors (one device tensor per matrix, exactly like
+`DionBatch.params / momentums / q_tensors / grads`,
+/root/reference/megatron/core/optimizer/dion/types.py:161-226) plus the batch
+factors P (B, m_P, r) and R (B, n_Q, r), and enqueues the HIP kernels on the
+current HIP stream.  Torch is used only for memory and streams.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _lib
+
+__all__ = ["HipDionCodec", "factor_rows"]
+
+
+def factor_rows(m: int, n: int, transposed: bool):
+    """(m_P, n_Q): P rows and Q rows for one m x n matrix (state.py:304-310 orientation)."""
+    return (n, m) if transposed else (m, n)
+
+
+def _ptrs(tensors: Sequence[Optional[torch.Tensor]]):
+    arr = (ctypes.c_void_p * max(1, len(tensors)))()
+    for i, t in enumerate(tensors):
+        arr[i] = None if t is None else t.data_ptr()
+    return arr
+
+
+def _dtype_code(t: Optional[torch.Tensor]) -> int:
+    if t is None:
+        return _lib.DTYPE_NONE
+    if t.dtype == torch.float32:
+        return _lib.DTYPE_F32
+    if t.dtype == torch.bfloat16:
+        return _lib.DTYPE_BF16
+    raise RuntimeError(f"[DION_UNSUPPORTED_DTYPE] {t.dtype}")
+
+
+def _row_stride(t: torch.Tensor) -> int:
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise RuntimeError(f"[DION_NON_ROW_MAJOR] shape={tuple(t.shape)} stride={t.stride()}")
+    return int(t.stride(0))
+
+
+class HipDionCodec:
+    """Enqueue the Dion codec kernels for batches of same-shape matrices."""
+
+    name = "hip"
+
+    def __init__(self, device: Optional[torch.device] = None):
+        self.lib = _lib.load()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self._ws = torch.empty(0, dtype=torch.uint8, device=self.device)
+
+    # ------------------------------------------------------------------ helpers
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _desc(self, batch, m, n, r, transposed, g=None, M=None, W=None) -> _lib.DionBatchDesc:
+        d = _lib.DionBatchDesc()
+        d.batch = int(batch)
+        d.m, d.n, d.r = int(m), int(n), int(r)
+        d.transposed = 1 if transposed else 0
+        d.g_dtype = _dtype_code(g)
+        d.m_dtype = _lib.DTYPE_F32
+        d.w_dtype = _lib.DTYPE_F32
+        d.ld_g = _row_stride(g) if g is not None else 0
+        d.ld_m = _row_stride(M) if M is not None else 0
+        d.ld_w = _row_stride(W) if W is not None else 0
+        return d
+
+    def workspace(self, desc, op) -> torch.Tensor:
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(self.lib.dion_workspace_bytes(ctypes.byref(desc), op, ctypes.byref(nbytes)),
+                   "dion_workspace_bytes")
+        if nbytes.value > self._ws.numel():
+            self._ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def _check_batch(self, mats: Sequence[torch.Tensor]):
+        m, n = mats[0].shape
+        for t in mats:
+            if tuple(t.shape) != (m, n) or t.dtype != torch.float32 or t.device != self.device:
+                raise RuntimeError(f"[DION_INCONSISTENT_BATCH] {tuple(t.shape)} {t.dtype} {t.device}")
+        return int(m), int(n)
+
+    # ------------------------------------------------------------------ passes
+    def project_p(self, grads: Optional[List[torch.Tensor]], momentums: List[torch.Tensor],
+                  qs: List[torch.Tensor], P: torch.Tensor, nonzero: torch.Tensor, transposed: bool) -> None:
+        """M += G; P = M Q (or M^T Q); nonzero flags.  runtime.py:1560-1616."""
+        B = len(momentums)
+        if B == 0:
+            return
+        m, n = self._check_batch(momentums)
+        r = int(qs[0].shape[1])
+        g0 = grads[0] if grads else None
+        if grads:
+            for g in grads:
+                if g.dtype != g0.dtype or tuple(g.shape) != (m, n) or g.stride() != g0.stride():
+                    raise RuntimeError("[DION_INCONSISTENT_GRADS]")
+        d = self._desc(B, m, n, r, transposed, g=g0, M=momentums[0])
+        ws = self.workspace(d, _lib.OP_PROJECT_P)
+        rc = self.lib.dion_project_p(ctypes.byref(d), _ptrs(grads) if grads else None, _ptrs(momentums),
+                                     _ptrs(qs), P.data_ptr(), nonzero.data_ptr(), ws.data_ptr(),
+                                     ws.numel(), self._stream())
+        _lib.check(rc, "dion_project_p")
+
+    def orthonormalize(self, P: torch.Tensor, m: int, n: int, transposed: bool, seed: int,
+                       oversample: float = 1.25, sketch: Optional[torch.Tensor] = None) -> None:
+        """Randomised Cholesky QR of every P_b in place.  ortho.py:71-123."""
+        B, _, r = P.shape
+        if B == 0:
+            return
+        d = self._desc(B, m, n, r, transposed)
+        ws = self.workspace(d, _lib.OP_ORTHONORMALIZE)
+        rc = self.lib.dion_orthonormalize(ctypes.byref(d), P.data_ptr(),
+                                          None if sketch is None else sketch.data_ptr(),
+                                          int(seed) & ((1 << 64) - 1), float(oversample),
+                                          ws.data_ptr(), ws.numel(), self._stream())
+        _lib.check(rc, "dion_orthonormalize")
+
+    def project_r(self, momentums: List[torch.Tensor], P: torch.Tensor, R: torch.Tensor,
+                  transposed: bool) -> None:
+        """R = M^T P (or M P).  runtime.py:1476-1477."""
+        B = len(momentums)
+        if B == 0:
+            return
+        m, n = self._check_batch(momentums)
+        r = int(P.shape[2])
+        d = self._desc(B, m, n, r, transposed, M=momentums[0])
+        ws = self.workspace(d, _lib.OP_PROJECT_R)
+        rc = self.lib.dion_project_r(ctypes.byref(d), _ptrs(momentums), P.data_ptr(), R.data_ptr(),
+                                     ws.data_ptr(), ws.numel(), self._stream())
+        _lib.check(rc, "dion_project_r")
+
+    def fixup_colnorm(self, P: torch.Tensor, R: torch.Tensor, qs: List[torch.Tensor],
+                      nonzero: torch.Tensor, eps: float, m: int, n: int, transposed: bool) -> None:
+        """fix_all_zero_or_nan + column normalisation; Q states receive Q_new."""
+        B = len(qs)
+        if B == 0:
+            return
+        r = int(P.shape[2])
+        d = self._desc(B, m, n, r, transposed)
+        rc = self.lib.dion_fixup_colnorm(ctypes.byref(d), P.data_ptr(), R.data_ptr(), _ptrs(qs),
+                                         nonzero.data_ptr(), float(eps), self._stream())
+        _lib.check(rc, "dion_fixup_colnorm")
+
+    def ef_apply(self, momentums: List[torch.Tensor], params: Optional[List[torch.Tensor]],
+                 P: torch.Tensor, R: torch.Tensor, qs: List[torch.Tensor], nonzero: torch.Tensor,
+                 mu: float, lr: float, wd: float, scaled_lr: float, transposed: bool) -> None:
+        """Error feedback and weight update.  kernels.py:54-154, runtime.py:1105-1113."""
+        B = len(momentums)
+        if B == 0:
+            return
+        m, n = self._check_batch(momentums)
+        if params is not None:
+            self._check_batch(params)
+        r = int(P.shape[2])
+        d = self._desc(B, m, n, r, transposed, M=momentums[0], W=params[0] if params else None)
+        rc = self.lib.dion_ef_apply(ctypes.byref(d), _ptrs(momentums), _ptrs(params) if params else None,
+                                    P.data_ptr(), R.data_ptr(), _ptrs(qs), nonzero.data_ptr(), float(mu),
+                                    float(lr), float(wd), float(scaled_lr), self._stream())
+        _lib.check(rc, "dion_ef_apply")

@@ -1,0 +1,1309 @@
+// dion_codec.hip -- MI355X (gfx950, CDNA4) kernels of the Dion gradient codec.
+//
+// What each kernel replaces in the reference (all paths under
+// /root/reference/megatron/core/optimizer/):
+//   rowproj_kernel / colproj_kernel  dion/runtime.py:1560-1616 (M += G, P = M Q),
+//                                     dion/runtime.py:1476-1477 (R = M^T P)
+//   sketch/gram colproj (panel mode), householder_qr_kernel, cholesky_kernel,
+//   trsm_kernel                       dion/ortho.py:71-123 (randomised Cholesky QR)
+//   fixup_colnorm_kernel, pfix_kernel dion/kernels.py:157-210, 279-290
+//   ef_update_kernel                  dion/kernels.py:54-154, 229-276;
+//                                     dion/runtime.py:1105-1113
+//
+// Design (DESIGN.md has the long form):
+//  * All arithmetic is fp32 (the reference disables TF32, ortho.py:25-45); the
+//    contractions run on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32 for the
+//    projections, v_mfma_f32_32x32x2_f32 for the rank-r updates), which is a
+//    k-ordered fmaf chain.
+//  * The big operand (momentum M, m x n fp32 row-major) is streamed once per
+//    pass straight into MFMA operand registers with 16-byte loads: for P = M Q
+//    each lane reads 8 consecutive columns of one row (16 rows x 128 B per
+//    load pair), for R = M^T P each lane reads 4 consecutive columns
+//    (4 rows x 256 B per load).  The K order inside an MFMA is free, so no LDS
+//    transpose is needed.  The thin operand (Q or P, <= 1 MB) is L2-resident.
+//  * Split-K partials go to fp32 slabs in the caller's workspace and are summed
+//    by a deterministic reduction (no float atomics: bitwise-reproducible).
+//  * Per-matrix pointers travel in the kernel-argument block (up to 64
+//    matrices per launch), so there is no pointer-array upload.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <stdarg.h>
+
+#include <type_traits>
+
+#include "../../include/dion_codec.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define MAXB 64  // matrices per launch (pointer arrays live in kernel arguments)
+
+// ----------------------------------------------------------------------------- errors
+static thread_local char g_err[512];
+
+static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+static int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(DION_E_LAUNCH, "%s: %s", what, hipGetErrorString(e));
+  return DION_OK;
+}
+
+// ----------------------------------------------------------------------------- helpers
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(static_cast<uint32_t>(h) << 16);
+}
+
+__device__ __forceinline__ float nan_to_num(float x) {
+  // torch.nan_to_num defaults: NaN -> 0, +inf -> FLT_MAX, -inf -> -FLT_MAX
+  if (x != x) return 0.f;
+  if (x == INFINITY) return 3.402823466e38f;
+  if (x == -INFINITY) return -3.402823466e38f;
+  return x;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Counter-based N(0,1) draw for the on-device sketch: two 32-bit outputs of a
+// splitmix64-style mix of (seed, row, col) feed Box-Muller.  Stateless, so any
+// tile of S can be regenerated anywhere without storing S in HBM.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float gauss(uint64_t seed, uint32_t row, uint32_t col) {
+  const uint64_t h = mix64(seed ^ mix64((static_cast<uint64_t>(row) << 32) | col));
+  const float u1 = (static_cast<float>(static_cast<uint32_t>(h >> 40)) + 0.5f) * (1.0f / 16777216.0f);
+  const float u2 = static_cast<float>(static_cast<uint32_t>(h & 0xFFFFFFu)) * (1.0f / 16777216.0f);
+  return sqrtf(-2.0f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+}
+
+// ----------------------------------------------------------------------------- args
+struct ProjArgs {
+  const void* g[MAXB];     // gradient per matrix (pass A) or null
+  float* m[MAXB];          // momentum per matrix (read; written when G present)
+  const float* thin[MAXB]; // thin operand per matrix: Q (pass A) or P_b (pass B) or P_b (panels)
+  float* out;              // (batch, nchunk, out_rows, r) slab or final (nchunk == 1)
+  uint32_t* nonzero;       // per-matrix nonzero flags (pass A) or null
+  const float* sketch;     // explicit sketch (batch, k, m_P) or null
+  uint64_t seed;
+  float sketch_std;
+  int rows, cols, r;       // X is rows x cols; thin is (rows or cols) x r
+  long ld_m, ld_g;
+  int kchunk, nchunk, out_rows;
+  int vec;                 // 16-byte loads allowed
+};
+
+// ============================================================================
+// Row projection:  out[b][i][c] = sum_j X_b[i][j] * T_b[j][c]    (X = M (+ G))
+//   P = M Q for is_transposed == 0 (pass A) and R = M P for is_transposed == 1
+//   (pass B).  256 threads = 4 waves, wave tile 32 rows x r, block 128 rows,
+//   split-K over columns (blockIdx.y).  MFMA 16x16x4 f32:
+//   A operand lane l = X[row0 + (l&15)][j0 + 8*(l>>4) + s], s = 0..7 (one
+//   16-byte load pair per lane = 128 contiguous bytes per row per wave);
+//   B operand lane l = T[j0 + 8*(l>>4) + s][16*cb + (l&15)].
+// ============================================================================
+template <int GDT>
+__device__ __forceinline__ void load_row8(const ProjArgs& a, float* __restrict__ M,
+                                          const void* __restrict__ G, int row, int jj, int j_end,
+                                          float (&x)[8], bool& nz) {
+  if (row >= a.rows) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) x[s] = 0.f;
+    return;
+  }
+  float* p = M + static_cast<long>(row) * a.ld_m + jj;
+  if (a.vec && jj + 8 <= j_end) {
+    f32x4 v0 = *reinterpret_cast<const f32x4*>(p);
+    f32x4 v1 = *reinterpret_cast<const f32x4*>(p + 4);
+    if constexpr (GDT == DION_DTYPE_F32) {
+      const float* gp = static_cast<const float*>(G) + static_cast<long>(row) * a.ld_g + jj;
+      v0 += *reinterpret_cast<const f32x4*>(gp);
+      v1 += *reinterpret_cast<const f32x4*>(gp + 4);
+    } else if constexpr (GDT == DION_DTYPE_BF16) {
+      const uint16_t* gp = static_cast<const uint16_t*>(G) + static_cast<long>(row) * a.ld_g + jj;
+      const uint4 gv = *reinterpret_cast<const uint4*>(gp);
+      v0[0] += __uint_as_float(gv.x << 16);
+      v0[1] += __uint_as_float(gv.x & 0xFFFF0000u);
+      v0[2] += __uint_as_float(gv.y << 16);
+      v0[3] += __uint_as_float(gv.y & 0xFFFF0000u);
+      v1[0] += __uint_as_float(gv.z << 16);
+      v1[1] += __uint_as_float(gv.z & 0xFFFF0000u);
+      v1[2] += __uint_as_float(gv.w << 16);
+      v1[3] += __uint_as_float(gv.w & 0xFFFF0000u);
+    }
+    if constexpr (GDT != DION_DTYPE_NONE) {
+      *reinterpret_cast<f32x4*>(p) = v0;
+      *reinterpret_cast<f32x4*>(p + 4) = v1;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      x[s] = v0[s];
+      x[s + 4] = v1[s];
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      float v = 0.f;
+      if (jj + s < j_end) {
+        v = p[s];
+        if constexpr (GDT == DION_DTYPE_F32) {
+          v += static_cast<const float*>(G)[static_cast<long>(row) * a.ld_g + jj + s];
+        } else if constexpr (GDT == DION_DTYPE_BF16) {
+          v += bf16_to_f32(static_cast<const uint16_t*>(G)[static_cast<long>(row) * a.ld_g + jj + s]);
+        }
+        if constexpr (GDT != DION_DTYPE_NONE) p[s] = v;
+      }
+      x[s] = v;
+    }
+  }
+  if constexpr (GDT != DION_DTYPE_NONE) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) nz |= (x[s] != 0.f);
+  }
+}
+
+template <int RB, int GDT>
+__global__ void __launch_bounds__(256) rowproj_kernel(const ProjArgs a) {
+  const int b = blockIdx.z;
+  const int kc = blockIdx.y;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int row_base = blockIdx.x * 128 + wave * 32;
+  const int j_begin = kc * a.kchunk;
+  const int j_end = min(a.cols, j_begin + a.kchunk);
+  float* __restrict__ M = a.m[b];
+  const void* __restrict__ G = a.g[b];
+  const float* __restrict__ T = a.thin[b];
+  const int r = a.r;
+
+  f32x4 acc[2][RB];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bool nz = false;
+
+  for (int j0 = j_begin; j0 < j_end; j0 += 32) {
+    const int jj = j0 + 8 * g;
+    float xv[2][8];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) load_row8<GDT>(a, M, G, row_base + 16 * rb + t, jj, j_end, xv[rb], nz);
+    float tv[8][RB];
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int cb = 0; cb < RB; ++cb) {
+        const int j = jj + s;
+        const int c = 16 * cb + t;
+        tv[s][cb] = (j < j_end && c < r) ? T[static_cast<long>(j) * r + c] : 0.f;
+      }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < RB; ++cb)
+          acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[rb][s], tv[s][cb], acc[rb][cb], 0, 0, 0);
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * r;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = row_base + 16 * rb + 4 * g + q;
+        const int c = 16 * cb + t;
+        if (row < a.rows && c < r) out[static_cast<long>(row) * r + c] = acc[rb][cb][q];
+      }
+  if constexpr (GDT != DION_DTYPE_NONE) {
+    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+  }
+}
+
+// ============================================================================
+// Column projection:  out[b][j][c] = sum_i X_b[i][j] * T_b[i][c]
+//   P = M^T Q for is_transposed == 1 (pass A), R = M^T P for is_transposed == 0
+//   (pass B); in PANEL mode also the RCQR reductions S P (X = S^T, generated or
+//   explicit) and P^T P (X = P).
+//   MFMA 16x16x4 f32: A operand lane l = X[i0 + (l>>4)][col0 + 4*(l&15) + e]
+//   (one 16-byte load per lane covers 4 rows x 256 contiguous bytes), block e
+//   of the output holds columns col0 + 4*t + e; B operand = T[i0 + (l>>4)][16cb + (l&15)].
+//   PANEL == 0: 4 waves split 256 columns; PANEL == 1: 4 waves split the rows
+//   of a 64-column tile and reduce through LDS (for narrow X such as P).
+//   XMODE: 0 = row-major X (momentum, optional fused G), 1 = explicit sketch
+//   S^T, 2 = generated sketch.
+// ============================================================================
+template <int GDT, int XMODE>
+__device__ __forceinline__ void load_col4(const ProjArgs& a, int b, float* __restrict__ M,
+                                          const void* __restrict__ G, int i, int i_end, int col,
+                                          float (&x)[4], bool& nz) {
+  if (i >= i_end) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = 0.f;
+    return;
+  }
+  if constexpr (XMODE == 1) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int aa = col + e;
+      x[e] = (aa < a.cols) ? a.sketch[(static_cast<long>(b) * a.cols + aa) * a.rows + i] : 0.f;
+    }
+    return;
+  } else if constexpr (XMODE == 2) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int aa = col + e;
+      x[e] = (aa < a.cols) ? a.sketch_std * gauss(a.seed + 0x632BE59BD9B4E019ull * (b + 1), aa, i) : 0.f;
+    }
+    return;
+  } else {
+    float* p = M + static_cast<long>(i) * a.ld_m + col;
+    if (a.vec && col + 4 <= a.cols) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(p);
+      if constexpr (GDT == DION_DTYPE_F32) {
+        v += *reinterpret_cast<const f32x4*>(static_cast<const float*>(G) + static_cast<long>(i) * a.ld_g + col);
+      } else if constexpr (GDT == DION_DTYPE_BF16) {
+        const uint2 gv = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(G) +
+                                                         static_cast<long>(i) * a.ld_g + col);
+        v[0] += __uint_as_float(gv.x << 16);
+        v[1] += __uint_as_float(gv.x & 0xFFFF0000u);
+        v[2] += __uint_as_float(gv.y << 16);
+        v[3] += __uint_as_float(gv.y & 0xFFFF0000u);
+      }
+      if constexpr (GDT != DION_DTYPE_NONE) *reinterpret_cast<f32x4*>(p) = v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = v[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = 0.f;
+        if (col + e < a.cols) {
+          v = p[e];
+          if constexpr (GDT == DION_DTYPE_F32) {
+            v += static_cast<const float*>(G)[static_cast<long>(i) * a.ld_g + col + e];
+          } else if constexpr (GDT == DION_DTYPE_BF16) {
+            v += bf16_to_f32(static_cast<const uint16_t*>(G)[static_cast<long>(i) * a.ld_g + col + e]);
+          }
+          if constexpr (GDT != DION_DTYPE_NONE) p[e] = v;
+        }
+        x[e] = v;
+      }
+    }
+    if constexpr (GDT != DION_DTYPE_NONE) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) nz |= (x[e] != 0.f);
+    }
+  }
+}
+
+template <int RB, int GDT, int XMODE, int PANEL>
+__global__ void __launch_bounds__(256) colproj_kernel(const ProjArgs a) {
+  const int b = blockIdx.z;
+  const int kc = blockIdx.y;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int col_base = PANEL ? blockIdx.x * 64 : blockIdx.x * 256 + wave * 64;
+  const int i_begin = kc * a.kchunk;
+  const int i_end = min(a.rows, i_begin + a.kchunk);
+  float* __restrict__ M = (XMODE == 0) ? a.m[b] : nullptr;
+  const void* __restrict__ G = (XMODE == 0) ? a.g[b] : nullptr;
+  const float* __restrict__ T = a.thin[b];
+  const int r = a.r;
+  const int col = col_base + 4 * t;
+
+  f32x4 acc[4][RB];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[e][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bool nz = false;
+
+  const int i_first = i_begin + (PANEL ? 4 * wave : 0);
+  const int i_step = PANEL ? 16 : 4;
+  for (int i0 = i_first; i0 < i_end; i0 += i_step) {
+    const int i = i0 + g;
+    float xv[4];
+    load_col4<GDT, XMODE>(a, b, M, G, i, i_end, col, xv, nz);
+    float tv[RB];
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      const int c = 16 * cb + t;
+      tv[cb] = (i < i_end && c < r) ? T[static_cast<long>(i) * r + c] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int cb = 0; cb < RB; ++cb)
+        acc[e][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[e], tv[cb], acc[e][cb], 0, 0, 0);
+  }
+
+  if constexpr (PANEL) {
+    // fixed-order cross-wave reduction through one LDS buffer (deterministic)
+    __shared__ float red[64][4 * RB * 4 + 1];
+    for (int w = 1; w < 4; ++w) {
+      __syncthreads();
+      if (wave == w) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[lane][(e * RB + cb) * 4 + q] = acc[e][cb][q];
+      }
+      __syncthreads();
+      if (wave == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[e][cb][q] += red[lane][(e * RB + cb) * 4 + q];
+      }
+    }
+    if (wave != 0) return;
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = col_base + 4 * (4 * g + q) + e;
+        const int c = 16 * cb + t;
+        if (j < a.cols && c < r) out[static_cast<long>(j) * r + c] = acc[e][cb][q];
+      }
+  if constexpr (GDT != DION_DTYPE_NONE) {
+    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+  }
+}
+
+// out[b][e] = sum_k slab[b][k][e] in fixed k order.
+__global__ void __launch_bounds__(256) reduce_slabs_kernel(float* __restrict__ out,
+                                                           const float* __restrict__ slab, int nchunk,
+                                                           long per_entry, int batch) {
+  const long total = per_entry * batch;
+  for (long idx = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
+       idx += static_cast<long>(gridDim.x) * blockDim.x) {
+    const long b = idx / per_entry;
+    const long e = idx - b * per_entry;
+    const float* s = slab + b * nchunk * per_entry + e;
+    float v = 0.f;
+    for (int k = 0; k < nchunk; ++k) v += s[k * per_entry];
+    out[idx] = v;
+  }
+}
+
+// ============================================================================
+// Householder QR of one K x r matrix per block (LAPACK dgeqr2 / dlarfg sign
+// convention, which torch.linalg.qr on CPU and the reference inherit):
+//   mode 0: write R (r x r upper) to R_out[b];
+//   mode 1: form the K x r Q factor in place (dorg2r) and write it to Q_out[b]
+//           (the m_P <= r branch of ortho.py:93-94).
+// The matrix lives column-major in LDS.
+// ============================================================================
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float s = 0.f;
+  const int nw = blockDim.x >> 6;
+  for (int w = 0; w < nw; ++w) s += red[w];
+  return s;
+}
+
+__global__ void __launch_bounds__(256) householder_qr_kernel(const float* __restrict__ A_in,
+                                                             float* __restrict__ R_out,
+                                                             float* __restrict__ Q_out, int K, int r,
+                                                             int mode) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int b = blockIdx.x;
+  const int ld = K + 1;
+  float* As = sm;               // r columns x ld
+  float* tau = As + r * ld;     // r
+  float* red = tau + r + 3;     // reduction scratch (8)
+  float* bc = red + 8;          // broadcast scalars (4)
+  const int tid = threadIdx.x;
+  const int nt = blockDim.x;
+  const float* A = A_in + static_cast<long>(b) * K * r;
+  for (int idx = tid; idx < K * r; idx += nt) {
+    const int i = idx / r, c = idx - i * r;
+    As[c * ld + i] = A[idx];
+  }
+  __syncthreads();
+  const int kmax = min(K, r);
+  const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+  for (int j = 0; j < kmax; ++j) {
+    float* aj = As + j * ld;
+    float ss = 0.f;
+    for (int i = j + 1 + tid; i < K; i += nt) ss += aj[i] * aj[i];
+    ss = block_sum(ss, red);
+    if (tid == 0) {
+      const float alpha = aj[j];
+      const float xnorm = sqrtf(ss);
+      float tj, beta, scale;
+      if (xnorm == 0.f) {
+        tj = 0.f;
+        beta = alpha;
+        scale = 1.f;
+      } else {
+        beta = -copysignf(hypotf(alpha, xnorm), alpha);
+        tj = (beta - alpha) / beta;
+        scale = 1.f / (alpha - beta);
+      }
+      tau[j] = tj;
+      bc[0] = scale;
+      bc[1] = beta;
+    }
+    __syncthreads();
+    const float scale = bc[0];
+    for (int i = j + 1 + tid; i < K; i += nt) aj[i] *= scale;
+    __syncthreads();
+    if (tid == 0) aj[j] = bc[1];
+    const float tj = tau[j];
+    // apply H_j = I - tau v v^T (v_j = 1) to the trailing columns, one wave per column
+    for (int c = j + 1 + wave; c < r; c += nw) {
+      float* ac = As + c * ld;
+      float w = 0.f;
+      for (int i = j + 1 + lane; i < K; i += 64) w += aj[i] * ac[i];
+      w = wave_sum(w) + ac[j];
+      w *= tj;
+      if (lane == 0) ac[j] -= w;
+      for (int i = j + 1 + lane; i < K; i += 64) ac[i] -= w * aj[i];
+    }
+    __syncthreads();
+  }
+  if (mode == 0) {
+    float* R = R_out + static_cast<long>(b) * r * r;
+    for (int idx = tid; idx < r * r; idx += nt) {
+      const int i = idx / r, c = idx - i * r;
+      R[idx] = (i <= c && i < K) ? As[c * ld + i] : 0.f;
+    }
+    return;
+  }
+  // dorg2r: form Q (K x r) in place from the stored reflectors
+  for (int j = kmax - 1; j >= 0; --j) {
+    float* aj = As + j * ld;
+    const float tj = tau[j];
+    if (j < r - 1) {
+      for (int c = j + 1 + wave; c < r; c += nw) {
+        float* ac = As + c * ld;
+        float w = 0.f;
+        for (int i = j + 1 + lane; i < K; i += 64) w += aj[i] * ac[i];
+        w = wave_sum(w) + ac[j];  // v_j = 1
+        w *= tj;
+        if (lane == 0) ac[j] -= w;
+        for (int i = j + 1 + lane; i < K; i += 64) ac[i] -= w * aj[i];
+      }
+    }
+    __syncthreads();
+    for (int i = j + 1 + tid; i < K; i += nt) aj[i] *= -tj;
+    if (tid == 0) aj[j] = 1.f - tj;
+    for (int i = tid; i < j; i += nt) aj[i] = 0.f;
+    __syncthreads();
+  }
+  float* Q = Q_out + static_cast<long>(b) * K * r;
+  for (int idx = tid; idx < K * r; idx += nt) {
+    const int i = idx / r, c = idx - i * r;
+    Q[idx] = As[c * ld + i];
+  }
+}
+
+// ============================================================================
+// Upper Cholesky (LAPACK dpotf2 order: ajj = a_jj - u_j.u_j, u_jj = sqrt(ajj),
+// row j scaled by 1/u_jj) of one r x r Gram matrix per block.  A non-positive
+// or NaN pivot poisons the remaining diagonal with NaN (cholesky_ex does not
+// raise, ortho.py:112-115; the downstream nan_to_num fix-up handles it).
+// ============================================================================
+__global__ void __launch_bounds__(256) cholesky_kernel(const float* __restrict__ G_in,
+                                                       float* __restrict__ U_out, int r) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int b = blockIdx.x;
+  const int ld = r + 1;
+  float* U = sm;  // r x ld, row-major, upper triangle used
+  float* bc = U + r * ld;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const float* Gm = G_in + static_cast<long>(b) * r * r;
+  for (int idx = tid; idx < r * r; idx += nt) {
+    const int i = idx / r, c = idx - i * r;
+    U[i * ld + c] = Gm[idx];
+  }
+  __syncthreads();
+  int jf = r;  // first failed pivot (r = none)
+  for (int j = 0; j < r; ++j) {
+    if (tid == 0) {
+      float ajj = U[j * ld + j];
+      for (int k = 0; k < j; ++k) ajj -= U[k * ld + j] * U[k * ld + j];
+      bc[0] = ajj;
+    }
+    __syncthreads();
+    const float ajj = bc[0];
+    if (!(ajj > 0.f)) {  // uniform across the block
+      jf = j;
+      break;
+    }
+    const float ujj = sqrtf(ajj);
+    const float inv = 1.f / ujj;
+    for (int c = j + 1 + tid; c < r; c += nt) {
+      float v = U[j * ld + c];
+      for (int k = 0; k < j; ++k) v -= U[k * ld + j] * U[k * ld + c];
+      U[j * ld + c] = v * inv;
+    }
+    __syncthreads();
+    if (tid == 0) U[j * ld + j] = ujj;
+    __syncthreads();
+  }
+  float* O = U_out + static_cast<long>(b) * r * r;
+  for (int idx = tid; idx < r * r; idx += nt) {
+    const int i = idx / r, c = idx - i * r;
+    float v = 0.f;
+    if (i < jf) v = (i <= c) ? U[i * ld + c] : 0.f;
+    else if (i == c) v = __builtin_nanf("");
+    O[idx] = v;
+  }
+}
+
+// ============================================================================
+// Inverse of an upper-triangular r x r matrix, one block per matrix.  The
+// reference applies U^-1 by a triangular solve (solve_triangular, ortho.py:105-121);
+// here U^-1 is formed once in fp64 (row-oriented back substitution, one thread
+// per column) and rounded to fp32, so that P U^-1 becomes an MFMA row
+// projection instead of an m_P-long serial solve.  A zero or NaN pivot gives
+// inf/NaN entries exactly as the solve would.
+// ============================================================================
+template <typename XT>
+__global__ void __launch_bounds__(256) triinv_kernel(const float* __restrict__ U_in, float* __restrict__ X_out,
+                                                     int r) {
+  extern __shared__ __attribute__((aligned(16))) char tri_sm[];
+  float* U = reinterpret_cast<float*>(tri_sm);                  // r x r
+  XT* X = reinterpret_cast<XT*>(tri_sm + sizeof(float) * ((r * r + 3) / 4 * 4));  // r x r
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const float* Ub = U_in + static_cast<long>(b) * r * r;
+  for (int idx = tid; idx < r * r; idx += nt) {
+    U[idx] = Ub[idx];
+    X[idx] = XT(0);
+  }
+  __syncthreads();
+  for (int i = r - 1; i >= 0; --i) {
+    const double uii = static_cast<double>(U[i * r + i]);
+    for (int c = i + tid; c < r; c += nt) {
+      double acc = (c == i) ? 1.0 : 0.0;
+      for (int k = i + 1; k <= c; ++k) acc -= static_cast<double>(U[i * r + k]) * static_cast<double>(X[k * r + c]);
+      X[i * r + c] = static_cast<XT>(acc / uii);
+    }
+    __syncthreads();
+  }
+  float* Xo = X_out + static_cast<long>(b) * r * r;
+  for (int idx = tid; idx < r * r; idx += nt) Xo[idx] = static_cast<float>(X[idx]);
+}
+
+// ============================================================================
+// Fix-up + column normalisation + Q commit, one block per matrix.
+//   R <- z ? nan_to_num(Q) : nan_to_num(R);  Q <- R / (sqrt(sum_rows R^2) + eps)
+// Threads are grouped per column (tpc threads per column, fixed-order tree
+// reduction), so the column sums are deterministic.
+// ============================================================================
+struct FixArgs {
+  float* q[MAXB];
+  float* R;           // (batch, nq, r)
+  const uint32_t* nonzero;
+  int nq, r, tpc;
+  float eps;
+};
+
+__global__ void __launch_bounds__(256) fixup_colnorm_kernel(const FixArgs a) {
+  __shared__ float part[256];
+  __shared__ float denom[256];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int r = a.r, nq = a.nq, tpc = a.tpc;
+  const bool zero = (a.nonzero[b] == 0u);
+  float* R = a.R + static_cast<long>(b) * nq * r;
+  float* Q = a.q[b];
+  const int c = tid % r;
+  const int p = tid / r;
+  const bool active = (p < tpc);
+  float ss = 0.f;
+  if (active) {
+    for (int row = p; row < nq; row += tpc) {
+      const long idx = static_cast<long>(row) * r + c;
+      const float v = zero ? nan_to_num(Q[idx]) : nan_to_num(R[idx]);
+      R[idx] = v;
+      ss += v * v;
+    }
+  }
+  part[tid] = ss;
+  __syncthreads();
+  if (tid < r) {
+    float s = 0.f;
+    for (int k = 0; k < tpc; ++k) s += part[k * r + tid];
+    denom[tid] = sqrtf(s) + a.eps;
+  }
+  __syncthreads();
+  if (active) {
+    const float d = denom[c];
+    for (int row = p; row < nq; row += tpc) {
+      const long idx = static_cast<long>(row) * r + c;
+      Q[idx] = R[idx] / d;
+    }
+  }
+}
+
+// P <- z ? 0 : nan_to_num(P) for the real entries (kernels.py:185-188)
+__global__ void __launch_bounds__(256) pfix_kernel(float* __restrict__ P, const uint32_t* __restrict__ nonzero,
+                                                   long per_entry, int batch) {
+  const long total = per_entry * batch;
+  for (long idx = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
+       idx += static_cast<long>(gridDim.x) * blockDim.x) {
+    const long b = idx / per_entry;
+    P[idx] = (nonzero[b] == 0u) ? 0.f : nan_to_num(P[idx]);
+  }
+}
+
+// ============================================================================
+// Error feedback + weight update on the m x n storage of every matrix:
+//   M[i][j] += sum_c (ra_m[i][c]) (ca_m[j][c])      (scales folded into the R / Qn side)
+//   W[i][j]  = d W[i][j] + sum_c (ra_w[i][c]) (ca_w[j][c])
+// MFMA 32x32x2 f32 with K = r split over the two lane halves (c = h*RH + s):
+// A operand lane l = rowF[i0 + (l&31)][h*RH + s], B operand = colF[j0 + (l&31)][h*RH + s];
+// the accumulator tile is loaded from / stored to M and W directly (each
+// register = two 128-byte row segments per wave).  Block = 4 waves = 64 x 128.
+// ============================================================================
+struct EfArgs {
+  float* m[MAXB];
+  float* w[MAXB];
+  const float* qn[MAXB];
+  const float* P;     // (batch, m_P, r)
+  const float* R;     // (batch, n_Q, r)
+  const uint32_t* nonzero;
+  int rows, cols, r, transposed;
+  long ld_m, ld_w;
+  float alpha;        // -(1 - mu)
+  float beta;         // -scaled_lr
+  float decay;        // 1 - lr*wd (or 1)
+  int has_w;
+};
+
+template <int RH>
+__device__ __forceinline__ void load_factor(const float* __restrict__ F, int idx, int nrows, int r, int h,
+                                            float scale, float (&v)[RH]) {
+  const int c0 = h * RH;
+  if (idx < nrows) {
+    const float* p = F + static_cast<long>(idx) * r + c0;
+    if ((r % 4) == 0 && c0 + RH <= r) {
+#pragma unroll
+      for (int s = 0; s < RH; s += 4) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(p + s);
+        v[s] = x[0] * scale;
+        v[s + 1] = x[1] * scale;
+        v[s + 2] = x[2] * scale;
+        v[s + 3] = x[3] * scale;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < RH; ++s) v[s] = (c0 + s < r) ? p[s] * scale : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < RH; ++s) v[s] = 0.f;
+  }
+}
+
+template <int RH>
+__global__ void __launch_bounds__(256) ef_update_kernel(const EfArgs a) {
+  const int b = blockIdx.z;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int t = lane & 31;
+  const int h = lane >> 5;
+  const int i0 = blockIdx.y * 64 + (wave >> 1) * 32;
+  const int j0 = blockIdx.x * 128 + (wave & 1) * 64;
+  const int rows = a.rows, cols = a.cols, r = a.r;
+  const bool zero = (a.nonzero[b] == 0u);
+  const int m_p = a.transposed ? cols : rows;
+  const int n_q = a.transposed ? rows : cols;
+  const float* Pb = a.P + static_cast<long>(b) * m_p * r;
+  const float* Rb = a.R + static_cast<long>(b) * n_q * r;
+  const float* Qb = a.qn[b];
+  // row factor (indexed by i) and column factor (indexed by j) of each update
+  const float* rowF_m = a.transposed ? Rb : Pb;
+  const float* colF_m = a.transposed ? Pb : Rb;
+  const float* rowF_w = a.transposed ? Qb : Pb;
+  const float* colF_w = a.transposed ? Pb : Qb;
+  const float rs_m = a.transposed ? a.alpha : 1.f, cs_m = a.transposed ? 1.f : a.alpha;
+  const float rs_w = a.transposed ? a.beta : 1.f, cs_w = a.transposed ? 1.f : a.beta;
+
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 0 && zero) continue;          // z: momentum is all zero and stays so
+    if (pass == 1 && !a.has_w) break;
+    float* X = (pass == 0) ? a.m[b] : a.w[b];
+    const long ld = (pass == 0) ? a.ld_m : a.ld_w;
+    float ra[RH];
+    load_factor<RH>(pass == 0 ? rowF_m : rowF_w, i0 + t, rows, r, h, pass == 0 ? rs_m : rs_w, ra);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int jc = j0 + 32 * cb + t;
+      float ca[RH];
+      load_factor<RH>(pass == 0 ? colF_m : colF_w, jc, cols, r, h, pass == 0 ? cs_m : cs_w, ca);
+      f32x16 acc;
+      const float dscale = (pass == 0) ? 1.f : a.decay;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        acc[q] = (i < rows && jc < cols) ? X[static_cast<long>(i) * ld + jc] * dscale : 0.f;
+      }
+      if (!(pass == 1 && zero)) {
+#pragma unroll
+        for (int s = 0; s < RH; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[s], ca[s], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (i < rows && jc < cols) X[static_cast<long>(i) * ld + jc] = acc[q];
+      }
+    }
+  }
+}
+
+// ============================================================================
+// host side
+// ============================================================================
+namespace {
+
+int rblocks16(int r) { return (r + 15) / 16; }
+
+int round_up(long v, long m) { return static_cast<int>((v + m - 1) / m * m); }
+
+long ceil_div(long a, long b) { return (a + b - 1) / b; }
+
+int validate(const DionBatchDesc* d) {
+  if (d == nullptr) return fail(DION_E_INVALID, "desc is null");
+  if (d->batch < 0) return fail(DION_E_INVALID, "batch=%d", d->batch);
+  if (d->m <= 0 || d->n <= 0) return fail(DION_E_INVALID, "bad shape m=%d n=%d", d->m, d->n);
+  if (d->r <= 0 || d->r > 128)
+    return fail(DION_E_UNSUPPORTED, "rank r=%d outside 1..128", d->r);
+  if (d->r > d->m || d->r > d->n)
+    return fail(DION_E_INVALID, "rank r=%d exceeds min(m=%d, n=%d)", d->r, d->m, d->n);
+  if (d->m_dtype != DION_DTYPE_F32) return fail(DION_E_UNSUPPORTED, "momentum dtype %d", d->m_dtype);
+  if (d->w_dtype != DION_DTYPE_F32) return fail(DION_E_UNSUPPORTED, "weight dtype %d", d->w_dtype);
+  if (d->g_dtype != DION_DTYPE_NONE && d->g_dtype != DION_DTYPE_F32 && d->g_dtype != DION_DTYPE_BF16)
+    return fail(DION_E_UNSUPPORTED, "grad dtype %d", d->g_dtype);
+  if (d->transposed != 0 && d->transposed != 1) return fail(DION_E_INVALID, "transposed=%d", d->transposed);
+  return DION_OK;
+}
+
+long ldv(long ld, int n) { return ld == 0 ? n : ld; }
+
+// split-K geometry of one projection; identical in workspace sizing and launch
+struct Geo {
+  int gx, nchunk, kchunk, out_rows;
+};
+
+constexpr int kTargetBlocks = 2048;
+
+// row projection: X rows x cols, reduce over cols
+Geo rowproj_geo(int rows, int cols, int batch) {
+  Geo g;
+  g.gx = static_cast<int>(ceil_div(rows, 128));
+  long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
+  long maxc = ceil_div(cols, 256);
+  long nc = want < maxc ? want : maxc;
+  if (nc < 1) nc = 1;
+  g.kchunk = round_up(ceil_div(cols, nc), 32);
+  g.nchunk = static_cast<int>(ceil_div(cols, g.kchunk));
+  g.out_rows = rows;
+  return g;
+}
+
+// column projection: X rows x cols, reduce over rows
+Geo colproj_geo(int rows, int cols, int batch, bool panel) {
+  Geo g;
+  g.gx = static_cast<int>(ceil_div(cols, panel ? 64 : 256));
+  long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
+  long maxc = ceil_div(rows, panel ? 512 : 256);
+  long nc = want < maxc ? want : maxc;
+  if (nc < 1) nc = 1;
+  g.kchunk = round_up(ceil_div(rows, nc), 16);
+  g.nchunk = static_cast<int>(ceil_div(rows, g.kchunk));
+  g.out_rows = cols;
+  return g;
+}
+
+size_t slab_bytes(const Geo& g, int batch, int r) {
+  return g.nchunk > 1 ? sizeof(float) * static_cast<size_t>(batch) * g.nchunk * g.out_rows * r : 0;
+}
+
+int sketch_k(int r, float oversample) {
+  return static_cast<int>(ceil(static_cast<double>(oversample) * r / 128.0)) * 128;
+}
+
+struct OrthoPlan {
+  bool plain_qr;
+  int k;
+  Geo sk, gr;
+  size_t off_sk_slab, off_sp, off_r1, off_gslab, off_g, off_r2, off_inv, off_p1, total;
+};
+
+OrthoPlan ortho_plan(int mp, int r, int batch, float oversample) {
+  OrthoPlan p{};
+  p.plain_qr = (mp <= r);
+  p.k = sketch_k(r, oversample);
+  if (p.plain_qr) return p;
+  p.sk = colproj_geo(mp, p.k, batch, true);
+  p.gr = colproj_geo(mp, r, batch, true);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) / 256 * 256;
+    return o;
+  };
+  p.off_sk_slab = take(slab_bytes(p.sk, batch, r));
+  p.off_sp = take(sizeof(float) * static_cast<size_t>(batch) * p.k * r);
+  p.off_r1 = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
+  p.off_gslab = take(slab_bytes(p.gr, batch, r));
+  p.off_g = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
+  p.off_r2 = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
+  p.off_inv = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
+  p.off_p1 = take(sizeof(float) * static_cast<size_t>(batch) * mp * r);
+  p.total = off;
+  return p;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template <class F>
+int dispatch_rb(int r, F&& f) {
+  switch (rblocks16(r)) {
+    case 1: return f(std::integral_constant<int, 1>{});
+    case 2: return f(std::integral_constant<int, 2>{});
+    case 3:
+    case 4: return f(std::integral_constant<int, 4>{});
+    case 5: case 6: case 7: case 8: return f(std::integral_constant<int, 8>{});
+  }
+  return fail(DION_E_UNSUPPORTED, "rank %d", r);
+}
+
+template <class F>
+int dispatch_gdt(int gdt, F&& f) {
+  switch (gdt) {
+    case DION_DTYPE_NONE: return f(std::integral_constant<int, DION_DTYPE_NONE>{});
+    case DION_DTYPE_F32: return f(std::integral_constant<int, DION_DTYPE_F32>{});
+    case DION_DTYPE_BF16: return f(std::integral_constant<int, DION_DTYPE_BF16>{});
+  }
+  return fail(DION_E_UNSUPPORTED, "grad dtype %d", gdt);
+}
+
+int launch_reduce(float* out, const float* slab, int nchunk, long per_entry, int batch, hipStream_t st) {
+  long total = per_entry * batch;
+  long blocks = ceil_div(total, 256);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, out, slab,
+                     nchunk, per_entry, batch);
+  return check_launch("reduce_slabs");
+}
+
+// One projection over up to MAXB matrices.  `row_mode`: reduce over columns.
+int run_projection(bool row_mode, int rows, int cols, int r, int batch, const void* const* G, float* const* M,
+                   const float* const* thin, long ld_m, long ld_g, int gdt, float* out, uint32_t* nonzero,
+                   void* ws, size_t ws_bytes, hipStream_t st) {
+  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch) : colproj_geo(rows, cols, batch, false);
+  const size_t need = slab_bytes(geo, batch, r);
+  if (need > ws_bytes || (need > 0 && ws == nullptr))
+    return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
+  ProjArgs a;
+  memset(&a, 0, sizeof(a));
+  bool vec = (ld_m % 4) == 0 && (gdt == DION_DTYPE_NONE || (ld_g % (gdt == DION_DTYPE_BF16 ? 8 : 4)) == 0);
+  for (int b = 0; b < batch; ++b) {
+    a.g[b] = G ? G[b] : nullptr;
+    a.m[b] = M[b];
+    a.thin[b] = thin[b];
+    if (M[b] == nullptr || thin[b] == nullptr || (gdt != DION_DTYPE_NONE && G[b] == nullptr))
+      return fail(DION_E_INVALID, "null matrix pointer at entry %d", b);
+    vec = vec && aligned16(M[b]) && (gdt == DION_DTYPE_NONE || aligned16(G[b]));
+  }
+  a.out = geo.nchunk > 1 ? static_cast<float*>(ws) : out;
+  a.nonzero = nonzero;
+  a.rows = rows;
+  a.cols = cols;
+  a.r = r;
+  a.ld_m = ld_m;
+  a.ld_g = ld_g;
+  a.kchunk = geo.kchunk;
+  a.nchunk = geo.nchunk;
+  a.out_rows = geo.out_rows;
+  a.vec = vec ? 1 : 0;
+  const dim3 grid(geo.gx, geo.nchunk, batch);
+  int rc = dispatch_rb(r, [&](auto RBc) {
+    constexpr int RB = decltype(RBc)::value;
+    return dispatch_gdt(gdt, [&](auto Gc) {
+      constexpr int GD = decltype(Gc)::value;
+      if (row_mode)
+        hipLaunchKernelGGL((rowproj_kernel<RB, GD>), grid, dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((colproj_kernel<RB, GD, 0, 0>), grid, dim3(256), 0, st, a);
+      return check_launch(row_mode ? "rowproj" : "colproj");
+    });
+  });
+  if (rc != DION_OK) return rc;
+  if (geo.nchunk > 1)
+    return launch_reduce(out, static_cast<const float*>(ws), geo.nchunk, static_cast<long>(geo.out_rows) * r, batch, st);
+  return DION_OK;
+}
+
+// panel reduction over the rows of P: out[b] (cols x r) = X_b^T P_b
+int run_panel(int xmode, int mp, int cols, int r, int batch, const float* P, const float* sketch, uint64_t seed,
+              float std_, float* out, void* slab, const Geo& geo, hipStream_t st) {
+  ProjArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int b = 0; b < batch; ++b) {
+    a.thin[b] = P + static_cast<long>(b) * mp * r;
+    a.m[b] = const_cast<float*>(P + static_cast<long>(b) * mp * r);
+  }
+  a.out = geo.nchunk > 1 ? static_cast<float*>(slab) : out;
+  a.sketch = sketch;
+  a.seed = seed;
+  a.sketch_std = std_;
+  a.rows = mp;
+  a.cols = cols;
+  a.r = r;
+  a.ld_m = r;
+  a.ld_g = 0;
+  a.kchunk = geo.kchunk;
+  a.nchunk = geo.nchunk;
+  a.out_rows = geo.out_rows;
+  a.vec = ((r % 4) == 0 && aligned16(P)) ? 1 : 0;
+  const dim3 grid(geo.gx, geo.nchunk, batch);
+  int rc = dispatch_rb(r, [&](auto RBc) {
+    constexpr int RB = decltype(RBc)::value;
+    if (xmode == 0)
+      hipLaunchKernelGGL((colproj_kernel<RB, DION_DTYPE_NONE, 0, 1>), grid, dim3(256), 0, st, a);
+    else if (xmode == 1)
+      hipLaunchKernelGGL((colproj_kernel<RB, DION_DTYPE_NONE, 1, 1>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((colproj_kernel<RB, DION_DTYPE_NONE, 2, 1>), grid, dim3(256), 0, st, a);
+    return check_launch("panel colproj");
+  });
+  if (rc != DION_OK) return rc;
+  if (geo.nchunk > 1)
+    return launch_reduce(out, static_cast<const float*>(slab), geo.nchunk, static_cast<long>(cols) * r, batch, st);
+  return DION_OK;
+}
+
+int launch_triinv(const float* U, float* Uinv, int r, int batch, hipStream_t st) {
+  const size_t ubytes = sizeof(float) * static_cast<size_t>((r * r + 3) / 4 * 4);
+  if (r <= 96) {
+    hipLaunchKernelGGL((triinv_kernel<double>), dim3(batch), dim3(256), ubytes + sizeof(double) * r * r, st, U, Uinv, r);
+  } else {
+    hipLaunchKernelGGL((triinv_kernel<float>), dim3(batch), dim3(256), ubytes + sizeof(float) * r * r, st, U, Uinv, r);
+  }
+  return check_launch("triinv");
+}
+
+// dst_b = src_b Uinv_b for every matrix (m_P x r times r x r), an MFMA row projection
+int apply_right(const float* src, float* dst, const float* Uinv, int mp, int r, int batch, hipStream_t st) {
+  const Geo geo = rowproj_geo(mp, r, batch);
+  if (geo.nchunk != 1) return fail(DION_E_INVALID, "internal: right-apply split");
+  ProjArgs a;
+  memset(&a, 0, sizeof(a));
+  bool vec = (r % 4) == 0;
+  for (int b = 0; b < batch; ++b) {
+    a.m[b] = const_cast<float*>(src + static_cast<long>(b) * mp * r);
+    a.thin[b] = Uinv + static_cast<long>(b) * r * r;
+    vec = vec && aligned16(a.m[b]);
+  }
+  a.out = dst;
+  a.rows = mp;
+  a.cols = r;
+  a.r = r;
+  a.ld_m = r;
+  a.kchunk = geo.kchunk;
+  a.nchunk = 1;
+  a.out_rows = mp;
+  a.vec = vec ? 1 : 0;
+  const dim3 grid(geo.gx, 1, batch);
+  return dispatch_rb(r, [&](auto RBc) {
+    constexpr int RB = decltype(RBc)::value;
+    hipLaunchKernelGGL((rowproj_kernel<RB, DION_DTYPE_NONE>), grid, dim3(256), 0, st, a);
+    return check_launch("apply_right");
+  });
+}
+
+size_t qr_lds_bytes(int K, int r) { return sizeof(float) * (static_cast<size_t>(r) * (K + 1) + r + 3 + 8 + 4); }
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int dion_abi_version(void) { return DION_ABI_VERSION; }
+
+const char* dion_last_error(void) { return g_err; }
+
+int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
+  int rc = validate(d);
+  if (rc != DION_OK) return rc;
+  if (bytes == nullptr) return fail(DION_E_INVALID, "bytes is null");
+  const int mp = d->transposed ? d->n : d->m;
+  const int nq = d->transposed ? d->m : d->n;
+  size_t need = 0;
+  const int chunks[2] = {d->batch < MAXB ? d->batch : MAXB, d->batch % MAXB};
+  for (int ci = 0; ci < 2; ++ci) {
+    const int chunk = chunks[ci];
+    if (chunk <= 0) continue;
+    size_t n = 0;
+    switch (op) {
+      case DION_OP_PROJECT_P: {
+        Geo g = d->transposed ? colproj_geo(d->m, d->n, chunk, false) : rowproj_geo(d->m, d->n, chunk);
+        n = slab_bytes(g, chunk, d->r);
+        break;
+      }
+      case DION_OP_PROJECT_R: {
+        Geo g = d->transposed ? rowproj_geo(d->m, d->n, chunk) : colproj_geo(d->m, d->n, chunk, false);
+        n = slab_bytes(g, chunk, d->r);
+        break;
+      }
+      case DION_OP_ORTHONORMALIZE: {
+        // k = ceil(oversample r / 128) * 128 is bounded by the value at oversample 2
+        n = ortho_plan(mp, d->r, chunk, 2.0f).total;
+        break;
+      }
+      default:
+        return fail(DION_E_INVALID, "unknown op %d", op);
+    }
+    if (n > need) need = n;
+  }
+  (void)nq;
+  *bytes = need;
+  return DION_OK;
+}
+
+int dion_project_p(const DionBatchDesc* d, const void* const* G, float* const* M, const float* const* Q, float* P,
+                   uint32_t* nonzero, void* ws, size_t ws_bytes, dion_stream_t stream) {
+  int rc = validate(d);
+  if (rc != DION_OK) return rc;
+  if (M == nullptr || Q == nullptr || P == nullptr) return fail(DION_E_INVALID, "null argument");
+  if (d->g_dtype != DION_DTYPE_NONE && G == nullptr) return fail(DION_E_INVALID, "G is null");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int mp = d->transposed ? d->n : d->m;
+  const long ld_m = ldv(d->ld_m, d->n), ld_g = ldv(d->ld_g, d->n);
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    rc = run_projection(!d->transposed, d->m, d->n, d->r, nb, G ? G + b0 : nullptr, M + b0, Q + b0, ld_m, ld_g,
+                        d->g_dtype, P + static_cast<long>(b0) * mp * d->r, nonzero ? nonzero + b0 : nullptr, ws,
+                        ws_bytes, st);
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_project_r(const DionBatchDesc* d, const float* const* M, const float* P, float* R, void* ws,
+                   size_t ws_bytes, dion_stream_t stream) {
+  int rc = validate(d);
+  if (rc != DION_OK) return rc;
+  if (M == nullptr || P == nullptr || R == nullptr) return fail(DION_E_INVALID, "null argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int mp = d->transposed ? d->n : d->m;
+  const int nq = d->transposed ? d->m : d->n;
+  const long ld_m = ldv(d->ld_m, d->n);
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    const float* thin[MAXB];
+    for (int b = 0; b < nb; ++b) thin[b] = P + static_cast<long>(b0 + b) * mp * d->r;
+    rc = run_projection(d->transposed != 0, d->m, d->n, d->r, nb, nullptr, const_cast<float* const*>(M + b0), thin,
+                        ld_m, 0, DION_DTYPE_NONE, R + static_cast<long>(b0) * nq * d->r, nullptr, ws, ws_bytes, st);
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, uint64_t seed, float oversample,
+                        void* ws, size_t ws_bytes, dion_stream_t stream) {
+  int rc = validate(d);
+  if (rc != DION_OK) return rc;
+  if (P == nullptr) return fail(DION_E_INVALID, "P is null");
+  if (!(oversample > 0.f)) return fail(DION_E_INVALID, "oversample=%f", oversample);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int mp = d->transposed ? d->n : d->m;
+  const int r = d->r;
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    float* Pb = P + static_cast<long>(b0) * mp * r;
+    const OrthoPlan plan = ortho_plan(mp, r, nb, oversample);
+    if (plan.plain_qr) {
+      const size_t lds = qr_lds_bytes(mp, r);
+      if (lds > 160 * 1024) return fail(DION_E_UNSUPPORTED, "plain QR of %dx%d does not fit LDS", mp, r);
+      hipLaunchKernelGGL(householder_qr_kernel, dim3(nb), dim3(256), lds, st, Pb, nullptr, Pb, mp, r, 1);
+      rc = check_launch("householder_qr(Q)");
+      if (rc != DION_OK) return rc;
+      continue;
+    }
+    if (plan.total > ws_bytes || ws == nullptr)
+      return fail(DION_E_WORKSPACE, "orthonormalize needs %zu workspace bytes, got %zu", plan.total, ws_bytes);
+    char* base = static_cast<char*>(ws);
+    float* sk_slab = reinterpret_cast<float*>(base + plan.off_sk_slab);
+    float* sp = reinterpret_cast<float*>(base + plan.off_sp);
+    float* r1 = reinterpret_cast<float*>(base + plan.off_r1);
+    float* gslab = reinterpret_cast<float*>(base + plan.off_gslab);
+    float* gm = reinterpret_cast<float*>(base + plan.off_g);
+    float* r2 = reinterpret_cast<float*>(base + plan.off_r2);
+    const int K = plan.k;
+    const size_t lds = qr_lds_bytes(K, r);
+    if (lds > 160 * 1024) return fail(DION_E_UNSUPPORTED, "sketch QR of %dx%d does not fit LDS", K, r);
+    // (1) S P  (K x r)
+    const float std_ = sqrtf(1.0f / static_cast<float>(K));
+    rc = run_panel(sketch ? 1 : 2, mp, K, r, nb, Pb, sketch ? sketch + static_cast<long>(b0) * K * mp : nullptr,
+                   seed + 0x9E3779B97F4A7C15ull * static_cast<uint64_t>(b0), std_, sp, sk_slab, plan.sk, st);
+    if (rc != DION_OK) return rc;
+    // (2) R1 = qr(S P).R
+    hipLaunchKernelGGL(householder_qr_kernel, dim3(nb), dim3(256), lds, st, sp, r1, nullptr, K, r, 0);
+    rc = check_launch("householder_qr(R)");
+    if (rc != DION_OK) return rc;
+    float* uinv = reinterpret_cast<float*>(base + plan.off_inv);
+    float* p1 = reinterpret_cast<float*>(base + plan.off_p1);
+    // (3) P1 = P R1^-1  (into workspace)
+    rc = launch_triinv(r1, uinv, r, nb, st);
+    if (rc != DION_OK) return rc;
+    rc = apply_right(Pb, p1, uinv, mp, r, nb, st);
+    if (rc != DION_OK) return rc;
+    // (4) Gram = P1^T P1, (5) R2 = chol_upper(Gram)
+    rc = run_panel(0, mp, r, r, nb, p1, nullptr, 0, 0.f, gm, gslab, plan.gr, st);
+    if (rc != DION_OK) return rc;
+    hipLaunchKernelGGL(cholesky_kernel, dim3(nb), dim3(256), sizeof(float) * (r * (r + 1) + 4), st, gm, r2, r);
+    rc = check_launch("cholesky");
+    if (rc != DION_OK) return rc;
+    // (6) P = P1 R2^-1  (back into the caller's buffer)
+    rc = launch_triinv(r2, uinv, r, nb, st);
+    if (rc != DION_OK) return rc;
+    rc = apply_right(p1, Pb, uinv, mp, r, nb, st);
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_fixup_colnorm(const DionBatchDesc* d, float* P, float* R, float* const* Q, const uint32_t* nonzero,
+                       float eps, dion_stream_t stream) {
+  int rc = validate(d);
+  if (rc != DION_OK) return rc;
+  if (P == nullptr || R == nullptr || Q == nullptr || nonzero == nullptr)
+    return fail(DION_E_INVALID, "null argument");
+  if (d->batch == 0) return DION_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int mp = d->transposed ? d->n : d->m;
+  const int nq = d->transposed ? d->m : d->n;
+  const int r = d->r;
+  {
+    const long per = static_cast<long>(mp) * r;
+    long blocks = ceil_div(per * d->batch, 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(pfix_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, P, nonzero, per, d->batch);
+    rc = check_launch("pfix");
+    if (rc != DION_OK) return rc;
+  }
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    FixArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int b = 0; b < nb; ++b) {
+      if (Q[b0 + b] == nullptr) return fail(DION_E_INVALID, "null Q at %d", b0 + b);
+      a.q[b] = Q[b0 + b];
+    }
+    a.R = R + static_cast<long>(b0) * nq * r;
+    a.nonzero = nonzero + b0;
+    a.nq = nq;
+    a.r = r;
+    a.tpc = 256 / r;
+    a.eps = eps;
+    hipLaunchKernelGGL(fixup_colnorm_kernel, dim3(nb), dim3(256), 0, st, a);
+    rc = check_launch("fixup_colnorm");
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, const float* P, const float* R,
+                  const float* const* Qn, const uint32_t* nonzero, float mu, float lr, float wd, float scaled_lr,
+                  dion_stream_t stream) {
+  int rc = validate(d);
+  if (rc != DION_OK) return rc;
+  if (M == nullptr || P == nullptr || R == nullptr || Qn == nullptr || nonzero == nullptr)
+    return fail(DION_E_INVALID, "null argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int mp = d->transposed ? d->n : d->m;
+  const int nq = d->transposed ? d->m : d->n;
+  const int r = d->r;
+  const int rpad = (r + 1) / 2 * 2;
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    EfArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int b = 0; b < nb; ++b) {
+      a.m[b] = M[b0 + b];
+      a.w[b] = W ? W[b0 + b] : nullptr;
+      a.qn[b] = Qn[b0 + b];
+      if (a.m[b] == nullptr || a.qn[b] == nullptr || (W && a.w[b] == nullptr))
+        return fail(DION_E_INVALID, "null pointer at entry %d", b0 + b);
+    }
+    a.P = P + static_cast<long>(b0) * mp * r;
+    a.R = R + static_cast<long>(b0) * nq * r;
+    a.nonzero = nonzero + b0;
+    a.rows = d->m;
+    a.cols = d->n;
+    a.r = r;
+    a.transposed = d->transposed;
+    a.ld_m = ldv(d->ld_m, d->n);
+    a.ld_w = ldv(d->ld_w, d->n);
+    a.alpha = -(1.0f - mu);
+    a.beta = -scaled_lr;
+    a.decay = (wd > 0.f) ? (1.0f - lr * wd) : 1.0f;
+    a.has_w = W ? 1 : 0;
+    const dim3 grid(static_cast<unsigned>(ceil_div(d->n, 128)), static_cast<unsigned>(ceil_div(d->m, 64)), nb);
+    const int rh = rpad / 2;
+    if (rh <= 4)
+      hipLaunchKernelGGL((ef_update_kernel<4>), grid, dim3(256), 0, st, a);
+    else if (rh <= 8)
+      hipLaunchKernelGGL((ef_update_kernel<8>), grid, dim3(256), 0, st, a);
+    else if (rh <= 16)
+      hipLaunchKernelGGL((ef_update_kernel<16>), grid, dim3(256), 0, st, a);
+    else if (rh <= 32)
+      hipLaunchKernelGGL((ef_update_kernel<32>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((ef_update_kernel<64>), grid, dim3(256), 0, st, a);
+    rc = check_launch("ef_update");
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,166 @@
+"""`MegatronDion`: the optimizer Megatron's DistributedOptimizer selects, MI355X edition.
+
+Mirrors /root/reference/megatron/core/optimizer/dion/algorithm.py:29-221:
+same constructor keywords and `defaults` keys (:48-105), the same
+`enable_distributed_mode(route_step_params=...)` hook (runtime.py:632-644) and
+the same `step()` contract (:149-221): bump `param_group['step']` and
+`_step_count`, ask the adapter for `(List[DionBatch], List[ElementwiseStepParam])`,
+run the batches through a width-limited AsyncRuntime.  The per-batch work runs
+in HIP kernels (`codec=` backend, default `HipDionCodec`); there is no CPU
+fallback.
+
+Out of scope on this path: the elementwise AdamW/Lion branch for
+non-2D parameters, TP/FS-sharded Dion and split-qkv children.
+"""
+from __future__ import annotations
+
+import os
+import time
+from collections import OrderedDict
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+from torch.optim.optimizer import Optimizer
+
+from .batches import build_dion_batches
+from .runtime import AsyncRuntime, coalesce_local_batches, run_dion_batch_async
+from .state import init_dion_state
+from .types import DionDistMeta, DionMixedPrecisionConfig, DionStepParam
+
+
+class MegatronDion(Optimizer):
+    def __init__(self, params, lr: float = 0.01, mu: float = 0.95, weight_decay: float = 0.01,
+                 rank_fraction: float = 1.0, rank_multiple_of: int = 1, epsilon: float = 1e-8,
+                 rcqr_oversample: float = 1.25, betas: tuple = (0.9, 0.95), elementwise_eps: float = 1e-8,
+                 rp_average_in_collective: bool = True, use_fs_collectives: bool = True,
+                 mixed_precision_config: Optional[DionMixedPrecisionConfig] = None, enable_async: bool = True,
+                 use_low_rank_sync: bool = True, elementwise_optimizer: str = "adam",
+                 elementwise_lr_scale: float = 1.0, scale_mode: str = "spectral",
+                 extra_scale_factor: float = 0.2, split_qkv: bool = False, split_linear: bool = False,
+                 max_concurrent_tasks: Optional[int] = None, *, codec=None, sketch_seed: int = 0,
+                 coalesce_local: bool = True):
+        if isinstance(params, (list, tuple)):
+            for pg in params:
+                if isinstance(pg, dict) and "wd_mult" in pg:
+                    pg["weight_decay"] = float(pg.get("weight_decay", weight_decay)) * float(pg.get("wd_mult", 1.0))
+        if scale_mode not in ("spectral", "unit_rms_norm", "shape_scaling"):
+            raise RuntimeError(f"[DION_INVALID_SCALE_MODE] got {scale_mode!r}")
+        if float(elementwise_lr_scale) < 0.0:
+            raise RuntimeError(f"[DION_INVALID_ELEMENTWISE_LR_SCALE] elementwise_lr_scale={elementwise_lr_scale}")
+        defaults = dict(lr=lr, mu=mu, weight_decay=weight_decay, rank_fraction=rank_fraction,
+                        rank_multiple_of=rank_multiple_of, epsilon=epsilon, rcqr_oversample=rcqr_oversample,
+                        betas=betas, elementwise_eps=elementwise_eps,
+                        rp_average_in_collective=rp_average_in_collective, use_fs_collectives=use_fs_collectives,
+                        enable_async=enable_async, use_low_rank_sync=use_low_rank_sync,
+                        elementwise_optimizer=elementwise_optimizer, elementwise_lr_scale=elementwise_lr_scale,
+                        scale_mode=scale_mode, extra_scale_factor=extra_scale_factor, split_qkv=bool(split_qkv),
+                        split_linear=bool(split_linear), algorithm="dion", step=0)
+        super().__init__(params, defaults)
+        self._global_rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        self.is_distributed_mode = False
+        self.use_fs_collectives = use_fs_collectives
+        self.use_low_rank_sync = use_low_rank_sync
+        self.enable_async = enable_async
+        self.max_concurrent_tasks = max_concurrent_tasks
+        self._mixed_precision_config = mixed_precision_config or DionMixedPrecisionConfig()
+        self._route_step_params = None
+        self._dion_update_count = 0
+        self._elementwise_update_count = 0
+        self._step_count = 0
+        self._sketch_seed = int(sketch_seed)
+        self._coalesce_local = bool(coalesce_local)
+        self._codec = codec
+        self._profile_records: List[Tuple[str, float]] = []
+
+    # ------------------------------------------------------------------ backend
+    @property
+    def codec(self):
+        if self._codec is None:
+            from .codec import HipDionCodec
+            self._codec = HipDionCodec()
+        return self._codec
+
+    # ------------------------------------------------------------------ plugin surface
+    def enable_distributed_mode(self, *, route_step_params=None) -> None:
+        """runtime.py:632-644: install the adapter's routing callback."""
+        if route_step_params is None:
+            raise RuntimeError(f"[DION_MISSING_DIST_STEP_ITEMS_CALLBACK] step={self._step_count}")
+        self.is_distributed_mode = True
+        self._route_step_params = route_step_params
+
+    def _tasks(self, sketches=None):
+        batches, elementwise = self._route_step_params()
+        if elementwise:
+            raise RuntimeError(
+                "[DION_ELEMENTWISE_UNSUPPORTED] the MI355X codec covers the 2D Dion path only; route "
+                "non-2D parameters to a separate optimizer")
+        self._dion_update_count += sum(int(b.real_batch_size) for b in batches)
+        if self._coalesce_local:
+            batches = coalesce_local_batches(batches)
+        for b in batches:
+            yield run_dion_batch_async(self, b, sketches=sketches(b) if sketches else None)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self._dion_update_count = 0
+        self._elementwise_update_count = 0
+        for group in self.param_groups:
+            group["step"] = group.get("step", 0) + 1
+        self._step_count += 1
+        if not self.is_distributed_mode:
+            raise RuntimeError(f"[DION_STEP_REQUIRES_DISTRIBUTED_MODE] step={self._step_count}")
+        profile = os.environ.get("DION_PROFILE_SPLIT", "").lower() in ("1", "true", "yes")
+        t0 = time.perf_counter() if profile else None
+        width = 3 if self.max_concurrent_tasks is None else int(self.max_concurrent_tasks)
+        AsyncRuntime(self._tasks(getattr(self, "_sketch_override", None)), width).run()
+        if profile:
+            torch.cuda.synchronize()
+            self._profile_records.append(("step", time.perf_counter() - t0))
+        return loss
+
+
+# ---------------------------------------------------------------------------- standalone routing
+def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str, torch.Tensor]],
+                      replicate_group=None, base_seed: int = 0) -> Dict[str, torch.Tensor]:
+    """Stand-alone adapter: state init + `route_step_params` for plain data parallelism.
+
+    Plays the part of the reference's DionDistributedOptimizer routing
+    (distrib_dion/bootstrap.py:519-606 -> batches.py:971 build_dion_batches) for
+    users outside Megatron and for the benchmark: params sorted by uid, one
+    batch per `batch_world_size` same-key matrices.  Each parameter's `.grad`
+    (bf16 or fp32) is the G of the step.
+    """
+    group = optimizer.param_groups[0]
+    rf = float(group.get("rank_fraction", optimizer.defaults["rank_fraction"]))
+    mult = int(optimizer.defaults.get("rank_multiple_of", 1))
+    metas = {}
+    for name, p in named_params:
+        state, cfg = init_dion_state(p, rank_fraction=rf, rank_multiple_of=mult, base_seed=base_seed,
+                                     param_uid=(name,), param_name=name,
+                                     use_low_rank_sync=optimizer.use_low_rank_sync)
+        optimizer.state[p].update(state)
+        metas[name] = (cfg, DionDistMeta(shape=tuple(p.shape), global_shape=tuple(p.shape), rank_fraction=rf,
+                                         is_transposed=cfg.is_transposed, param_uid=(name,), is_dion_param=True,
+                                         param_name=name, param_config=cfg))
+    ordered = sorted(named_params, key=lambda kv: kv[0])
+
+    def route():
+        steps = []
+        for name, p in ordered:
+            if p.grad is None:
+                continue
+            cfg, meta = metas[name]
+            steps.append(DionStepParam(param=p, grad=p.grad, optimizer_state=optimizer.state[p],
+                                       optim_group=group, config=cfg, dist_meta=meta))
+        batches = build_dion_batches(
+            dion_params=steps, get_replicate_group=lambda: replicate_group,
+            group_size=lambda g: dist.get_world_size(g))
+        return batches, []
+
+    optimizer.enable_distributed_mode(route_step_params=route)
+    return {name: p for name, p in named_params}

@@ -1,0 +1,258 @@
+"""Batch runtime of the Dion data-parallel step on MI355X.
+
+Device-side counterpart of /root/reference/megatron/core/optimizer/dion/runtime.py:
+  AsyncRuntime                 :140-171   (<= max_concurrent batch generators, round robin)
+  validate_update_contract     :196-291
+  batch_dion_update_async      :1499-1911 (the hot path; ddp low-rank branch :1379-1496)
+Each batch is a generator that enqueues HIP kernels (through the codec backend)
+on the current stream and yields right after launching an asynchronous RCCL
+collective (reduce-scatter of P, all-gather of P, all-reduce of R), so the
+next batch's kernels are enqueued while the collective runs -- the same
+overlap structure as the reference, with per-batch buffers (the reference's
+unscoped "replicated_p_ortho_full" buffer, runtime.py:1419-1424, lets
+concurrent same-shape batches read each other's P).
+"""
+from __future__ import annotations
+
+from typing import Callable, Generator, Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .codec import factor_rows
+from .kernels import scaled_lr_for_shape
+
+
+class AsyncRuntime:
+    """Round-robin driver of batch generators with bounded width."""
+
+    def __init__(self, tasks: Iterable[Generator], max_concurrent_tasks: int = 3):
+        if int(max_concurrent_tasks) <= 0:
+            raise ValueError(f"Invalid max_concurrent_tasks={max_concurrent_tasks}")
+        self.tasks = tasks
+        self.width = int(max_concurrent_tasks)
+
+    @staticmethod
+    def _advance(gen) -> bool:
+        try:
+            next(gen)
+            return True
+        except StopIteration:
+            return False
+
+    def run(self) -> None:
+        pending = iter(self.tasks)
+        more = True
+        live: List[Generator] = []
+        while more or live:
+            nxt: List[Generator] = []
+            if more and len(live) < self.width:
+                gen = next(pending, None)
+                if gen is None:
+                    more = False
+                elif self._advance(gen):
+                    nxt.append(gen)
+            for gen in live:
+                if self._advance(gen):
+                    nxt.append(gen)
+            live = nxt
+
+
+def _group_world(group) -> int:
+    if group is None:
+        return 1
+    return int(dist.get_world_size(group))
+
+
+def validate_update_contract(optimizer, *, optim_groups, optimizer_states, dist_metas, param_shapes,
+                             real_batch_size: int) -> None:
+    """All real entries of a batch must share shape, lr, rank_fraction, wd, mu and r."""
+    rows = []
+    for i in range(int(real_batch_size)):
+        st = optimizer_states[i] or {}
+        grp = optim_groups[i] or {}
+        meta = dist_metas[i]
+        gshape = st.get("per_expert_global_shape") or st.get("global_shape") \
+            or getattr(meta, "global_shape", None) or param_shapes[i]
+        wd_mult = float(grp.get("wd_mult", 1.0))
+        rows.append((
+            tuple(int(d) for d in gshape),
+            float(grp.get("lr", optimizer.defaults["lr"])),
+            float(grp.get("rank_fraction", optimizer.defaults.get("rank_fraction", 0.25))),
+            float(grp.get("weight_decay", optimizer.defaults["weight_decay"] * wd_mult)),
+            float(grp.get("mu", optimizer.defaults["mu"])),
+            int(st.get("r", -1)),
+        ))
+    bad = [i for i, row in enumerate(rows) if row != rows[0]]
+    if bad:
+        raise RuntimeError(
+            "[DION_BATCH_UPDATE_CONTRACT_MISMATCH] "
+            f"step={optimizer._step_count} expected={rows[0]} mismatched={[rows[i] for i in bad]}")
+
+
+def _sketch_seed(optimizer, batch_cache_key: int, entry: int) -> int:
+    """Per (step, matrix) sketch seed; the reference's sketch is unseeded (ortho.py:659-661)."""
+    base = int(getattr(optimizer, "_sketch_seed", 0))
+    return (base * 0x9E3779B97F4A7C15 + optimizer._step_count * 0xBF58476D1CE4E5B9
+            + (int(batch_cache_key) + entry) * 0x94D049BB133111EB) & ((1 << 64) - 1)
+
+
+def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_metas, optim_groups, grads=None,
+                            optimizer_states=None, param_shapes=None, real_batch_size=None,
+                            batch_cache_key: int = 0, batch_group=None, batch_collectives=None,
+                            commit_updates: Optional[List[Optional[Callable]]] = None,
+                            sketches: Optional[dict] = None) -> Generator[None, None, None]:
+    """One batch of same-shape matrices: project, exchange, orthonormalise, update.
+
+    `sketches` (tests only) maps an entry index to an explicit (k, m_P) sketch so
+    parity runs can reuse the sketch the reference drew.
+    """
+    codec = optimizer.codec
+    B = len(params)
+    real = B if real_batch_size is None else int(real_batch_size)
+    if batch_group is None:
+        raise RuntimeError(f"[DION_MISSING_BATCH_GROUPS] step={optimizer._step_count}")
+    if real <= 0:
+        return
+    param_shapes = list(param_shapes) if param_shapes else [tuple(p.shape) for p in params]
+    validate_update_contract(optimizer, optim_groups=optim_groups, optimizer_states=optimizer_states,
+                             dist_metas=dist_metas, param_shapes=param_shapes, real_batch_size=real)
+    group = getattr(batch_group, "replicate_group", None)
+    W = _group_world(group)
+    use_low_rank = bool(optimizer.use_low_rank_sync) and W > 1 and any(
+        bool(c.use_low_rank_sync) for c in configs)
+    real_grads = [g for g in (grads or [])[:real]] if grads is not None else []
+
+    if W > 1 and not use_low_rank and real_grads:
+        # runtime.py:439-491: dense all-reduce of the gradients across replicas
+        op = dist.ReduceOp.AVG if optimizer.defaults.get("rp_average_in_collective", True) else dist.ReduceOp.SUM
+        works = [dist.all_reduce(g, op=op, group=group, async_op=True) for g in real_grads]
+        yield
+        for w in works:
+            w.wait()
+
+    m, n = (int(d) for d in param_shapes[0])
+    transposed = bool(configs[0].is_transposed)
+    r = int(Qs[0].shape[1])
+    mp, nq = factor_rows(m, n, transposed)
+    dev = momentums[0].device
+    oversample = float(optimizer.defaults["rcqr_oversample"])
+
+    P = torch.zeros((B, mp, r), dtype=torch.float32, device=dev)
+    nonzero = torch.zeros((B,), dtype=torch.int32, device=dev)
+    codec.project_p(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed)
+
+    def ortho(P_slice, entry):
+        S = None if sketches is None else sketches.get(entry)
+        codec.orthonormalize(P_slice, m, n, transposed, _sketch_seed(optimizer, batch_cache_key, entry),
+                             oversample, sketch=None if S is None else S.reshape(1, *S.shape[-2:]).contiguous())
+
+    if W > 1:
+        rank = dist.get_rank(group)
+        padded = (B + W - 1) // W * W
+        if padded != B:
+            P = torch.cat([P, P.new_zeros((padded - B, mp, r))], dim=0)
+        for start in range(0, padded, W):
+            chunk = P[start:start + W]
+            P_single = torch.empty((1, mp, r), dtype=torch.float32, device=dev)
+            if use_low_rank:
+                # runtime.py:1428-1434: reduce-scatter(avg) hands entry start+rank to this rank
+                work = dist.reduce_scatter_tensor(P_single, chunk, op=dist.ReduceOp.AVG, group=group,
+                                                  async_op=True)
+                yield
+                work.wait()
+            else:
+                P_single.copy_(chunk[rank:rank + 1])
+            idx = start + rank
+            if idx < real:
+                ortho(P_single, idx)
+            else:
+                P_single.zero_()  # padded entries stay inert (runtime.py:1436-1441)
+            work = dist.all_gather_into_tensor(chunk, P_single, group=group, async_op=True)
+            yield
+            work.wait()
+        P = P[:B]
+        R = torch.zeros((B, nq, r), dtype=torch.float32, device=dev)
+        codec.project_r(list(momentums[:real]), P, R, transposed)
+        if use_low_rank:
+            work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
+            yield
+            work.wait()
+    else:
+        if sketches is None:
+            codec.orthonormalize(P[:real], m, n, transposed, _sketch_seed(optimizer, batch_cache_key, 0),
+                                 oversample)
+        else:
+            for i in range(real):
+                ortho(P[i:i + 1], i)
+        R = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
+        codec.project_r(list(momentums[:real]), P, R, transposed)
+
+    eps = float(optimizer.defaults["epsilon"])
+    codec.fixup_colnorm(P, R, list(Qs[:real]), nonzero, eps, m, n, transposed)
+
+    grp = optim_groups[0] or {}
+    st0 = optimizer_states[0] or {}
+    gshape = st0.get("per_expert_global_shape") or st0.get("global_shape") \
+        or getattr(dist_metas[0], "global_shape", None) or (m, n)
+    lr = float(grp.get("lr", optimizer.defaults["lr"]))
+    mu = float(grp.get("mu", optimizer.defaults["mu"]))
+    wd = float(grp.get("weight_decay", optimizer.defaults["weight_decay"] * float(grp.get("wd_mult", 1.0))))
+    rank_fraction = float(grp.get("rank_fraction", optimizer.defaults.get("rank_fraction", 0.25)))
+    scaled = scaled_lr_for_shape(lr=lr, m_global=int(gshape[0]), n_global=int(gshape[1]),
+                                 scale_mode=optimizer.defaults.get("scale_mode", "spectral"),
+                                 rank_fraction=rank_fraction,
+                                 extra_scale_factor=optimizer.defaults.get("extra_scale_factor", 0.2))
+    codec.ef_apply(list(momentums[:real]), list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd,
+                   scaled, transposed)
+    if commit_updates is not None:
+        for i in range(real):
+            if commit_updates[i] is not None:
+                commit_updates[i](params[i], momentums[i])
+    optimizer._last_batch_factors = (P, R) if getattr(optimizer, "_keep_factors", False) else None
+
+
+def run_dion_batch_async(optimizer, batch, sketches=None) -> Generator[None, None, None]:
+    """Unpack a DionBatch (ours or the reference's) into batch_dion_update_async."""
+    if batch is None or not batch.params:
+        return
+    entries = getattr(batch, "entries", ())
+    commit = [getattr(e, "commit_update", None) for e in entries[:int(batch.real_batch_size)]]
+    yield from batch_dion_update_async(
+        optimizer, list(batch.params), list(batch.momentums), list(batch.q_tensors), list(batch.configs),
+        list(batch.dist_metas), list(batch.optim_groups), list(batch.grads), list(batch.optimizer_states),
+        list(batch.param_shapes), int(batch.real_batch_size), int(batch.batch_cache_key), batch.batch_group,
+        batch.batch_collectives, commit_updates=commit, sketches=sketches)
+
+
+def coalesce_local_batches(batches, max_entries: int = 64):
+    """Merge consecutive same-key batches of a world-size-1 schedule into one launch group.
+
+    At batch_world_size 1 every DionBatch holds one matrix (batches.py:1001-1036)
+    and the matrices are independent, so running k of them through one set of
+    kernel launches is the same computation with k times fewer launches.
+    """
+    from .types import DionBatch
+
+    out = []
+    for b in batches:
+        bg = b.batch_group
+        if _group_world(getattr(bg, "replicate_group", None)) > 1 or int(b.real_batch_size) != len(b.params):
+            out.append(b)
+            continue
+        if out and isinstance(out[-1], DionBatch) and getattr(out[-1], "_coalesced", False) \
+                and out[-1].batch_key == b.batch_key and len(out[-1].entries) + len(b.entries) <= max_entries:
+            prev = out[-1]
+            merged = DionBatch(batch_key=prev.batch_key, entries=tuple(prev.entries) + tuple(b.entries),
+                               real_batch_size=prev.real_batch_size + b.real_batch_size,
+                               batch_cache_key=prev.batch_cache_key, batch_group=prev.batch_group,
+                               batch_collectives=prev.batch_collectives)
+            merged._coalesced = True
+            out[-1] = merged
+        else:
+            nb = DionBatch(batch_key=b.batch_key, entries=tuple(b.entries), real_batch_size=b.real_batch_size,
+                           batch_cache_key=b.batch_cache_key, batch_group=b.batch_group,
+                           batch_collectives=b.batch_collectives)
+            nb._coalesced = True
+            out.append(nb)
+    return out

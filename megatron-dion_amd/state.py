@@ -1,0 +1,87 @@
+"""Per-matrix Dion state rules: rank, orientation, low-rank sync, Q initialisation.
+
+Integer rules are bit-exact restatements of the reference:
+  rank rule            dion/state.py:179-188 (resolve_q_state_layout)
+  low-rank sync rule   dion/state.py:220-230 (should_use_low_rank_sync)
+  orientation rule     dion/state.py:304-310 (is_transposed = m < n, no TP/FS)
+  Q-init seed          dion/state.py:233-260 (blake2b of the param key)
+  Q-init values        dion/state.py:86-88 (CPU path: torch.randn(q_global_shape, generator=seed))
+State layout follows dion/state.py:527-654: momentum = zeros like the param
+(m x n), Q = (n_Q x r), r, local_shape, global_shape.
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from .types import DionParamConfig
+
+
+def rank_for_shape(m: int, n: int, rank_fraction: float, rank_multiple_of: int = 1) -> int:
+    """r = max(1, int(min(mult * ceil(rf * min(m, n) / mult), m, n)))."""
+    r = rank_fraction * min(m, n)
+    r = rank_multiple_of * math.ceil(r / rank_multiple_of)
+    r = min(r, m, n)
+    return max(1, int(r))
+
+
+def should_use_low_rank_sync(*, global_shape: Tuple[int, int], r_global: int, rank_fraction: float) -> bool:
+    """Compressed exchange only when (m + n) r < m n and rank_fraction < 1."""
+    m, n = int(global_shape[0]), int(global_shape[1])
+    if rank_fraction >= 1.0:
+        return False
+    return (m + n) * int(r_global) < m * n
+
+
+def is_transposed_shape(m: int, n: int) -> bool:
+    """Orientation: P is taken over the longer side (m < n => work on M^T)."""
+    return int(m) < int(n)
+
+
+def q_seed_from_param_key(*, base_seed: int, param_uid, param_name: str,
+                          q_global_shape: Tuple[int, int], is_transposed: bool) -> int:
+    """63-bit seed of blake2b(repr(key)), topology-invariant like the reference."""
+    if param_uid is None and not param_name:
+        raise RuntimeError("[DION_Q_INIT_SEED_ID_MISSING] Dion Q init requires param_uid or param_name")
+    key = repr(("dion_q_init", int(base_seed), param_uid if param_uid is not None else param_name,
+                tuple(int(d) for d in q_global_shape), bool(is_transposed))).encode("utf-8")
+    return int.from_bytes(hashlib.blake2b(key, digest_size=8).digest(), "little") & ((1 << 63) - 1)
+
+
+def init_q(q_global_shape: Tuple[int, int], seed: int, device, dtype=torch.float32) -> torch.Tensor:
+    """Q0 ~ N(0, 1): drawn on the CPU generator (the reference's CPU stream) then moved."""
+    gen = torch.Generator(device="cpu")
+    gen.manual_seed(int(seed))
+    q = torch.randn(tuple(int(d) for d in q_global_shape), generator=gen, dtype=dtype)
+    return q.to(device)
+
+
+def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_of: int = 1,
+                    base_seed: int = 0, param_uid=None, param_name: str = "",
+                    momentum_dtype: Optional[torch.dtype] = None,
+                    use_low_rank_sync: bool = True) -> Tuple[dict, DionParamConfig]:
+    """Fresh optimizer state + config for one 2D parameter (no TP/FS sharding)."""
+    if param.dim() != 2:
+        raise RuntimeError(f"[DION_NOT_2D] shape={tuple(param.shape)}")
+    m, n = (int(d) for d in param.shape)
+    transposed = is_transposed_shape(m, n)
+    r = rank_for_shape(m, n, rank_fraction, rank_multiple_of)
+    q_shape = (m if transposed else n, r)
+    seed = q_seed_from_param_key(base_seed=base_seed, param_uid=param_uid, param_name=param_name,
+                                 q_global_shape=q_shape, is_transposed=transposed)
+    state = {
+        "momentum": torch.zeros_like(param, dtype=momentum_dtype or param.dtype),
+        "Q": init_q(q_shape, seed, param.device),
+        "r": r,
+        "local_shape": (m, n),
+        "global_shape": (m, n),
+    }
+    cfg = DionParamConfig(
+        is_transposed=transposed,
+        use_low_rank_sync=bool(use_low_rank_sync) and should_use_low_rank_sync(
+            global_shape=(m, n), r_global=r, rank_fraction=rank_fraction),
+    )
+    return state, cfg

@@ -1,0 +1,59 @@
+"""Test-only codec backend built from the CPU oracle.
+
+Lets the multi-process (gloo) tests drive the product's batch runtime and
+collective schedule (megatron_dion_amd/runtime.py) on CPU tensors.  It is
+injected explicitly by tests (`MegatronDion(..., codec=OracleCodec())`); the
+product never constructs it and has no CPU fallback of its own.
+"""
+import torch
+
+from oracle import dion_oracle as O
+
+
+class OracleCodec:
+    name = "oracle-cpu"
+
+    def __init__(self, sketch_lookup=None, hyper_eps=1e-8):
+        self.sketch_lookup = sketch_lookup  # fn(P (1, m_P, r)) -> sketch (1, k, m_P) or None
+
+    def project_p(self, grads, momentums, qs, P, nonzero, transposed):
+        for b, M in enumerate(momentums):
+            if grads is not None:
+                M.add_(grads[b].to(M.dtype))
+            X = M.mT if transposed else M
+            P[b] = X @ qs[b]
+            nonzero[b] = int(bool((M != 0).any()))
+
+    def orthonormalize(self, P, m, n, transposed, seed, oversample=1.25, sketch=None):
+        for b in range(P.shape[0]):
+            S = sketch
+            if S is None and self.sketch_lookup is not None:
+                S = self.sketch_lookup(P[b:b + 1])
+            gen = torch.Generator().manual_seed(int(seed) & ((1 << 63) - 1))
+            P[b:b + 1] = O.orthogonalize(P[b:b + 1], oversample, sketch=S, generator=gen)
+
+    def project_r(self, momentums, P, R, transposed):
+        for b, M in enumerate(momentums):
+            X = M.mT if transposed else M
+            R[b] = X.mT @ P[b]
+
+    def fixup_colnorm(self, P, R, qs, nonzero, eps, m, n, transposed):
+        B = len(qs)
+        Q = torch.stack(qs, 0)
+        zero = (nonzero[:B] == 0).view(B, 1, 1)
+        P[:B] = torch.where(zero, torch.zeros_like(P[:B]), P[:B].nan_to_num())
+        R[:B] = torch.where(zero, Q.nan_to_num(), R[:B].nan_to_num())
+        Qn = O.column_normalize(R[:B], eps)
+        for b in range(B):
+            qs[b].copy_(Qn[b])
+
+    def ef_apply(self, momentums, params, P, R, qs, nonzero, mu, lr, wd, scaled_lr, transposed):
+        for b, M in enumerate(momentums):
+            upd = (R[b] @ P[b].mT) if transposed else (P[b] @ R[b].mT)
+            M.add_(upd * (-(1.0 - mu)))
+            if params is not None:
+                W = params[b]
+                if wd > 0:
+                    W.mul_(1 - lr * wd)
+                delta = (qs[b] @ P[b].mT) if transposed else (P[b] @ qs[b].mT)
+                W.add_(delta, alpha=-scaled_lr)

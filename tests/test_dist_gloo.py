@@ -1,0 +1,112 @@
+"""World-size-2 gloo tests of the replicate (DP) exchange schedule on CPU.
+
+The product's batch runtime (megatron_dion_amd/runtime.py) runs unchanged --
+batching, padding, reduce-scatter(avg) of P, owner-rank orthonormalisation,
+all-gather of P, all-reduce(avg) of R, AsyncRuntime interleave -- with the
+test-only oracle codec (tests/_cpu_codec.py) in place of the HIP kernels, so the
+N > 1 path is covered without GPUs.  Checked against the reference's own
+2-rank golden captures (c8: exact; c4: the intended per-batch-P semantics, see
+test_oracle_golden.test_reference_shared_p_buffer_defect_is_the_only_w2_difference).
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.slow
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, name, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    import megatron_dion_amd as mda
+    from megatron_dion_amd.optimizer import attach_dp_routing
+    from tests._cpu_codec import OracleCodec
+    from tests._golden import Case
+
+    case = Case(name)
+    h = case.hyper
+    names = [n for n, _, _ in case.mats]
+    params = {n: torch.nn.Parameter(case.t(rank, 0, f"{n}_W0").clone()) for n in names}
+    state = {"step": 0}
+    codec = OracleCodec(sketch_lookup=lambda P: case.sketch_for(rank, state["step"], P))
+    opt = mda.MegatronDion([params[n] for n in names], lr=h["lr"], mu=h["mu"], weight_decay=h["weight_decay"],
+                           rank_fraction=case.rank_fraction, epsilon=h["epsilon"],
+                           rcqr_oversample=h["rcqr_oversample"], codec=codec)
+    attach_dp_routing(opt, [(n, params[n]) for n in names], replicate_group=dist.group.WORLD)
+    for n in names:
+        opt.state[params[n]]["Q"].copy_(case.t(rank, 0, f"{n}_Q0"))
+    results = {}
+    for step in range(case.steps):
+        state["step"] = step
+        for n in names:
+            params[n].grad = case.t(rank, step, f"{n}_G").clone()
+        batches, _ = opt._route_step_params()
+        results[f"s{step}_schedule"] = [([e.dist_meta.param_name if e.dist_meta else "<pad>"
+                                          for e in b.entries], b.real_batch_size) for b in batches]
+        opt.step()
+        for n in names:
+            results[f"s{step}_{n}_W"] = params[n].detach().clone()
+            results[f"s{step}_{n}_M"] = opt.state[params[n]]["momentum"].clone()
+            results[f"s{step}_{n}_Q"] = opt.state[params[n]]["Q"].clone()
+    torch.save(results, os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(name, world=2):
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_worker, args=(world, _free_port(), name, tmp), nprocs=world, join=True,
+                           start_method="spawn")
+        return [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+
+
+def _maxrel(a, b):
+    return (a.double() - b.double()).abs().max().item() / max(b.double().abs().max().item(), 1e-30)
+
+
+def test_gloo_w2_matches_reference_single_batch():
+    from tests._golden import Case
+
+    case = Case("c8_w2_two_steps_T")
+    res = _run(case.name)
+    names = [n for n, _, _ in case.mats]
+    for rank in range(2):
+        for step in range(case.steps):
+            assert res[rank][f"s{step}_schedule"] == [(["x", "y"], 2)]
+            for n in names:
+                for k, ref in (("W", "W1"), ("M", "M1"), ("Q", "Q1")):
+                    err = _maxrel(res[rank][f"s{step}_{n}_{k}"], case.t(rank, step, f"{n}_{ref}"))
+                    assert err <= 1e-6, (rank, step, n, k, err)
+    # replicas agree bit-for-bit on W and Q; momentum stays rank-local
+    for n in names:
+        assert torch.equal(res[0][f"s1_{n}_W"], res[1][f"s1_{n}_W"])
+        assert torch.equal(res[0][f"s1_{n}_Q"], res[1][f"s1_{n}_Q"])
+        assert not torch.equal(res[0][f"s1_{n}_M"], res[1][f"s1_{n}_M"])
+
+
+def test_gloo_w2_padding_and_per_batch_p():
+    from tests._golden import Case
+    from tests.test_oracle_golden import _run_oracle
+
+    case = Case("c4_w2_pad3")
+    res = _run(case.name)
+    # reference schedule: [a, b] then [c, <pad>] (batches.py:903-968)
+    assert res[0]["s0_schedule"] == [(["a", "b"], 2), (["c", "<pad>"], 1)]
+    assert res[1]["s0_schedule"] == res[0]["s0_schedule"]
+    for step, rank, n, st, _ in _run_oracle(case, shared_p_buffer=False):
+        for k in ("W", "M", "Q"):
+            err = _maxrel(res[rank][f"s{step}_{n}_{k}"], st[k])
+            assert err <= 1e-6, (rank, n, k, err)

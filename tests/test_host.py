@@ -1,0 +1,189 @@
+"""CPU tests of the host side: C-ABI library loading/exports, state rules, batching, runtime."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+import megatron_dion_amd as mda
+from megatron_dion_amd import _lib
+from megatron_dion_amd.batches import build_dion_batches
+from megatron_dion_amd.runtime import AsyncRuntime
+from megatron_dion_amd.types import DionDistMeta, DionStepParam
+from oracle import dion_oracle as O
+from tests._golden import Case, case_names
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    text = open(os.path.join(ROOT, "include", "dion_codec.h")).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(dion_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    syms = _header_symbols()
+    assert len(syms) == 8
+    assert sorted(_lib.EXPORTED) == syms
+    for s in syms:
+        assert getattr(lib, s) is not None
+    assert lib.dion_abi_version() == _lib.ABI_VERSION
+
+
+def test_abi_rejects_bad_descriptors_without_gpu():
+    lib = _lib.load()
+    d = _lib.DionBatchDesc(batch=1, m=64, n=48, r=8, transposed=0, g_dtype=_lib.DTYPE_BF16,
+                           m_dtype=_lib.DTYPE_F32, w_dtype=_lib.DTYPE_F32)
+    nbytes = ctypes.c_size_t(123)
+    assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P, ctypes.byref(nbytes)) == _lib.DION_OK
+    d.r = 0
+    assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P, ctypes.byref(nbytes)) == \
+        _lib.DION_E_UNSUPPORTED
+    assert b"rank" in lib.dion_last_error()
+    d.r = 8
+    d.m_dtype = _lib.DTYPE_BF16
+    assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P, ctypes.byref(nbytes)) == \
+        _lib.DION_E_UNSUPPORTED
+    d.m_dtype = _lib.DTYPE_F32
+    d.r = 100
+    assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P, ctypes.byref(nbytes)) == _lib.DION_E_INVALID
+    d.r = 8
+    assert lib.dion_workspace_bytes(ctypes.byref(d), 99, ctypes.byref(nbytes)) == _lib.DION_E_INVALID
+    # null pointers are rejected before any device work
+    assert lib.dion_project_p(ctypes.byref(d), None, None, None, None, None, None, 0, None) == _lib.DION_E_INVALID
+
+
+def test_workspace_sizes_cover_llama_batches():
+    lib = _lib.load()
+    for (m, n) in ((6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)):
+        for batch in (1, 8, 32, 100):
+            d = _lib.DionBatchDesc(batch=batch, m=m, n=n, r=64, transposed=int(m < n), g_dtype=_lib.DTYPE_BF16,
+                                   m_dtype=_lib.DTYPE_F32, w_dtype=_lib.DTYPE_F32)
+            for op in (_lib.OP_PROJECT_P, _lib.OP_ORTHONORMALIZE, _lib.OP_PROJECT_R):
+                nbytes = ctypes.c_size_t(0)
+                assert lib.dion_workspace_bytes(ctypes.byref(d), op, ctypes.byref(nbytes)) == 0
+                assert nbytes.value < 8 << 30
+
+
+def test_rules_match_oracle_and_reference():
+    for m, n in ((64, 48), (48, 96), (28672, 4096), (4096, 14336), (17, 19), (5, 3)):
+        for rf in (1 / 64, 0.25, 0.5, 1.0):
+            assert mda.rank_for_shape(m, n, rf) == O.rank_for_shape(m, n, rf)
+            r = mda.rank_for_shape(m, n, rf)
+            assert mda.should_use_low_rank_sync(global_shape=(m, n), r_global=r, rank_fraction=rf) == \
+                O.use_low_rank_sync(m, n, r, rf)
+        assert mda.is_transposed_shape(m, n) == (m < n)
+    assert mda.scaled_lr_for_shape(lr=1.0, m_global=16, n_global=4, scale_mode="spectral",
+                                   rank_fraction=0.25) == pytest.approx(0.8)
+    with pytest.raises(RuntimeError, match="DION_INVALID_SCALE_MODE"):
+        mda.scaled_lr_for_shape(lr=1.0, m_global=4, n_global=4, scale_mode="x", rank_fraction=0.25)
+
+
+def test_q_init_is_seeded_and_topology_invariant():
+    # dion/state.py:233-260 + :86-88: the seed depends only on the parameter key
+    s1 = mda.q_seed_from_param_key(base_seed=0, param_uid=("w",), param_name="w", q_global_shape=(48, 8),
+                                   is_transposed=False)
+    s2 = mda.q_seed_from_param_key(base_seed=0, param_uid=("w",), param_name="other", q_global_shape=(48, 8),
+                                   is_transposed=False)
+    s3 = mda.q_seed_from_param_key(base_seed=1, param_uid=("w",), param_name="w", q_global_shape=(48, 8),
+                                   is_transposed=False)
+    assert s1 == s2 and s1 != s3 and 0 <= s1 < 2 ** 63
+    p = torch.zeros(64, 48)
+    st_a, cfg = mda.init_dion_state(p, rank_fraction=1 / 6, param_uid=("w",))
+    st_b, _ = mda.init_dion_state(p, rank_fraction=1 / 6, param_uid=("w",))
+    assert torch.equal(st_a["Q"], st_b["Q"]) and st_a["Q"].shape == (48, 8)
+    gen = torch.Generator().manual_seed(s1)
+    assert torch.equal(st_a["Q"], torch.randn((48, 8), generator=gen))
+    assert cfg.is_transposed is False and cfg.use_low_rank_sync is True
+
+
+@pytest.mark.parametrize("name", [n for n in case_names() if Case(n).world == 1])
+def test_batch_schedule_matches_reference_w1(name):
+    case = Case(name)
+    group = {"lr": 0.01, "mu": 0.95, "weight_decay": 0.01, "rank_fraction": case.rank_fraction}
+    steps = []
+    for n, m, k in case.mats:
+        p = torch.nn.Parameter(torch.zeros(m, k))
+        st, cfg = mda.init_dion_state(p, rank_fraction=case.rank_fraction, param_uid=(n,), param_name=n)
+        steps.append(DionStepParam(param=p, grad=torch.zeros(m, k), optimizer_state=st, optim_group=group,
+                                   config=cfg, dist_meta=DionDistMeta(global_shape=(m, k), param_uid=(n,),
+                                                                      param_name=n)))
+    steps.sort(key=lambda s: s.dist_meta.param_uid)
+    batches = build_dion_batches(dion_params=steps, get_replicate_group=lambda: None)
+    got = [([e.dist_meta.param_name for e in b.entries], b.real_batch_size) for b in batches]
+    want = [(b["members"], b["real"]) for b in case.batches(0, 0)]
+    assert got == want
+
+
+def test_async_runtime_interleave_matches_reference_emulation():
+    trace_a, trace_b = [], []
+
+    def gen(tag, n, trace):
+        for i in range(n):
+            trace.append((tag, i))
+            yield
+        trace.append((tag, "done"))
+
+    tasks = [("t0", 3), ("t1", 1), ("t2", 4), ("t3", 2), ("t4", 0)]
+    AsyncRuntime((gen(t, n, trace_a) for t, n in tasks), 3).run()
+    O.run_async_runtime((gen(t, n, trace_b) for t, n in tasks), 3)
+    assert trace_a == trace_b
+
+
+def test_step_requires_distributed_mode_and_rejects_elementwise():
+    p = torch.nn.Parameter(torch.zeros(8, 8))
+    opt = mda.MegatronDion([p], codec=object())
+    with pytest.raises(RuntimeError, match="DION_STEP_REQUIRES_DISTRIBUTED_MODE"):
+        opt.step()
+    opt.enable_distributed_mode(route_step_params=lambda: ([], [object()]))
+    with pytest.raises(RuntimeError, match="DION_ELEMENTWISE_UNSUPPORTED"):
+        opt.step()
+    assert opt.param_groups[0]["step"] == 2 and opt._step_count == 2
+
+
+def test_optimizer_defaults_match_reference_keys():
+    p = torch.nn.Parameter(torch.zeros(8, 8))
+    opt = mda.MegatronDion([p], codec=object())
+    # dion/algorithm.py:82-105
+    for k in ("lr", "mu", "weight_decay", "rank_fraction", "rank_multiple_of", "epsilon", "rcqr_oversample",
+              "betas", "elementwise_eps", "rp_average_in_collective", "use_fs_collectives", "enable_async",
+              "use_low_rank_sync", "elementwise_optimizer", "elementwise_lr_scale", "scale_mode",
+              "extra_scale_factor", "split_qkv", "split_linear", "algorithm", "step"):
+        assert k in opt.defaults
+    assert opt.defaults["mu"] == 0.95 and opt.defaults["epsilon"] == 1e-8
+
+
+def test_product_path_fails_loudly_without_library(tmp_path):
+    with pytest.raises(_lib.DionLibraryError, match="DION_HIP_LIBRARY_MISSING"):
+        _lib.load(str(tmp_path / "missing.so"))
+
+
+def test_local_path_end_to_end_with_oracle_codec():
+    """Host runtime (W = 1, coalesced launch groups) reproduces the golden c7 (3 matrices, both
+    orientations, 2 steps) when the test-only oracle codec stands in for the kernels."""
+    from megatron_dion_amd.optimizer import attach_dp_routing
+    from tests._cpu_codec import OracleCodec
+
+    case = Case("c7_two_steps_mixed")
+    h = case.hyper
+    names = [n for n, _, _ in case.mats]
+    params = {n: torch.nn.Parameter(case.t(0, 0, f"{n}_W0").clone()) for n in names}
+    cur = {"step": 0}
+    opt = mda.MegatronDion([params[n] for n in names], lr=h["lr"], mu=h["mu"], weight_decay=h["weight_decay"],
+                           rank_fraction=case.rank_fraction,
+                           codec=OracleCodec(sketch_lookup=lambda P: case.sketch_for(0, cur["step"], P)))
+    attach_dp_routing(opt, [(n, params[n]) for n in names])
+    for n in names:
+        opt.state[params[n]]["Q"].copy_(case.t(0, 0, f"{n}_Q0"))
+    for step in range(case.steps):
+        cur["step"] = step
+        for n in names:
+            params[n].grad = case.t(0, step, f"{n}_G").clone()
+        opt.step()
+        for n in names:
+            for got, key in ((params[n], "W1"), (opt.state[params[n]]["momentum"], "M1"),
+                             (opt.state[params[n]]["Q"], "Q1")):
+                ref = case.t(0, step, f"{n}_{key}")
+                assert (got.detach() - ref).abs().max().item() <= 1e-6 * ref.abs().max().item()
