@@ -1022,9 +1022,15 @@ int run_panel(int xmode, int mp, int cols, int r, int batch, const float* P, con
 int launch_triinv(const float* U, float* Uinv, int r, int batch, hipStream_t st) {
   const size_t ubytes = sizeof(float) * static_cast<size_t>((r * r + 3) / 4 * 4);
   if (r <= 96) {
-    hipLaunchKernelGGL((triinv_kernel<double>), dim3(batch), dim3(256), ubytes + sizeof(double) * r * r, st, U, Uinv, r);
+    const size_t lds = ubytes + sizeof(double) * r * r;
+    int rc = allow_lds(triinv_kernel<double>, lds);
+    if (rc != DION_OK) return rc;
+    hipLaunchKernelGGL((triinv_kernel<double>), dim3(batch), dim3(256), lds, st, U, Uinv, r);
   } else {
-    hipLaunchKernelGGL((triinv_kernel<float>), dim3(batch), dim3(256), ubytes + sizeof(float) * r * r, st, U, Uinv, r);
+    const size_t lds = ubytes + sizeof(float) * r * r;
+    int rc = allow_lds(triinv_kernel<float>, lds);
+    if (rc != DION_OK) return rc;
+    hipLaunchKernelGGL((triinv_kernel<float>), dim3(batch), dim3(256), lds, st, U, Uinv, r);
   }
   return check_launch("triinv");
 }
@@ -1056,6 +1062,17 @@ int apply_right(const float* src, float* dst, const float* Uinv, int mp, int r, 
     hipLaunchKernelGGL((rowproj_kernel<RB, DION_DTYPE_NONE>), grid, dim3(256), 0, st, a);
     return check_launch("apply_right");
   });
+}
+
+// kernels that take more than the default 64 KiB of dynamic LDS must opt in
+template <class K>
+int allow_lds(K kernel, size_t bytes) {
+  if (bytes <= 64 * 1024) return DION_OK;
+  if (bytes > 160 * 1024) return fail(DION_E_UNSUPPORTED, "kernel needs %zu bytes of LDS (> 160 KiB)", bytes);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
+  if (e != hipSuccess) return fail(DION_E_LAUNCH, "hipFuncSetAttribute(%zu): %s", bytes, hipGetErrorString(e));
+  return DION_OK;
 }
 
 size_t qr_lds_bytes(int K, int r) { return sizeof(float) * (static_cast<size_t>(r) * (K + 1) + r + 3 + 8 + 4); }
@@ -1164,6 +1181,8 @@ int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, u
     if (plan.plain_qr) {
       const size_t lds = qr_lds_bytes(mp, r);
       if (lds > 160 * 1024) return fail(DION_E_UNSUPPORTED, "plain QR of %dx%d does not fit LDS", mp, r);
+      rc = allow_lds(householder_qr_kernel, lds);
+      if (rc != DION_OK) return rc;
       hipLaunchKernelGGL(householder_qr_kernel, dim3(nb), dim3(256), lds, st, Pb, nullptr, Pb, mp, r, 1);
       rc = check_launch("householder_qr(Q)");
       if (rc != DION_OK) return rc;
@@ -1181,6 +1200,8 @@ int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, u
     const int K = plan.k;
     const size_t lds = qr_lds_bytes(K, r);
     if (lds > 160 * 1024) return fail(DION_E_UNSUPPORTED, "sketch QR of %dx%d does not fit LDS", K, r);
+    rc = allow_lds(householder_qr_kernel, lds);
+    if (rc != DION_OK) return rc;
     // (1) S P  (K x r)
     const float std_ = sqrtf(1.0f / static_cast<float>(K));
     rc = run_panel(sketch ? 1 : 2, mp, K, r, nb, Pb, sketch ? sketch + static_cast<long>(b0) * K * mp : nullptr,
