@@ -1019,6 +1019,17 @@ int run_panel(int xmode, int mp, int cols, int r, int batch, const float* P, con
   return DION_OK;
 }
 
+// kernels that take more than the default 64 KiB of dynamic LDS must opt in
+template <class K>
+int allow_lds(K kernel, size_t bytes) {
+  if (bytes <= 64 * 1024) return DION_OK;
+  if (bytes > 160 * 1024) return fail(DION_E_UNSUPPORTED, "kernel needs %zu bytes of LDS (> 160 KiB)", bytes);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
+  if (e != hipSuccess) return fail(DION_E_LAUNCH, "hipFuncSetAttribute(%zu): %s", bytes, hipGetErrorString(e));
+  return DION_OK;
+}
+
 int launch_triinv(const float* U, float* Uinv, int r, int batch, hipStream_t st) {
   const size_t ubytes = sizeof(float) * static_cast<size_t>((r * r + 3) / 4 * 4);
   if (r <= 96) {
@@ -1062,17 +1073,6 @@ int apply_right(const float* src, float* dst, const float* Uinv, int mp, int r, 
     hipLaunchKernelGGL((rowproj_kernel<RB, DION_DTYPE_NONE>), grid, dim3(256), 0, st, a);
     return check_launch("apply_right");
   });
-}
-
-// kernels that take more than the default 64 KiB of dynamic LDS must opt in
-template <class K>
-int allow_lds(K kernel, size_t bytes) {
-  if (bytes <= 64 * 1024) return DION_OK;
-  if (bytes > 160 * 1024) return fail(DION_E_UNSUPPORTED, "kernel needs %zu bytes of LDS (> 160 KiB)", bytes);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
-  if (e != hipSuccess) return fail(DION_E_LAUNCH, "hipFuncSetAttribute(%zu): %s", bytes, hipGetErrorString(e));
-  return DION_OK;
 }
 
 size_t qr_lds_bytes(int K, int r) { return sizeof(float) * (static_cast<size_t>(r) * (K + 1) + r + 3 + 8 + 4); }
