@@ -134,7 +134,7 @@ def main():
     named = []
     for name, m, n in shapes:
         w = torch.nn.Parameter(torch.empty(m, n, device=dev).normal_(0.0, 0.02))
-        w.grad = torch.empty(m, n, device=dev).normal_(0.0, 1e-3).to(torch.bfloat16)
+        w.main_grad = torch.empty(m, n, device=dev).normal_(0.0, 1e-3).to(torch.bfloat16)
         named.append((name, w))
     codec = TimedCodec(HipDionCodec(dev))
     opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=1 / 64,

@@ -132,8 +132,9 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
     Plays the part of the reference's DionDistributedOptimizer routing
     (distrib_dion/bootstrap.py:519-606 -> batches.py:971 build_dion_batches) for
     users outside Megatron and for the benchmark: params sorted by uid, one
-    batch per `batch_world_size` same-key matrices.  Each parameter's `.grad`
-    (bf16 or fp32) is the G of the step.
+    batch per `batch_world_size` same-key matrices.  G of each step is taken
+    from `param.main_grad` (Megatron's grad buffer view, bf16 or fp32) when
+    present, else from `param.grad`.
     """
     group = optimizer.param_groups[0]
     rf = float(group.get("rank_fraction", optimizer.defaults["rank_fraction"]))
@@ -152,10 +153,13 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
     def route():
         steps = []
         for name, p in ordered:
-            if p.grad is None:
+            g = getattr(p, "main_grad", None)
+            if g is None:
+                g = p.grad
+            if g is None:
                 continue
             cfg, meta = metas[name]
-            steps.append(DionStepParam(param=p, grad=p.grad, optimizer_state=optimizer.state[p],
+            steps.append(DionStepParam(param=p, grad=g, optimizer_state=optimizer.state[p],
                                        optim_group=group, config=cfg, dist_meta=meta))
         batches = build_dion_batches(
             dion_params=steps, get_replicate_group=lambda: replicate_group,
