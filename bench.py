@@ -83,7 +83,8 @@ def cpu_baseline(sample_layers=1, steps=1):
     """The pinned CPU oracle (`port`) on one Llama-3-8B layer, timed on this host's cores."""
     from oracle import dion_oracle as O
 
-    cores = len(os.sched_getaffinity(0))
+    # the GPU box exposes the whole host's CPUs; its share is OMP_NUM_THREADS (16 per GPU)
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     torch.set_num_threads(cores)
     gen = torch.Generator().manual_seed(99)
     hyper = O.DionHyper(rank_fraction=1 / 64)
