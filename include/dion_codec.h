@@ -35,7 +35,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 1
+#define DION_ABI_VERSION 2
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -51,6 +51,7 @@ typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 #define DION_OP_PROJECT_P 1
 #define DION_OP_ORTHONORMALIZE 2
 #define DION_OP_PROJECT_R 3
+#define DION_OP_FIXUP_COLNORM 4
 
 typedef struct DionBatchDesc {
   int32_t batch;      /* matrices in this call (all the same shape)            */
@@ -115,7 +116,8 @@ int dion_project_r(const DionBatchDesc* desc, const float* const* M, const float
  *   Q_b <- R_b / (sqrt(sum_rows R_b^2) + eps)          (Q_b is overwritten)
  */
 int dion_fixup_colnorm(const DionBatchDesc* desc, float* P, float* R, float* const* Q,
-                       const uint32_t* nonzero, float eps, dion_stream_t stream);
+                       const uint32_t* nonzero, float eps, void* ws, size_t ws_bytes,
+                       dion_stream_t stream);
 
 /*
  * Error feedback + weight update (kernels.py:54-154, 229-276; runtime.py:1105-1113):

@@ -11,7 +11,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "csrc", "libdion_codec.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -26,6 +26,7 @@ DTYPE_BF16 = 2
 OP_PROJECT_P = 1
 OP_ORTHONORMALIZE = 2
 OP_PROJECT_R = 3
+OP_FIXUP_COLNORM = 4
 
 # every symbol include/dion_codec.h declares
 EXPORTED = (
@@ -72,7 +73,7 @@ _SIGNATURES = {
     "dion_orthonormalize": ([_DESC, _P, _P, ctypes.c_uint64, ctypes.c_float, _P, ctypes.c_size_t, _P],
                             ctypes.c_int),
     "dion_project_r": ([_DESC, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
-    "dion_fixup_colnorm": ([_DESC, _P, _P, _PP, _P, ctypes.c_float, _P], ctypes.c_int),
+    "dion_fixup_colnorm": ([_DESC, _P, _P, _PP, _P, ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_ef_apply": ([_DESC, _PP, _PP, _P, _P, _PP, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                        ctypes.c_float, _P], ctypes.c_int),
 }

@@ -146,8 +146,10 @@ class HipDionCodec:
             return
         r = int(P.shape[2])
         d = self._desc(B, m, n, r, transposed)
+        ws = self.workspace(d, _lib.OP_FIXUP_COLNORM)
         rc = self.lib.dion_fixup_colnorm(ctypes.byref(d), P.data_ptr(), R.data_ptr(), _ptrs(qs),
-                                         nonzero.data_ptr(), float(eps), self._stream())
+                                         nonzero.data_ptr(), float(eps), ws.data_ptr(), ws.numel(),
+                                         self._stream())
         _lib.check(rc, "dion_fixup_colnorm")
 
     def ef_apply(self, momentums: List[torch.Tensor], params: Optional[List[torch.Tensor]],

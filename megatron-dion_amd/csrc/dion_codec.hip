@@ -460,7 +460,8 @@ __global__ void __launch_bounds__(256) householder_qr_kernel(const float* __rest
   }
   __syncthreads();
   const int kmax = min(K, r);
-  const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+  int tpc = 64;  // lanes per trailing column: a power of two with tpc * r <= 2 * nt
+  while (tpc > 1 && tpc * r > 2 * nt) tpc >>= 1;
   for (int j = 0; j < kmax; ++j) {
     float* aj = As + j * ld;
     float ss = 0.f;
@@ -489,15 +490,23 @@ __global__ void __launch_bounds__(256) householder_qr_kernel(const float* __rest
     __syncthreads();
     if (tid == 0) aj[j] = bc[1];
     const float tj = tau[j];
-    // apply H_j = I - tau v v^T (v_j = 1) to the trailing columns, one wave per column
-    for (int c = j + 1 + wave; c < r; c += nw) {
-      float* ac = As + c * ld;
+    // apply H_j = I - tau v v^T (v_j = 1) to the trailing columns: `tpc` lanes per
+    // column split the rows, reduce with butterfly shuffles inside their group
+    for (int c0 = j + 1; c0 < r; c0 += nt / tpc) {
+      const int c = c0 + tid / tpc;
+      const int p = tid % tpc;
       float w = 0.f;
-      for (int i = j + 1 + lane; i < K; i += 64) w += aj[i] * ac[i];
-      w = wave_sum(w) + ac[j];
-      w *= tj;
-      if (lane == 0) ac[j] -= w;
-      for (int i = j + 1 + lane; i < K; i += 64) ac[i] -= w * aj[i];
+      if (c < r) {
+        const float* ac = As + c * ld;
+        for (int i = j + 1 + p; i < K; i += tpc) w += aj[i] * ac[i];
+      }
+      for (int off = tpc >> 1; off > 0; off >>= 1) w += __shfl_xor(w, off, 64);
+      if (c < r) {
+        float* ac = As + c * ld;
+        w = (w + ac[j]) * tj;
+        if (p == 0) ac[j] -= w;
+        for (int i = j + 1 + p; i < K; i += tpc) ac[i] -= w * aj[i];
+      }
     }
     __syncthreads();
   }
@@ -513,15 +522,20 @@ __global__ void __launch_bounds__(256) householder_qr_kernel(const float* __rest
   for (int j = kmax - 1; j >= 0; --j) {
     float* aj = As + j * ld;
     const float tj = tau[j];
-    if (j < r - 1) {
-      for (int c = j + 1 + wave; c < r; c += nw) {
+    for (int c0 = j + 1; c0 < r; c0 += nt / tpc) {
+      const int c = c0 + tid / tpc;
+      const int p = tid % tpc;
+      float w = 0.f;
+      if (c < r) {
+        const float* ac = As + c * ld;
+        for (int i = j + 1 + p; i < K; i += tpc) w += aj[i] * ac[i];
+      }
+      for (int off = tpc >> 1; off > 0; off >>= 1) w += __shfl_xor(w, off, 64);
+      if (c < r) {
         float* ac = As + c * ld;
-        float w = 0.f;
-        for (int i = j + 1 + lane; i < K; i += 64) w += aj[i] * ac[i];
-        w = wave_sum(w) + ac[j];  // v_j = 1
-        w *= tj;
-        if (lane == 0) ac[j] -= w;
-        for (int i = j + 1 + lane; i < K; i += 64) ac[i] -= w * aj[i];
+        w = (w + ac[j]) * tj;  // v_j = 1
+        if (p == 0) ac[j] -= w;
+        for (int i = j + 1 + p; i < K; i += tpc) ac[i] -= w * aj[i];
       }
     }
     __syncthreads();
@@ -558,11 +572,15 @@ __global__ void __launch_bounds__(256) cholesky_kernel(const float* __restrict__
   }
   __syncthreads();
   int jf = r;  // first failed pivot (r = none)
+  int tpc = 64;
+  while (tpc > 1 && tpc * r > 2 * nt) tpc >>= 1;
+  const int lane = tid & 63;
   for (int j = 0; j < r; ++j) {
-    if (tid == 0) {
-      float ajj = U[j * ld + j];
-      for (int k = 0; k < j; ++k) ajj -= U[k * ld + j] * U[k * ld + j];
-      bc[0] = ajj;
+    if (tid < 64) {  // wave 0: ajj = a_jj - sum_k u_kj^2 (fixed lane order)
+      float v = 0.f;
+      for (int k = lane; k < j; k += 64) v += U[k * ld + j] * U[k * ld + j];
+      v = wave_sum(v);
+      if (lane == 0) bc[0] = U[j * ld + j] - v;
     }
     __syncthreads();
     const float ajj = bc[0];
@@ -572,10 +590,14 @@ __global__ void __launch_bounds__(256) cholesky_kernel(const float* __restrict__
     }
     const float ujj = sqrtf(ajj);
     const float inv = 1.f / ujj;
-    for (int c = j + 1 + tid; c < r; c += nt) {
-      float v = U[j * ld + c];
-      for (int k = 0; k < j; ++k) v -= U[k * ld + j] * U[k * ld + c];
-      U[j * ld + c] = v * inv;
+    for (int c0 = j + 1; c0 < r; c0 += nt / tpc) {
+      const int c = c0 + tid / tpc;
+      const int p = tid % tpc;
+      float v = 0.f;
+      if (c < r)
+        for (int k = p; k < j; k += tpc) v += U[k * ld + j] * U[k * ld + c];
+      for (int off = tpc >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (c < r && p == 0) U[j * ld + c] = (U[j * ld + c] - v) * inv;
     }
     __syncthreads();
     if (tid == 0) U[j * ld + j] = ujj;
@@ -613,12 +635,19 @@ __global__ void __launch_bounds__(256) triinv_kernel(const float* __restrict__ U
     X[idx] = XT(0);
   }
   __syncthreads();
+  int tpc = 64;
+  while (tpc > 1 && tpc * r > 2 * nt) tpc >>= 1;
   for (int i = r - 1; i >= 0; --i) {
     const double uii = static_cast<double>(U[i * r + i]);
-    for (int c = i + tid; c < r; c += nt) {
-      double acc = (c == i) ? 1.0 : 0.0;
-      for (int k = i + 1; k <= c; ++k) acc -= static_cast<double>(U[i * r + k]) * static_cast<double>(X[k * r + c]);
-      X[i * r + c] = static_cast<XT>(acc / uii);
+    for (int c0 = i; c0 < r; c0 += nt / tpc) {
+      const int c = c0 + tid / tpc;
+      const int p = tid % tpc;
+      double acc = 0.0;
+      if (c < r)
+        for (int k = i + 1 + p; k <= c; k += tpc)
+          acc += static_cast<double>(U[i * r + k]) * static_cast<double>(X[k * r + c]);
+      for (int off = tpc >> 1; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+      if (c < r && p == 0) X[i * r + c] = static_cast<XT>(((c == i) ? 1.0 : 0.0) - acc) / static_cast<XT>(uii);
     }
     __syncthreads();
   }
@@ -635,43 +664,63 @@ __global__ void __launch_bounds__(256) triinv_kernel(const float* __restrict__ U
 struct FixArgs {
   float* q[MAXB];
   float* R;           // (batch, nq, r)
+  float* part;        // (batch, nchunk, r) partial column sums of squares
   const uint32_t* nonzero;
-  int nq, r, tpc;
+  int nq, r, tpc, nchunk, rows_per_chunk;
   float eps;
 };
 
-__global__ void __launch_bounds__(256) fixup_colnorm_kernel(const FixArgs a) {
-  __shared__ float part[256];
-  __shared__ float denom[256];
-  const int b = blockIdx.x;
+// phase 1: fix R rows of one chunk and write its column partial sums
+__global__ void __launch_bounds__(256) fixup_partial_kernel(const FixArgs a) {
+  __shared__ float red[256];
+  const int b = blockIdx.y, ch = blockIdx.x;
   const int tid = threadIdx.x;
   const int r = a.r, nq = a.nq, tpc = a.tpc;
   const bool zero = (a.nonzero[b] == 0u);
   float* R = a.R + static_cast<long>(b) * nq * r;
-  float* Q = a.q[b];
-  const int c = tid % r;
-  const int p = tid / r;
-  const bool active = (p < tpc);
+  const float* Q = a.q[b];
+  const int c = tid % r, p = tid / r;
+  const int row0 = ch * a.rows_per_chunk;
+  const int row1 = min(nq, row0 + a.rows_per_chunk);
   float ss = 0.f;
-  if (active) {
-    for (int row = p; row < nq; row += tpc) {
+  if (p < tpc) {
+    for (int row = row0 + p; row < row1; row += tpc) {
       const long idx = static_cast<long>(row) * r + c;
       const float v = zero ? nan_to_num(Q[idx]) : nan_to_num(R[idx]);
       R[idx] = v;
       ss += v * v;
     }
   }
-  part[tid] = ss;
+  red[tid] = ss;
   __syncthreads();
   if (tid < r) {
     float s = 0.f;
-    for (int k = 0; k < tpc; ++k) s += part[k * r + tid];
+    for (int k = 0; k < tpc; ++k) s += red[k * r + tid];
+    a.part[(static_cast<long>(b) * a.nchunk + ch) * r + tid] = s;
+  }
+}
+
+// phase 2: column norms from the partials (fixed order), Q <- R / (norm + eps)
+__global__ void __launch_bounds__(256) colnorm_apply_kernel(const FixArgs a) {
+  __shared__ float denom[256];
+  const int b = blockIdx.y, ch = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int r = a.r, nq = a.nq, tpc = a.tpc;
+  if (tid < r) {
+    float s = 0.f;
+    const float* pp = a.part + static_cast<long>(b) * a.nchunk * r + tid;
+    for (int k = 0; k < a.nchunk; ++k) s += pp[static_cast<long>(k) * r];
     denom[tid] = sqrtf(s) + a.eps;
   }
   __syncthreads();
-  if (active) {
+  const float* R = a.R + static_cast<long>(b) * nq * r;
+  float* Q = a.q[b];
+  const int c = tid % r, p = tid / r;
+  const int row0 = ch * a.rows_per_chunk;
+  const int row1 = min(nq, row0 + a.rows_per_chunk);
+  if (p < tpc) {
     const float d = denom[c];
-    for (int row = p; row < nq; row += tpc) {
+    for (int row = row0 + p; row < row1; row += tpc) {
       const long idx = static_cast<long>(row) * r + c;
       Q[idx] = R[idx] / d;
     }
@@ -738,60 +787,169 @@ __device__ __forceinline__ void load_factor(const float* __restrict__ F, int idx
   }
 }
 
-template <int RH>
-__global__ void __launch_bounds__(256) ef_update_kernel(const EfArgs a) {
+// v2 geometry: a wave owns a 32-wide strip of the side whose factors differ
+// between the two updates (R for M, Qn for W) and keeps both in registers;
+// it then streams 32 x 32 tiles along the other side, where the shared factor
+// P lives, with the next tile's loads (P slice, M tile, W tile) in flight while
+// the current tile's MFMA chains run.  ROWFIX = transposed (R, Qn indexed by
+// rows); otherwise R, Qn are indexed by columns and P by rows.
+constexpr int kEfStream = 512;  // streamed extent per block (16 tiles)
+
+template <int RH, bool ROWFIX>
+struct EfTile {
+  float sp[RH];
+  f32x16 accm, accw;
+};
+
+// Tile addressing: element (i, j) of the 32 x 32 tile at (row0, col0) held in
+// accumulator register q of lane (t, h) is (row0 + (q&3) + 8(q>>2) + 4h, col0 + t).
+// Its byte offset splits into a per-lane part 4(4h ld + t), loop-invariant, and
+// a wave-uniform part 4((row0 + (q&3) + 8(q>>2)) ld + col0), so full tiles use
+// buffer loads/stores with one VGPR offset and an SGPR offset per register.
+struct EfBuf {
+  __amdgpu_buffer_rsrc_t m, w;
+  int voff_m, voff_w;
+};
+
+template <int RH, bool ROWFIX, bool FAST>
+__device__ __forceinline__ void ef_load_tile(const EfArgs& a, const EfBuf& bf, int b, int fbase, int s0, int t,
+                                             int h, bool zero, const float* __restrict__ Pb,
+                                             EfTile<RH, ROWFIX>& T) {
+  const int rows = a.rows, cols = a.cols, r = a.r;
+  load_factor<RH>(Pb, s0 + t, ROWFIX ? cols : rows, r, h, 1.f, T.sp);
+  const int row0 = ROWFIX ? fbase : s0;
+  const int col0 = ROWFIX ? s0 : fbase;
+  if constexpr (FAST) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int rq = row0 + (q & 3) + 8 * (q >> 2);
+      if (!zero) {
+        const int so = __builtin_amdgcn_readfirstlane((rq * static_cast<int>(a.ld_m) + col0) * 4);
+        T.accm[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bf.m, bf.voff_m, so, 0));
+      } else {
+        T.accm[q] = 0.f;
+      }
+      if (a.has_w) {
+        const int so = __builtin_amdgcn_readfirstlane((rq * static_cast<int>(a.ld_w) + col0) * 4);
+        T.accw[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bf.w, bf.voff_w, so, 0)) * a.decay;
+      } else {
+        T.accw[q] = 0.f;
+      }
+    }
+    return;
+  } else {
+  const float* M = a.m[b];
+  const float* W = a.w[b];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    const int j = col0 + t;
+    const bool ok = (i < rows) && (j < cols);
+    T.accm[q] = (ok && !zero) ? M[static_cast<long>(i) * a.ld_m + j] : 0.f;
+    T.accw[q] = (ok && a.has_w) ? W[static_cast<long>(i) * a.ld_w + j] * a.decay : 0.f;
+  }
+  }
+}
+
+template <int RH, bool ROWFIX, bool FAST>
+__device__ __forceinline__ void ef_compute_store(const EfArgs& a, const EfBuf& bf, int b, int fbase, int s0, int t,
+                                                 int h, bool zero, const float (&fm)[RH], const float (&fw)[RH],
+                                                 EfTile<RH, ROWFIX>& T) {
+  if (!zero) {
+#pragma unroll
+    for (int s = 0; s < RH; ++s)
+      T.accm = ROWFIX ? __builtin_amdgcn_mfma_f32_32x32x2f32(fm[s], T.sp[s], T.accm, 0, 0, 0)
+                      : __builtin_amdgcn_mfma_f32_32x32x2f32(T.sp[s], fm[s], T.accm, 0, 0, 0);
+  }
+  if (a.has_w && !zero) {
+#pragma unroll
+    for (int s = 0; s < RH; ++s)
+      T.accw = ROWFIX ? __builtin_amdgcn_mfma_f32_32x32x2f32(fw[s], T.sp[s], T.accw, 0, 0, 0)
+                      : __builtin_amdgcn_mfma_f32_32x32x2f32(T.sp[s], fw[s], T.accw, 0, 0, 0);
+  }
+  const int rows = a.rows, cols = a.cols;
+  const int row0 = ROWFIX ? fbase : s0;
+  const int col0 = ROWFIX ? s0 : fbase;
+  if constexpr (FAST) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int rq = row0 + (q & 3) + 8 * (q >> 2);
+      if (!zero) {
+        const int so = __builtin_amdgcn_readfirstlane((rq * static_cast<int>(a.ld_m) + col0) * 4);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(T.accm[q]), bf.m, bf.voff_m, so, 0);
+      }
+      if (a.has_w) {
+        const int so = __builtin_amdgcn_readfirstlane((rq * static_cast<int>(a.ld_w) + col0) * 4);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(T.accw[q]), bf.w, bf.voff_w, so, 0);
+      }
+    }
+    return;
+  } else {
+  float* M = a.m[b];
+  float* W = a.w[b];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    const int j = col0 + t;
+    if (i < rows && j < cols) {
+      if (!zero) M[static_cast<long>(i) * a.ld_m + j] = T.accm[q];
+      if (a.has_w) W[static_cast<long>(i) * a.ld_w + j] = T.accw[q];
+    }
+  }
+  }
+}
+
+template <int RH, bool ROWFIX, bool FAST>
+__device__ __forceinline__ void ef_stream(const EfArgs& a, const EfBuf& bf, int b, int fbase, int s_begin, int s_end,
+                                          int t, int h, bool zero, const float* __restrict__ Pb,
+                                          const float (&fm)[RH], const float (&fw)[RH]) {
+  EfTile<RH, ROWFIX> A, B;
+  ef_load_tile<RH, ROWFIX, FAST>(a, bf, b, fbase, s_begin, t, h, zero, Pb, A);
+  for (int s0 = s_begin; s0 < s_end; s0 += 64) {
+    const bool more = s0 + 32 < s_end;
+    if (more) ef_load_tile<RH, ROWFIX, FAST>(a, bf, b, fbase, s0 + 32, t, h, zero, Pb, B);
+    ef_compute_store<RH, ROWFIX, FAST>(a, bf, b, fbase, s0, t, h, zero, fm, fw, A);
+    if (!more) break;
+    if (s0 + 64 < s_end) ef_load_tile<RH, ROWFIX, FAST>(a, bf, b, fbase, s0 + 64, t, h, zero, Pb, A);
+    ef_compute_store<RH, ROWFIX, FAST>(a, bf, b, fbase, s0 + 32, t, h, zero, fm, fw, B);
+  }
+}
+
+template <int RH, bool ROWFIX, bool FAST>
+__global__ void __launch_bounds__(256, (RH >= 64 ? 1 : 2)) ef_update_kernel(const EfArgs a) {
   const int b = blockIdx.z;
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int t = lane & 31;
   const int h = lane >> 5;
-  const int i0 = blockIdx.y * 64 + (wave >> 1) * 32;
-  const int j0 = blockIdx.x * 128 + (wave & 1) * 64;
   const int rows = a.rows, cols = a.cols, r = a.r;
   const bool zero = (a.nonzero[b] == 0u);
-  const int m_p = a.transposed ? cols : rows;
-  const int n_q = a.transposed ? rows : cols;
+  const int m_p = ROWFIX ? cols : rows;
+  const int n_q = ROWFIX ? rows : cols;
   const float* Pb = a.P + static_cast<long>(b) * m_p * r;
   const float* Rb = a.R + static_cast<long>(b) * n_q * r;
   const float* Qb = a.qn[b];
-  // row factor (indexed by i) and column factor (indexed by j) of each update
-  const float* rowF_m = a.transposed ? Rb : Pb;
-  const float* colF_m = a.transposed ? Pb : Rb;
-  const float* rowF_w = a.transposed ? Qb : Pb;
-  const float* colF_w = a.transposed ? Pb : Qb;
-  const float rs_m = a.transposed ? a.alpha : 1.f, cs_m = a.transposed ? 1.f : a.alpha;
-  const float rs_w = a.transposed ? a.beta : 1.f, cs_w = a.transposed ? 1.f : a.beta;
+  const int fbase = blockIdx.x * 128 + __builtin_amdgcn_readfirstlane(wave) * 32;  // fixed strip
+  const int flen = ROWFIX ? rows : cols;
+  const int s_begin = blockIdx.y * kEfStream;
+  const int s_end = min(ROWFIX ? cols : rows, s_begin + kEfStream);
+  if (fbase >= flen) return;
+  float fm[RH], fw[RH];
+  load_factor<RH>(Rb, fbase + t, n_q, r, h, a.alpha, fm);
+  load_factor<RH>(Qb, fbase + t, n_q, r, h, a.beta, fw);
 
-  for (int pass = 0; pass < 2; ++pass) {
-    if (pass == 0 && zero) continue;          // z: momentum is all zero and stays so
-    if (pass == 1 && !a.has_w) break;
-    float* X = (pass == 0) ? a.m[b] : a.w[b];
-    const long ld = (pass == 0) ? a.ld_m : a.ld_w;
-    float ra[RH];
-    load_factor<RH>(pass == 0 ? rowF_m : rowF_w, i0 + t, rows, r, h, pass == 0 ? rs_m : rs_w, ra);
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int jc = j0 + 32 * cb + t;
-      float ca[RH];
-      load_factor<RH>(pass == 0 ? colF_m : colF_w, jc, cols, r, h, pass == 0 ? cs_m : cs_w, ca);
-      f32x16 acc;
-      const float dscale = (pass == 0) ? 1.f : a.decay;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        acc[q] = (i < rows && jc < cols) ? X[static_cast<long>(i) * ld + jc] * dscale : 0.f;
-      }
-      if (!(pass == 1 && zero)) {
-#pragma unroll
-        for (int s = 0; s < RH; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[s], ca[s], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        if (i < rows && jc < cols) X[static_cast<long>(i) * ld + jc] = acc[q];
-      }
-    }
-  }
+  EfBuf bf;
+  bf.m = __builtin_amdgcn_make_buffer_rsrc(a.m[b], static_cast<short>(0),
+                                           static_cast<int>(min(static_cast<long>(rows) * a.ld_m * 4, 0x7FFFFFF0L)),
+                                           0x00020000);
+  bf.w = __builtin_amdgcn_make_buffer_rsrc(a.has_w ? a.w[b] : a.m[b], static_cast<short>(0),
+                                           static_cast<int>(min(static_cast<long>(rows) * a.ld_w * 4, 0x7FFFFFF0L)),
+                                           0x00020000);
+  bf.voff_m = (4 * h * static_cast<int>(a.ld_m) + t) * 4;
+  bf.voff_w = (4 * h * static_cast<int>(a.ld_w) + t) * 4;
+
+  // FAST: every tile is full (m, n multiples of 32), chosen per launch by the host
+  ef_stream<RH, ROWFIX, FAST>(a, bf, b, fbase, s_begin, s_end, t, h, zero, Pb, fm, fw);
 }
 
 // ============================================================================
@@ -1116,6 +1274,11 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
         n = ortho_plan(mp, d->r, chunk, 2.0f).total;
         break;
       }
+      case DION_OP_FIXUP_COLNORM: {
+        const int nq = d->transposed ? d->m : d->n;
+        n = sizeof(float) * static_cast<size_t>(chunk) * ceil_div(nq, 256) * d->r;
+        break;
+      }
       default:
         return fail(DION_E_INVALID, "unknown op %d", op);
     }
@@ -1234,7 +1397,7 @@ int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, u
 }
 
 int dion_fixup_colnorm(const DionBatchDesc* d, float* P, float* R, float* const* Q, const uint32_t* nonzero,
-                       float eps, dion_stream_t stream) {
+                       float eps, void* ws, size_t ws_bytes, dion_stream_t stream) {
   int rc = validate(d);
   if (rc != DION_OK) return rc;
   if (P == nullptr || R == nullptr || Q == nullptr || nonzero == nullptr)
@@ -1265,8 +1428,16 @@ int dion_fixup_colnorm(const DionBatchDesc* d, float* P, float* R, float* const*
     a.nq = nq;
     a.r = r;
     a.tpc = 256 / r;
+    a.rows_per_chunk = 256;
+    a.nchunk = static_cast<int>(ceil_div(nq, a.rows_per_chunk));
+    if (ws_bytes < sizeof(float) * static_cast<size_t>(nb) * a.nchunk * r || ws == nullptr)
+      return fail(DION_E_WORKSPACE, "fixup needs %zu workspace bytes", sizeof(float) * static_cast<size_t>(nb) * a.nchunk * r);
+    a.part = static_cast<float*>(ws);
     a.eps = eps;
-    hipLaunchKernelGGL(fixup_colnorm_kernel, dim3(nb), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(fixup_partial_kernel, dim3(a.nchunk, nb), dim3(256), 0, st, a);
+    rc = check_launch("fixup_partial");
+    if (rc != DION_OK) return rc;
+    hipLaunchKernelGGL(colnorm_apply_kernel, dim3(a.nchunk, nb), dim3(256), 0, st, a);
     rc = check_launch("fixup_colnorm");
     if (rc != DION_OK) return rc;
   }
@@ -1309,18 +1480,26 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
     a.beta = -scaled_lr;
     a.decay = (wd > 0.f) ? (1.0f - lr * wd) : 1.0f;
     a.has_w = W ? 1 : 0;
-    const dim3 grid(static_cast<unsigned>(ceil_div(d->n, 128)), static_cast<unsigned>(ceil_div(d->m, 64)), nb);
+    const int flen = d->transposed ? d->m : d->n;
+    const int slen = d->transposed ? d->n : d->m;
+    const dim3 grid(static_cast<unsigned>(ceil_div(flen, 128)), static_cast<unsigned>(ceil_div(slen, kEfStream)), nb);
     const int rh = rpad / 2;
-    if (rh <= 4)
-      hipLaunchKernelGGL((ef_update_kernel<4>), grid, dim3(256), 0, st, a);
-    else if (rh <= 8)
-      hipLaunchKernelGGL((ef_update_kernel<8>), grid, dim3(256), 0, st, a);
-    else if (rh <= 16)
-      hipLaunchKernelGGL((ef_update_kernel<16>), grid, dim3(256), 0, st, a);
-    else if (rh <= 32)
-      hipLaunchKernelGGL((ef_update_kernel<32>), grid, dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((ef_update_kernel<64>), grid, dim3(256), 0, st, a);
+    const bool fast = (d->m % 32 == 0) && (d->n % 32 == 0);
+    auto go = [&](auto RHc) {
+      constexpr int RHv = decltype(RHc)::value;
+      if (d->transposed) {
+        if (fast) hipLaunchKernelGGL((ef_update_kernel<RHv, true, true>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((ef_update_kernel<RHv, true, false>), grid, dim3(256), 0, st, a);
+      } else {
+        if (fast) hipLaunchKernelGGL((ef_update_kernel<RHv, false, true>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((ef_update_kernel<RHv, false, false>), grid, dim3(256), 0, st, a);
+      }
+    };
+    if (rh <= 4) go(std::integral_constant<int, 4>{});
+    else if (rh <= 8) go(std::integral_constant<int, 8>{});
+    else if (rh <= 16) go(std::integral_constant<int, 16>{});
+    else if (rh <= 32) go(std::integral_constant<int, 32>{});
+    else go(std::integral_constant<int, 64>{});
     rc = check_launch("ef_update");
     if (rc != DION_OK) return rc;
   }

@@ -138,7 +138,10 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     dev = momentums[0].device
     oversample = float(optimizer.defaults["rcqr_oversample"])
 
-    P = torch.zeros((B, mp, r), dtype=torch.float32, device=dev)
+    # padded entries (and the W > 1 exchange buffers) must read as zero; a full
+    # world-size-1 batch is written completely by the kernels
+    alloc = torch.empty if (W == 1 and real == B) else torch.zeros
+    P = alloc((B, mp, r), dtype=torch.float32, device=dev)
     nonzero = torch.zeros((B,), dtype=torch.int32, device=dev)
     codec.project_p(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed)
 
