@@ -952,6 +952,140 @@ __global__ void __launch_bounds__(256, (RH >= 64 ? 1 : 2)) ef_update_kernel(cons
   ef_stream<RH, ROWFIX, FAST>(a, bf, b, fbase, s_begin, s_end, t, h, zero, Pb, fm, fw);
 }
 
+// ----------------------------------------------------------------------------
+// Fast path of the same update for the common case (m, n multiples of 32,
+// r == 2 RH with r % 4 == 0, ld_w == ld_m, 16-byte aligned factors): all
+// addressing is precomputed -- 16 per-register VGPR offsets shared by M and W,
+// one SGPR tile offset -- so the loop body is loads, MFMAs and stores only.
+// ----------------------------------------------------------------------------
+template <int RH>
+__device__ __forceinline__ void load_factor_vec(const float* __restrict__ F, int idx, int h, float scale,
+                                                float (&v)[RH]) {
+  const float* p = F + static_cast<long>(idx) * (2 * RH) + h * RH;
+#pragma unroll
+  for (int s = 0; s < RH; s += 4) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(p + s);
+    v[s] = x[0] * scale;
+    v[s + 1] = x[1] * scale;
+    v[s + 2] = x[2] * scale;
+    v[s + 3] = x[3] * scale;
+  }
+}
+
+template <int RH, bool ROWFIX, bool DO_M>
+__global__ void __launch_bounds__(256, (RH >= 64 ? 1 : 2)) ef_fast_kernel(const EfArgs a) {
+  const int b = blockIdx.z;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int t = lane & 31;
+  const int h = lane >> 5;
+  const int rows = a.rows, cols = a.cols;
+  const int m_p = ROWFIX ? cols : rows;
+  const int n_q = ROWFIX ? rows : cols;
+  constexpr int r = 2 * RH;
+  // entries whose accumulated momentum is all zero take the DO_M == false
+  // instantiation (host splits nothing: the flag is read here, uniformly)
+  const bool zero = __builtin_amdgcn_readfirstlane(a.nonzero[b]) == 0u;
+  if (DO_M == zero) return;
+  const float* Pb = a.P + static_cast<long>(b) * m_p * r;
+  const float* Rb = a.R + static_cast<long>(b) * n_q * r;
+  const float* Qb = a.qn[b];
+  const int fbase = blockIdx.x * 128 + wave * 32;
+  const int s_begin = blockIdx.y * kEfStream;
+  const int s_end = min(ROWFIX ? cols : rows, s_begin + kEfStream);
+  const int ld = static_cast<int>(a.ld_m);
+  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(
+      a.m[b], static_cast<short>(0), static_cast<int>(min(static_cast<long>(rows) * ld * 4, 0x7FFFFFF0L)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      a.has_w ? a.w[b] : a.m[b], static_cast<short>(0),
+      static_cast<int>(min(static_cast<long>(rows) * ld * 4, 0x7FFFFFF0L)), 0x00020000);
+  int voff[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) voff[q] = (((q & 3) + 8 * (q >> 2) + 4 * h) * ld + t) * 4;
+
+  float fm[RH], fw[RH];
+  if (DO_M) load_factor_vec<RH>(Rb, fbase + t, h, a.alpha, fm);
+  load_factor_vec<RH>(Qb, fbase + t, h, a.beta, fw);
+
+  auto tile_soff = [&](int s0) {
+    const int row0 = ROWFIX ? fbase : s0;
+    const int col0 = ROWFIX ? s0 : fbase;
+    return (row0 * ld + col0) * 4;
+  };
+  float spA[RH], spB[RH];
+  f32x16 mA, wA, mB, wB;
+  auto load = [&](int s0, float (&sp)[RH], f32x16& am, f32x16& aw) {
+    if (DO_M) load_factor_vec<RH>(Pb, s0 + t, h, 1.f, sp);
+    __builtin_amdgcn_sched_barrier(0);
+    const int so = tile_soff(s0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (DO_M) am[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rm, voff[q], so, 0));
+      aw[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, voff[q], so, 0));
+    }
+  };
+  auto compute_store = [&](int s0, const float (&sp)[RH], f32x16& am, f32x16& aw) {
+    const int so = tile_soff(s0);
+    if (DO_M) {
+#pragma unroll
+      for (int s = 0; s < RH; ++s)
+        am = ROWFIX ? __builtin_amdgcn_mfma_f32_32x32x2f32(fm[s], sp[s], am, 0, 0, 0)
+                    : __builtin_amdgcn_mfma_f32_32x32x2f32(sp[s], fm[s], am, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(am[q]), rm, voff[q], so, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) aw[q] *= a.decay;
+    if (DO_M) {
+#pragma unroll
+      for (int s = 0; s < RH; ++s)
+        aw = ROWFIX ? __builtin_amdgcn_mfma_f32_32x32x2f32(fw[s], sp[s], aw, 0, 0, 0)
+                    : __builtin_amdgcn_mfma_f32_32x32x2f32(sp[s], fw[s], aw, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(aw[q]), rw, voff[q], so, 0);
+  };
+
+  // Order per tile: wait for this tile's loads (an empty asm "use" makes the
+  // compiler place the vmcnt wait here), THEN issue the next tile's loads, then
+  // the MFMA chains and stores.  Issuing the next loads first would put them
+  // between this tile's loads and its use, and with the previous tile's 32
+  // stores that exceeds the 6-bit vmcnt window, forcing a full drain.
+  auto touch = [&](const float (&sp)[RH], f32x16& am, f32x16& aw) {
+    if (DO_M) {
+#pragma unroll
+      for (int s = 0; s < RH; ++s) asm volatile("" ::"v"(sp[s]));
+      asm volatile("" ::"v"(am));
+    }
+    asm volatile("" ::"v"(aw));
+  };
+  // The wait for a tile's loads sits at the END of the previous tile's work
+  // (after its stores), never at the loop header, where the waitcnt pass would
+  // merge the prologue state and drain everything.
+  load(s_begin, spA, mA, wA);
+  touch(spA, mA, wA);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int s0 = s_begin; s0 < s_end; s0 += 64) {
+    const bool more = s0 + 32 < s_end;
+    if (more) load(s0 + 32, spB, mB, wB);
+    __builtin_amdgcn_sched_barrier(0);
+    compute_store(s0, spA, mA, wA);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!more) break;
+    touch(spB, mB, wB);
+    __builtin_amdgcn_sched_barrier(0);
+    const bool more2 = s0 + 64 < s_end;
+    if (more2) load(s0 + 64, spA, mA, wA);
+    __builtin_amdgcn_sched_barrier(0);
+    compute_store(s0 + 32, spB, mB, wB);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more2) touch(spA, mA, wA);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // ============================================================================
 // host side
 // ============================================================================
@@ -1484,21 +1618,34 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
     const int slen = d->transposed ? d->n : d->m;
     const dim3 grid(static_cast<unsigned>(ceil_div(flen, 128)), static_cast<unsigned>(ceil_div(slen, kEfStream)), nb);
     const int rh = rpad / 2;
-    const bool fast = (d->m % 32 == 0) && (d->n % 32 == 0);
+    bool fast = (d->m % 32 == 0) && (d->n % 32 == 0) && (r % 4 == 0) && (r % 2 == 0) &&
+                (W == nullptr || ldv(d->ld_w, d->n) == ldv(d->ld_m, d->n)) && aligned16(a.P) && aligned16(a.R) &&
+                ((static_cast<long>(mp) * r) % 4 == 0) && ((static_cast<long>(nq) * r) % 4 == 0);
+    for (int b = 0; b < nb && fast; ++b) fast = aligned16(a.qn[b]);
+    const int rhv = rpad / 2;
+    const bool exact_rh = (rhv == 4 || rhv == 8 || rhv == 16 || rhv == 32 || rhv == 64);
     auto go = [&](auto RHc) {
       constexpr int RHv = decltype(RHc)::value;
-      if (d->transposed) {
-        if (fast) hipLaunchKernelGGL((ef_update_kernel<RHv, true, true>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((ef_update_kernel<RHv, true, false>), grid, dim3(256), 0, st, a);
+      if (fast && exact_rh && 2 * RHv == r) {
+        // two launches over the same grid: entries with a nonzero momentum do EF + W,
+        // all-zero entries only decay W (each block exits early in the other launch)
+        if (d->transposed) {
+          hipLaunchKernelGGL((ef_fast_kernel<RHv, true, true>), grid, dim3(256), 0, st, a);
+          hipLaunchKernelGGL((ef_fast_kernel<RHv, true, false>), grid, dim3(256), 0, st, a);
+        } else {
+          hipLaunchKernelGGL((ef_fast_kernel<RHv, false, true>), grid, dim3(256), 0, st, a);
+          hipLaunchKernelGGL((ef_fast_kernel<RHv, false, false>), grid, dim3(256), 0, st, a);
+        }
+      } else if (d->transposed) {
+        hipLaunchKernelGGL((ef_update_kernel<RHv, true, false>), grid, dim3(256), 0, st, a);
       } else {
-        if (fast) hipLaunchKernelGGL((ef_update_kernel<RHv, false, true>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((ef_update_kernel<RHv, false, false>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((ef_update_kernel<RHv, false, false>), grid, dim3(256), 0, st, a);
       }
     };
-    if (rh <= 4) go(std::integral_constant<int, 4>{});
-    else if (rh <= 8) go(std::integral_constant<int, 8>{});
-    else if (rh <= 16) go(std::integral_constant<int, 16>{});
-    else if (rh <= 32) go(std::integral_constant<int, 32>{});
+    if (rhv <= 4) go(std::integral_constant<int, 4>{});
+    else if (rhv <= 8) go(std::integral_constant<int, 8>{});
+    else if (rhv <= 16) go(std::integral_constant<int, 16>{});
+    else if (rhv <= 32) go(std::integral_constant<int, 32>{});
     else go(std::integral_constant<int, 64>{});
     rc = check_launch("ef_update");
     if (rc != DION_OK) return rc;
