@@ -404,6 +404,324 @@ __global__ void __launch_bounds__(256) colproj_kernel(const ProjArgs a) {
   }
 }
 
+// ============================================================================
+// Fast projections (the Llama-class shapes): no bounds checks, the thin
+// operand staged once per block in LDS, the big operand streamed one K-step
+// ahead in named register sets (no copies, so the prefetch stays in flight).
+// Preconditions (checked on the host): rows % 256 == 0 (row kernel) or
+// cols % 256 == 0 (column kernel), K-chunks aligned to the step, r == 16 RB,
+// row strides multiple of 8 elements, 16-byte aligned pointers.
+// ============================================================================
+template <int GDT>
+struct RowStep {           // 4 row blocks x 8 consecutive columns per lane
+  f32x4 x[4][2];
+  uint4 gb[4];             // bf16 G (8 values)
+  f32x4 gf[4][2];          // f32 G
+};
+
+template <int GDT>
+__device__ __forceinline__ void rp_load(RowStep<GDT>& S, const float* __restrict__ M, const void* __restrict__ G,
+                                        long ld_m, long ld_g, int j) {
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) {
+    const float* p = M + rb * 16 * ld_m + j;
+    S.x[rb][0] = *reinterpret_cast<const f32x4*>(p);
+    S.x[rb][1] = *reinterpret_cast<const f32x4*>(p + 4);
+    if constexpr (GDT == DION_DTYPE_BF16) {
+      S.gb[rb] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(G) + rb * 16 * ld_g + j);
+    } else if constexpr (GDT == DION_DTYPE_F32) {
+      const float* gp = static_cast<const float*>(G) + rb * 16 * ld_g + j;
+      S.gf[rb][0] = *reinterpret_cast<const f32x4*>(gp);
+      S.gf[rb][1] = *reinterpret_cast<const f32x4*>(gp + 4);
+    }
+  }
+}
+
+template <int RB>
+struct TStage {            // this thread's share of the 32 x r thin slice
+  float2 v[RB];
+};
+
+template <int RB>
+__device__ __forceinline__ void rp_tload(TStage<RB>& T, const float* __restrict__ Tp, int j0, int tid) {
+  constexpr int R = 16 * RB;
+  const float* src = Tp + static_cast<long>(j0 + tid / 8) * R + (tid % 8) * 2 * RB;
+#pragma unroll
+  for (int u = 0; u < RB; ++u) T.v[u] = *reinterpret_cast<const float2*>(src + 2 * u);
+}
+
+template <int RB>
+__device__ __forceinline__ void rp_tstore(const TStage<RB>& T, float* tl, int tid) {
+  constexpr int LDT = 16 * RB + 2;
+  float* dst = tl + (tid / 8) * LDT + (tid % 8) * 2 * RB;
+#pragma unroll
+  for (int u = 0; u < RB; ++u) *reinterpret_cast<float2*>(dst + 2 * u) = T.v[u];
+}
+
+template <int RB, int GDT>
+__device__ __forceinline__ void rp_compute(RowStep<GDT>& S, f32x4 (&acc)[4][RB], const float* tl, float* __restrict__ M,
+                                           long ld_m, int j, int g, int t, bool& nz) {
+  constexpr int LDT = 16 * RB + 2;
+  if constexpr (GDT != DION_DTYPE_NONE) {
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      if constexpr (GDT == DION_DTYPE_BF16) {
+        const uint4 gv = S.gb[rb];
+        S.x[rb][0][0] += __uint_as_float(gv.x << 16);
+        S.x[rb][0][1] += __uint_as_float(gv.x & 0xFFFF0000u);
+        S.x[rb][0][2] += __uint_as_float(gv.y << 16);
+        S.x[rb][0][3] += __uint_as_float(gv.y & 0xFFFF0000u);
+        S.x[rb][1][0] += __uint_as_float(gv.z << 16);
+        S.x[rb][1][1] += __uint_as_float(gv.z & 0xFFFF0000u);
+        S.x[rb][1][2] += __uint_as_float(gv.w << 16);
+        S.x[rb][1][3] += __uint_as_float(gv.w & 0xFFFF0000u);
+      } else {
+        S.x[rb][0] += S.gf[rb][0];
+        S.x[rb][1] += S.gf[rb][1];
+      }
+      float* p = M + rb * 16 * ld_m + j;
+      *reinterpret_cast<f32x4*>(p) = S.x[rb][0];
+      *reinterpret_cast<f32x4*>(p + 4) = S.x[rb][1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) nz |= (S.x[rb][0][e] != 0.f) | (S.x[rb][1][e] != 0.f);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      const float bv = tl[(8 * g + s) * LDT + 16 * cb + t];
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+        acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(S.x[rb][s >> 2][s & 3], bv, acc[rb][cb], 0, 0, 0);
+    }
+  }
+}
+
+template <int RB, int GDT>
+__global__ void __launch_bounds__(256, ((RB >= 4 && GDT != DION_DTYPE_NONE) || RB >= 8) ? 1 : 2)
+rowproj_fast_kernel(const ProjArgs a) {
+  constexpr int R = 16 * RB;
+  constexpr int LDT = R + 2;
+  __shared__ __attribute__((aligned(16))) float tl[2][32 * LDT];
+  const int b = blockIdx.z;
+  const int kc = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int row_base = blockIdx.x * 256 + wave * 64;
+  const int j_begin = kc * a.kchunk;
+  const int j_end = min(a.cols, j_begin + a.kchunk);
+  float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 8 * g;
+  const void* G = nullptr;
+  if constexpr (GDT == DION_DTYPE_BF16)
+    G = static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 8 * g;
+  else if constexpr (GDT == DION_DTYPE_F32)
+    G = static_cast<const float*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 8 * g;
+  const float* __restrict__ Tp = a.thin[b];
+
+  f32x4 acc[4][RB];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bool nz = false;
+
+  RowStep<GDT> SA, SB;
+  TStage<RB> TA;
+  rp_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j_begin);
+  rp_tload<RB>(TA, Tp, j_begin, tid);
+  rp_tstore<RB>(TA, tl[0], tid);
+  __syncthreads();
+  int cur = 0;
+  for (int j0 = j_begin; j0 < j_end; j0 += 64) {
+    const bool more = j0 + 32 < j_end;
+    if (more) {
+      rp_load<GDT>(SB, M, G, a.ld_m, a.ld_g, j0 + 32);
+      rp_tload<RB>(TA, Tp, j0 + 32, tid);
+    }
+    rp_compute<RB, GDT>(SA, acc, tl[cur], M, a.ld_m, j0, g, t, nz);
+    if (!more) break;
+    rp_tstore<RB>(TA, tl[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+    const bool more2 = j0 + 64 < j_end;
+    if (more2) {
+      rp_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j0 + 64);
+      rp_tload<RB>(TA, Tp, j0 + 64, tid);
+    }
+    rp_compute<RB, GDT>(SB, acc, tl[cur], M, a.ld_m, j0 + 32, g, t, nz);
+    if (!more2) break;
+    rp_tstore<RB>(TA, tl[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        out[static_cast<long>(row_base + 16 * rb + 4 * g + q) * R + 16 * cb + t] = acc[rb][cb][q];
+  if constexpr (GDT != DION_DTYPE_NONE) {
+    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fast column projection: block = 4 waves x 64 columns; per 16-row step the
+// block stages T[i0:i0+16][0:r] in LDS; each wave streams 16 rows x 64 columns
+// of X (+G, written back) as four 4-row MFMA K-steps, one step ahead.
+// ---------------------------------------------------------------------------
+template <int GDT>
+struct ColStep {
+  f32x4 x[4];
+  uint2 gb[4];
+  f32x4 gf[4];
+};
+
+template <int GDT>
+__device__ __forceinline__ void cp_load(ColStep<GDT>& S, const float* __restrict__ M, const void* __restrict__ G,
+                                        long ld_m, long ld_g, int i0) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    S.x[k] = *reinterpret_cast<const f32x4*>(M + static_cast<long>(i0 + 4 * k) * ld_m);
+    if constexpr (GDT == DION_DTYPE_BF16)
+      S.gb[k] = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(G) + static_cast<long>(i0 + 4 * k) * ld_g);
+    else if constexpr (GDT == DION_DTYPE_F32)
+      S.gf[k] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(G) + static_cast<long>(i0 + 4 * k) * ld_g);
+  }
+}
+
+template <int RB>
+struct CTStage {
+  float v[RB];
+};
+
+template <int RB>
+__device__ __forceinline__ void cp_tload(CTStage<RB>& T, const float* __restrict__ Tp, int i0, int tid) {
+  constexpr int R = 16 * RB;
+  const float* src = Tp + static_cast<long>(i0 + tid / 16) * R + (tid % 16) * RB;
+#pragma unroll
+  for (int u = 0; u < RB; ++u) T.v[u] = src[u];
+}
+
+template <int RB>
+__device__ __forceinline__ void cp_tstore(const CTStage<RB>& T, float* tl, int tid) {
+  constexpr int R = 16 * RB;
+  constexpr int LDT = (R % 32 == 0) ? R + 16 : R + 32;
+  float* dst = tl + (tid / 16) * LDT + (tid % 16) * RB;
+#pragma unroll
+  for (int u = 0; u < RB; ++u) dst[u] = T.v[u];
+}
+
+template <int RB, int GDT>
+__device__ __forceinline__ void cp_compute(ColStep<GDT>& S, f32x4 (&acc)[4][RB], const float* tl, float* __restrict__ M,
+                                           long ld_m, int i0, int g, int t, bool& nz) {
+  constexpr int R = 16 * RB;
+  constexpr int LDT = (R % 32 == 0) ? R + 16 : R + 32;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if constexpr (GDT != DION_DTYPE_NONE) {
+      if constexpr (GDT == DION_DTYPE_BF16) {
+        S.x[k][0] += __uint_as_float(S.gb[k].x << 16);
+        S.x[k][1] += __uint_as_float(S.gb[k].x & 0xFFFF0000u);
+        S.x[k][2] += __uint_as_float(S.gb[k].y << 16);
+        S.x[k][3] += __uint_as_float(S.gb[k].y & 0xFFFF0000u);
+      } else {
+        S.x[k] += S.gf[k];
+      }
+      *reinterpret_cast<f32x4*>(M + static_cast<long>(i0 + 4 * k) * ld_m) = S.x[k];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) nz |= (S.x[k][e] != 0.f);
+    }
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      const float bv = tl[(4 * k + g) * LDT + 16 * cb + t];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc[e][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(S.x[k][e], bv, acc[e][cb], 0, 0, 0);
+    }
+  }
+}
+
+template <int RB, int GDT>
+__global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_fast_kernel(const ProjArgs a) {
+  constexpr int R = 16 * RB;
+  constexpr int LDT = (R % 32 == 0) ? R + 16 : R + 32;
+  __shared__ __attribute__((aligned(16))) float tl[2][16 * LDT];
+  const int b = blockIdx.z;
+  const int kc = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int col_base = blockIdx.x * 256 + wave * 64;
+  const int i_begin = kc * a.kchunk;
+  const int i_end = min(a.rows, i_begin + a.kchunk);
+  float* __restrict__ M = a.m[b] + static_cast<long>(g) * a.ld_m + col_base + 4 * t;
+  const void* G = nullptr;
+  if constexpr (GDT == DION_DTYPE_BF16)
+    G = static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(g) * a.ld_g + col_base + 4 * t;
+  else if constexpr (GDT == DION_DTYPE_F32)
+    G = static_cast<const float*>(a.g[b]) + static_cast<long>(g) * a.ld_g + col_base + 4 * t;
+  const float* __restrict__ Tp = a.thin[b];
+
+  f32x4 acc[4][RB];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[e][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bool nz = false;
+
+  ColStep<GDT> SA, SB;
+  CTStage<RB> TA;
+  cp_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i_begin);
+  cp_tload<RB>(TA, Tp, i_begin, tid);
+  cp_tstore<RB>(TA, tl[0], tid);
+  __syncthreads();
+  int cur = 0;
+  for (int i0 = i_begin; i0 < i_end; i0 += 32) {
+    const bool more = i0 + 16 < i_end;
+    if (more) {
+      cp_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 16);
+      cp_tload<RB>(TA, Tp, i0 + 16, tid);
+    }
+    cp_compute<RB, GDT>(SA, acc, tl[cur], M, a.ld_m, i0, g, t, nz);
+    if (!more) break;
+    cp_tstore<RB>(TA, tl[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+    const bool more2 = i0 + 32 < i_end;
+    if (more2) {
+      cp_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 32);
+      cp_tload<RB>(TA, Tp, i0 + 32, tid);
+    }
+    cp_compute<RB, GDT>(SB, acc, tl[cur], M, a.ld_m, i0 + 16, g, t, nz);
+    if (!more2) break;
+    cp_tstore<RB>(TA, tl[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        out[static_cast<long>(col_base + 4 * (4 * g + q) + e) * R + 16 * cb + t] = acc[e][cb][q];
+  if constexpr (GDT != DION_DTYPE_NONE) {
+    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+  }
+}
+
 // out[b][e] = sum_k slab[b][k][e] in fixed k order.
 __global__ void __launch_bounds__(256) reduce_slabs_kernel(float* __restrict__ out,
                                                            const float* __restrict__ slab, int nchunk,
@@ -991,6 +1309,7 @@ __global__ void __launch_bounds__(256, (RH >= 64 ? 1 : 2)) ef_fast_kernel(const 
   const float* Rb = a.R + static_cast<long>(b) * n_q * r;
   const float* Qb = a.qn[b];
   const int fbase = blockIdx.x * 128 + wave * 32;
+  if (fbase >= (ROWFIX ? rows : cols)) return;  // partial last block: whole waves idle
   const int s_begin = blockIdx.y * kEfStream;
   const int s_end = min(ROWFIX ? cols : rows, s_begin + kEfStream);
   const int ld = static_cast<int>(a.ld_m);
@@ -1122,10 +1441,10 @@ struct Geo {
 
 constexpr int kTargetBlocks = 2048;
 
-// row projection: X rows x cols, reduce over cols
-Geo rowproj_geo(int rows, int cols, int batch) {
+// row projection: X rows x cols, reduce over cols (block_rows 128 generic, 256 fast)
+Geo rowproj_geo(int rows, int cols, int batch, int block_rows = 128) {
   Geo g;
-  g.gx = static_cast<int>(ceil_div(rows, 128));
+  g.gx = static_cast<int>(ceil_div(rows, block_rows));
   long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
   long maxc = ceil_div(cols, 256);
   long nc = want < maxc ? want : maxc;
@@ -1149,6 +1468,9 @@ Geo colproj_geo(int rows, int cols, int batch, bool panel) {
   g.out_rows = cols;
   return g;
 }
+
+bool rowproj_fast_ok(int rows, int cols, int r) { return rows % 256 == 0 && cols % 32 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
+bool colproj_fast_ok(int rows, int cols, int r) { return cols % 256 == 0 && rows % 16 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
 
 size_t slab_bytes(const Geo& g, int batch, int r) {
   return g.nchunk > 1 ? sizeof(float) * static_cast<size_t>(batch) * g.nchunk * g.out_rows * r : 0;
@@ -1228,7 +1550,11 @@ int launch_reduce(float* out, const float* slab, int nchunk, long per_entry, int
 int run_projection(bool row_mode, int rows, int cols, int r, int batch, const void* const* G, float* const* M,
                    const float* const* thin, long ld_m, long ld_g, int gdt, float* out, uint32_t* nonzero,
                    void* ws, size_t ws_bytes, hipStream_t st) {
-  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch) : colproj_geo(rows, cols, batch, false);
+  bool fast = row_mode ? rowproj_fast_ok(rows, cols, r) : colproj_fast_ok(rows, cols, r);
+  fast = fast && (ld_m % 8) == 0 && (gdt == DION_DTYPE_NONE || (ld_g % 8) == 0);
+  for (int b = 0; b < batch && fast; ++b)
+    fast = aligned16(M[b]) && aligned16(thin[b]) && (gdt == DION_DTYPE_NONE || aligned16(G[b]));
+  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, fast ? 256 : 128) : colproj_geo(rows, cols, batch, false);
   const size_t need = slab_bytes(geo, batch, r);
   if (need > ws_bytes || (need > 0 && ws == nullptr))
     return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
@@ -1259,7 +1585,11 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     constexpr int RB = decltype(RBc)::value;
     return dispatch_gdt(gdt, [&](auto Gc) {
       constexpr int GD = decltype(Gc)::value;
-      if (row_mode)
+      if (fast && row_mode)
+        hipLaunchKernelGGL((rowproj_fast_kernel<RB, GD>), grid, dim3(256), 0, st, a);
+      else if (fast)
+        hipLaunchKernelGGL((colproj_fast_kernel<RB, GD>), grid, dim3(256), 0, st, a);
+      else if (row_mode)
         hipLaunchKernelGGL((rowproj_kernel<RB, GD>), grid, dim3(256), 0, st, a);
       else
         hipLaunchKernelGGL((colproj_kernel<RB, GD, 0, 0>), grid, dim3(256), 0, st, a);
@@ -1393,14 +1723,15 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
     if (chunk <= 0) continue;
     size_t n = 0;
     switch (op) {
-      case DION_OP_PROJECT_P: {
-        Geo g = d->transposed ? colproj_geo(d->m, d->n, chunk, false) : rowproj_geo(d->m, d->n, chunk);
-        n = slab_bytes(g, chunk, d->r);
-        break;
-      }
+      case DION_OP_PROJECT_P:
       case DION_OP_PROJECT_R: {
-        Geo g = d->transposed ? rowproj_geo(d->m, d->n, chunk) : colproj_geo(d->m, d->n, chunk, false);
+        const bool row_mode = (op == DION_OP_PROJECT_P) ? !d->transposed : d->transposed;
+        Geo g = row_mode ? rowproj_geo(d->m, d->n, chunk) : colproj_geo(d->m, d->n, chunk, false);
         n = slab_bytes(g, chunk, d->r);
+        if (row_mode) {
+          const size_t nf = slab_bytes(rowproj_geo(d->m, d->n, chunk, 256), chunk, d->r);
+          if (nf > n) n = nf;
+        }
         break;
       }
       case DION_OP_ORTHONORMALIZE: {
