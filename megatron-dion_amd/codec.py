@@ -55,7 +55,7 @@ class HipDionCodec:
     def __init__(self, device: Optional[torch.device] = None):
         self.lib = _lib.load()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self._ws = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self._ws = {}  # per-stream scratch: batches may run concurrently on several streams
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
@@ -78,9 +78,12 @@ class HipDionCodec:
         nbytes = ctypes.c_size_t(0)
         _lib.check(self.lib.dion_workspace_bytes(ctypes.byref(desc), op, ctypes.byref(nbytes)),
                    "dion_workspace_bytes")
-        if nbytes.value > self._ws.numel():
-            self._ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=self.device)
-        return self._ws
+        key = torch.cuda.current_stream(self.device).cuda_stream
+        ws = self._ws.get(key)
+        if ws is None or nbytes.value > ws.numel():
+            ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        return ws
 
     def _check_batch(self, mats: Sequence[torch.Tensor]):
         m, n = mats[0].shape

@@ -408,22 +408,24 @@ __global__ void __launch_bounds__(256) colproj_kernel(const ProjArgs a) {
 // Fast projections (the Llama-class shapes): no bounds checks, the thin
 // operand staged once per block in LDS, the big operand streamed one K-step
 // ahead in named register sets (no copies, so the prefetch stays in flight).
-// Preconditions (checked on the host): rows % 256 == 0 (row kernel) or
+// Preconditions (checked on the host): rows % (64 kRB) == 0 (row kernel) or
 // cols % 256 == 0 (column kernel), K-chunks aligned to the step, r == 16 RB,
 // row strides multiple of 8 elements, 16-byte aligned pointers.
 // ============================================================================
+constexpr int kRB = 2;     // 16-row MFMA blocks per wave in the fast row projection
+
 template <int GDT>
-struct RowStep {           // 4 row blocks x 8 consecutive columns per lane
-  f32x4 x[4][2];
-  uint4 gb[4];             // bf16 G (8 values)
-  f32x4 gf[4][2];          // f32 G
+struct RowStep {           // kRB row blocks x 8 consecutive columns per lane
+  f32x4 x[kRB][2];
+  uint4 gb[kRB];           // bf16 G (8 values)
+  f32x4 gf[kRB][2];        // f32 G
 };
 
 template <int GDT>
 __device__ __forceinline__ void rp_load(RowStep<GDT>& S, const float* __restrict__ M, const void* __restrict__ G,
                                         long ld_m, long ld_g, int j) {
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb) {
+  for (int rb = 0; rb < kRB; ++rb) {
     const float* p = M + rb * 16 * ld_m + j;
     S.x[rb][0] = *reinterpret_cast<const f32x4*>(p);
     S.x[rb][1] = *reinterpret_cast<const f32x4*>(p + 4);
@@ -459,12 +461,12 @@ __device__ __forceinline__ void rp_tstore(const TStage<RB>& T, float* tl, int ti
 }
 
 template <int RB, int GDT>
-__device__ __forceinline__ void rp_compute(RowStep<GDT>& S, f32x4 (&acc)[4][RB], const float* tl, float* __restrict__ M,
-                                           long ld_m, int j, int g, int t, bool& nz) {
+__device__ __forceinline__ void rp_compute(RowStep<GDT>& S, f32x4 (&acc)[kRB][RB], const float* tl,
+                                           float* __restrict__ M, long ld_m, int j, int g, int t, bool& nz) {
   constexpr int LDT = 16 * RB + 2;
   if constexpr (GDT != DION_DTYPE_NONE) {
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) {
+    for (int rb = 0; rb < kRB; ++rb) {
       if constexpr (GDT == DION_DTYPE_BF16) {
         const uint4 gv = S.gb[rb];
         S.x[rb][0][0] += __uint_as_float(gv.x << 16);
@@ -492,15 +494,14 @@ __device__ __forceinline__ void rp_compute(RowStep<GDT>& S, f32x4 (&acc)[4][RB],
     for (int cb = 0; cb < RB; ++cb) {
       const float bv = tl[(8 * g + s) * LDT + 16 * cb + t];
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+      for (int rb = 0; rb < kRB; ++rb)
         acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(S.x[rb][s >> 2][s & 3], bv, acc[rb][cb], 0, 0, 0);
     }
   }
 }
 
 template <int RB, int GDT>
-__global__ void __launch_bounds__(256, ((RB >= 4 && GDT != DION_DTYPE_NONE) || RB >= 8) ? 1 : 2)
-rowproj_fast_kernel(const ProjArgs a) {
+__global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_fast_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int LDT = R + 2;
   __shared__ __attribute__((aligned(16))) float tl[2][32 * LDT];
@@ -511,7 +512,7 @@ rowproj_fast_kernel(const ProjArgs a) {
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
-  const int row_base = blockIdx.x * 256 + wave * 64;
+  const int row_base = blockIdx.x * (64 * kRB) + wave * (16 * kRB);
   const int j_begin = kc * a.kchunk;
   const int j_end = min(a.cols, j_begin + a.kchunk);
   float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 8 * g;
@@ -522,9 +523,9 @@ rowproj_fast_kernel(const ProjArgs a) {
     G = static_cast<const float*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 8 * g;
   const float* __restrict__ Tp = a.thin[b];
 
-  f32x4 acc[4][RB];
+  f32x4 acc[kRB][RB];
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
+  for (int rb = 0; rb < kRB; ++rb)
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
   bool nz = false;
@@ -561,7 +562,7 @@ rowproj_fast_kernel(const ProjArgs a) {
 
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
+  for (int rb = 0; rb < kRB; ++rb)
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb)
 #pragma unroll
@@ -1469,7 +1470,7 @@ Geo colproj_geo(int rows, int cols, int batch, bool panel) {
   return g;
 }
 
-bool rowproj_fast_ok(int rows, int cols, int r) { return rows % 256 == 0 && cols % 32 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
+bool rowproj_fast_ok(int rows, int cols, int r) { return rows % (64 * kRB) == 0 && cols % 32 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
 bool colproj_fast_ok(int rows, int cols, int r) { return cols % 256 == 0 && rows % 16 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
 
 size_t slab_bytes(const Geo& g, int batch, int r) {
@@ -1554,7 +1555,7 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
   fast = fast && (ld_m % 8) == 0 && (gdt == DION_DTYPE_NONE || (ld_g % 8) == 0);
   for (int b = 0; b < batch && fast; ++b)
     fast = aligned16(M[b]) && aligned16(thin[b]) && (gdt == DION_DTYPE_NONE || aligned16(G[b]));
-  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, fast ? 256 : 128) : colproj_geo(rows, cols, batch, false);
+  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, fast ? 64 * kRB : 128) : colproj_geo(rows, cols, batch, false);
   const size_t need = slab_bytes(geo, batch, r);
   if (need > ws_bytes || (need > 0 && ws == nullptr))
     return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
@@ -1729,7 +1730,7 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
         Geo g = row_mode ? rowproj_geo(d->m, d->n, chunk) : colproj_geo(d->m, d->n, chunk, false);
         n = slab_bytes(g, chunk, d->r);
         if (row_mode) {
-          const size_t nf = slab_bytes(rowproj_geo(d->m, d->n, chunk, 256), chunk, d->r);
+          const size_t nf = slab_bytes(rowproj_geo(d->m, d->n, chunk, 64 * kRB), chunk, d->r);
           if (nf > n) n = nf;
         }
         break;

@@ -24,7 +24,7 @@ import torch.distributed as dist
 from torch.optim.optimizer import Optimizer
 
 from .batches import build_dion_batches
-from .runtime import AsyncRuntime, coalesce_local_batches, run_dion_batch_async
+from .runtime import AsyncRuntime, coalesce_local_batches, is_replicated, run_dion_batch_async
 from .state import init_dion_state
 from .types import DionDistMeta, DionMixedPrecisionConfig, DionStepParam
 
@@ -39,7 +39,7 @@ class MegatronDion(Optimizer):
                  elementwise_lr_scale: float = 1.0, scale_mode: str = "spectral",
                  extra_scale_factor: float = 0.2, split_qkv: bool = False, split_linear: bool = False,
                  max_concurrent_tasks: Optional[int] = None, *, codec=None, sketch_seed: int = 0,
-                 coalesce_local: bool = True):
+                 coalesce_local: bool = True, local_streams: int = 2, coalesce_max_entries: int = 16):
         if isinstance(params, (list, tuple)):
             for pg in params:
                 if isinstance(pg, dict) and "wd_mult" in pg:
@@ -70,6 +70,9 @@ class MegatronDion(Optimizer):
         self._step_count = 0
         self._sketch_seed = int(sketch_seed)
         self._coalesce_local = bool(coalesce_local)
+        self._local_streams = max(1, int(local_streams))
+        self._coalesce_max = max(1, int(coalesce_max_entries))
+        self._streams = None
         self._codec = codec
         self._profile_records: List[Tuple[str, float]] = []
 
@@ -89,7 +92,7 @@ class MegatronDion(Optimizer):
         self.is_distributed_mode = True
         self._route_step_params = route_step_params
 
-    def _tasks(self, sketches=None):
+    def _batches(self):
         batches, elementwise = self._route_step_params()
         if elementwise:
             raise RuntimeError(
@@ -97,9 +100,31 @@ class MegatronDion(Optimizer):
                 "non-2D parameters to a separate optimizer")
         self._dion_update_count += sum(int(b.real_batch_size) for b in batches)
         if self._coalesce_local:
-            batches = coalesce_local_batches(batches)
-        for b in batches:
-            yield run_dion_batch_async(self, b, sketches=sketches(b) if sketches else None)
+            batches = coalesce_local_batches(batches, max_entries=self._coalesce_max)
+        return batches
+
+    def _run_local_overlapped(self, batches, sketches) -> bool:
+        """World-size-1 schedule: independent batches alternate over HIP streams, so one
+        batch's latency-bound orthonormalisation overlaps the next batch's streaming passes."""
+        if self._local_streams <= 1 or not torch.cuda.is_available() or not batches:
+            return False
+        if any(is_replicated(b) for b in batches):
+            return False
+        if not all(getattr(b.params[0], "is_cuda", False) for b in batches):
+            return False
+        dev = batches[0].params[0].device
+        if self._streams is None or self._streams[0].device != dev:
+            self._streams = [torch.cuda.Stream(device=dev) for _ in range(self._local_streams)]
+        main = torch.cuda.current_stream(dev)
+        for s in self._streams:
+            s.wait_stream(main)
+        for i, b in enumerate(batches):
+            with torch.cuda.stream(self._streams[i % len(self._streams)]):
+                for _ in run_dion_batch_async(self, b, sketches=sketches(b) if sketches else None):
+                    raise RuntimeError("[DION_INTERNAL] a world-size-1 batch yielded")
+        for s in self._streams:
+            main.wait_stream(s)
+        return True
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -117,7 +142,11 @@ class MegatronDion(Optimizer):
         profile = os.environ.get("DION_PROFILE_SPLIT", "").lower() in ("1", "true", "yes")
         t0 = time.perf_counter() if profile else None
         width = 3 if self.max_concurrent_tasks is None else int(self.max_concurrent_tasks)
-        AsyncRuntime(self._tasks(getattr(self, "_sketch_override", None)), width).run()
+        sketches = getattr(self, "_sketch_override", None)
+        batches = self._batches()
+        if not self._run_local_overlapped(batches, sketches):
+            AsyncRuntime((run_dion_batch_async(self, b, sketches=sketches(b) if sketches else None)
+                          for b in batches), width).run()
         if profile:
             torch.cuda.synchronize()
             self._profile_records.append(("step", time.perf_counter() - t0))

@@ -64,6 +64,11 @@ def _group_world(group) -> int:
     return int(dist.get_world_size(group))
 
 
+def is_replicated(batch) -> bool:
+    """True when the batch exchanges factors with replicas (replicate group size > 1)."""
+    return _group_world(getattr(getattr(batch, "batch_group", None), "replicate_group", None)) > 1
+
+
 def validate_update_contract(optimizer, *, optim_groups, optimizer_states, dist_metas, param_shapes,
                              real_batch_size: int) -> None:
     """All real entries of a batch must share shape, lr, rank_fraction, wd, mu and r."""
