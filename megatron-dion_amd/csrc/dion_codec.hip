@@ -1407,6 +1407,168 @@ __global__ void __launch_bounds__(256, (RH >= 64 ? 1 : 2)) ef_fast_kernel(const 
 }
 
 // ============================================================================
+// Rank-r update with split-bf16 MFMA ("bf16x6"), the production EF / weight path:
+//   X = decay * X + U,   U = sum_c A[i][c] B[j][c]   (one update per launch:
+//   M with (P, -(1-mu) R), then W with (P, -s Qn) -- separate launches keep one
+//   fixed factor per kernel, so the registers allow two waves per SIMD).
+// Each fp32 factor value is split exactly into hi + mid + lo bf16 pieces
+// (x - bf16(x) is exact in fp32) and U accumulates the six products
+// hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid on v_mfma_f32_32x32x16_bf16
+// (dropped terms are below 2^-25 relative: fp32-level accuracy at 16/6 times
+// the f32-MFMA rate).  U is accumulated from zero and added to decay * X at the
+// end, the reference's order (kernels.py:54-83: X*beta + alpha*(A B^T);
+// runtime.py:1110-1113: W*(1-lr wd) then add).
+// Geometry as ef_fast_kernel: a wave keeps the fixed factor of a 32-wide strip
+// (pre-split in registers) and streams 32 x 32 tiles along the other side.
+// ============================================================================
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+struct RankArgs {
+  float* x[MAXB];            // M or W per matrix
+  const float* fixed[MAXB];  // factor indexed by the fixed strip (R_b or Qn_b)
+  const float* S;            // streamed factor base: P (batch, len, r)
+  const uint32_t* nonzero;
+  long s_stride;             // elements between consecutive P_b
+  int rows, cols;
+  long ld;
+  float scale;               // applied to the fixed factor
+  float decay;               // X multiplier (1 for M)
+  int skip_zero;             // 1: entries with an all-zero momentum are left untouched
+};
+
+struct Split3 {
+  bf16x8 hi, mid, lo;
+};
+
+__device__ __forceinline__ void split3(const f32x4& a, const f32x4& b, float scale, Split3& o) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = (j < 4 ? a[j] : b[j - 4]) * scale;
+    const __bf16 h = static_cast<__bf16>(x);
+    const float r1 = x - static_cast<float>(h);
+    const __bf16 m = static_cast<__bf16>(r1);
+    const float r2 = r1 - static_cast<float>(m);
+    o.hi[j] = h;
+    o.mid[j] = m;
+    o.lo[j] = static_cast<__bf16>(r2);
+  }
+}
+
+__device__ __forceinline__ f32x16 mfma6(const Split3& A, const Split3& B, f32x16 acc) {
+  // smallest terms first
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.mid, B.mid, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.lo, B.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.hi, B.lo, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.mid, B.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.hi, B.mid, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.hi, B.hi, acc, 0, 0, 0);
+  return acc;
+}
+
+template <int RU>
+struct RTile {
+  f32x4 s[RU][2];  // streamed factor row: 8 consecutive values per k-step
+  f32x16 x;        // X tile (accumulator layout)
+};
+
+template <int RU, bool ROWFIX>
+__global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const RankArgs a) {
+  constexpr int R = 16 * RU;
+  const int b = blockIdx.z;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int t = lane & 31;
+  const int h = lane >> 5;
+  const int rows = a.rows, cols = a.cols;
+  if (a.skip_zero && __builtin_amdgcn_readfirstlane(a.nonzero[b]) == 0u) return;
+  const int fbase = blockIdx.x * 128 + wave * 32;
+  if (fbase >= (ROWFIX ? rows : cols)) return;
+  const int s_begin = blockIdx.y * kEfStream;
+  const int s_end = min(ROWFIX ? cols : rows, s_begin + kEfStream);
+  const int ld = static_cast<int>(a.ld);
+  const float* Sb = a.S + static_cast<long>(b) * a.s_stride;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      a.x[b], static_cast<short>(0), static_cast<int>(min(static_cast<long>(rows) * ld * 4, 0x7FFFFFF0L)), 0x00020000);
+  int voff[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) voff[q] = (((q & 3) + 8 * (q >> 2) + 4 * h) * ld + t) * 4;
+
+  // fixed factor of this lane's strip index, split once
+  Split3 F[RU];
+  {
+    const float* fp = a.fixed[b] + static_cast<long>(fbase + t) * R + 8 * h;
+#pragma unroll
+    for (int u = 0; u < RU; ++u)
+      split3(*reinterpret_cast<const f32x4*>(fp + 16 * u), *reinterpret_cast<const f32x4*>(fp + 16 * u + 4),
+             a.scale, F[u]);
+  }
+
+  auto load = [&](int s0, RTile<RU>& T) {
+    const float* sp = Sb + static_cast<long>(s0 + t) * R + 8 * h;
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      T.s[u][0] = *reinterpret_cast<const f32x4*>(sp + 16 * u);
+      T.s[u][1] = *reinterpret_cast<const f32x4*>(sp + 16 * u + 4);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int row0 = ROWFIX ? fbase : s0;
+    const int col0 = ROWFIX ? s0 : fbase;
+    const int so = (row0 * ld + col0) * 4;
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      T.x[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff[q], so, 0));
+  };
+  auto compute = [&](int s0, RTile<RU>& T) {
+    f32x16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      Split3 Sp;
+      split3(T.s[u][0], T.s[u][1], 1.f, Sp);
+      acc = ROWFIX ? mfma6(F[u], Sp, acc) : mfma6(Sp, F[u], acc);
+    }
+    const int row0 = ROWFIX ? fbase : s0;
+    const int col0 = ROWFIX ? s0 : fbase;
+    const int so = (row0 * ld + col0) * 4;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float v = T.x[q] * a.decay + acc[q];
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[q], so, 0);
+    }
+  };
+  auto touch_s = [&](RTile<RU>& T) {
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      asm volatile("" ::"v"(T.s[u][0]));
+      asm volatile("" ::"v"(T.s[u][1]));
+    }
+  };
+
+  RTile<RU> A, B;
+  load(s_begin, A);
+  touch_s(A);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int s0 = s_begin; s0 < s_end; s0 += 64) {
+    const bool more = s0 + 32 < s_end;
+    if (more) load(s0 + 32, B);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(s0, A);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!more) break;
+    touch_s(B);
+    __builtin_amdgcn_sched_barrier(0);
+    const bool more2 = s0 + 64 < s_end;
+    if (more2) load(s0 + 64, A);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(s0 + 32, B);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more2) touch_s(A);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// ============================================================================
 // host side
 // ============================================================================
 namespace {
@@ -1950,6 +2112,53 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
     const int slen = d->transposed ? d->n : d->m;
     const dim3 grid(static_cast<unsigned>(ceil_div(flen, 128)), static_cast<unsigned>(ceil_div(slen, kEfStream)), nb);
     const int rh = rpad / 2;
+    bool split_ok = (d->m % 32 == 0) && (d->n % 32 == 0) && (r % 16 == 0) && r <= 128 &&
+                    aligned16(a.P) && aligned16(a.R) && (ldv(d->ld_m, d->n) % 4 == 0) &&
+                    (W == nullptr || ldv(d->ld_w, d->n) % 4 == 0);
+    for (int b = 0; b < nb && split_ok; ++b) split_ok = aligned16(a.qn[b]);
+    if (split_ok) {
+      const int flen = d->transposed ? d->m : d->n;
+      const int slen = d->transposed ? d->n : d->m;
+      const dim3 grid(static_cast<unsigned>(ceil_div(flen, 128)), static_cast<unsigned>(ceil_div(slen, kEfStream)), nb);
+      for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1 && W == nullptr) break;
+        RankArgs ra;
+        memset(&ra, 0, sizeof(ra));
+        for (int b = 0; b < nb; ++b) {
+          ra.x[b] = pass == 0 ? a.m[b] : a.w[b];
+          ra.fixed[b] = pass == 0 ? a.R + static_cast<long>(b) * nq * r : a.qn[b];
+        }
+        ra.S = a.P;
+        ra.s_stride = static_cast<long>(mp) * r;
+        ra.nonzero = a.nonzero;
+        ra.rows = d->m;
+        ra.cols = d->n;
+        ra.ld = pass == 0 ? a.ld_m : a.ld_w;
+        ra.scale = pass == 0 ? a.alpha : a.beta;
+        ra.decay = pass == 0 ? 1.0f : a.decay;
+        ra.skip_zero = pass == 0 ? 1 : 0;
+        auto launch = [&](auto RUc) {
+          constexpr int RUv = decltype(RUc)::value;
+          if (d->transposed)
+            hipLaunchKernelGGL((rank_update_kernel<RUv, true>), grid, dim3(256), 0, st, ra);
+          else
+            hipLaunchKernelGGL((rank_update_kernel<RUv, false>), grid, dim3(256), 0, st, ra);
+        };
+        switch (r / 16) {
+          case 1: launch(std::integral_constant<int, 1>{}); break;
+          case 2: launch(std::integral_constant<int, 2>{}); break;
+          case 3: launch(std::integral_constant<int, 3>{}); break;
+          case 4: launch(std::integral_constant<int, 4>{}); break;
+          case 5: launch(std::integral_constant<int, 5>{}); break;
+          case 6: launch(std::integral_constant<int, 6>{}); break;
+          case 7: launch(std::integral_constant<int, 7>{}); break;
+          default: launch(std::integral_constant<int, 8>{}); break;
+        }
+        rc = check_launch("rank_update");
+        if (rc != DION_OK) return rc;
+      }
+      continue;
+    }
     bool fast = (d->m % 32 == 0) && (d->n % 32 == 0) && (r % 4 == 0) && (r % 2 == 0) &&
                 (W == nullptr || ldv(d->ld_w, d->n) == ldv(d->ld_m, d->n)) && aligned16(a.P) && aligned16(a.R) &&
                 ((static_cast<long>(mp) * r) % 4 == 0) && ((static_cast<long>(nq) * r) % 4 == 0);
