@@ -114,6 +114,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--layers", type=int, default=32, help="Llama-3-8B has 32; fewer only for debugging")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=2, help="HIP streams for independent batches (N=1 path)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -139,7 +140,7 @@ def main():
         named.append((name, w))
     codec = TimedCodec(HipDionCodec(dev))
     opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=1 / 64,
-                           codec=codec)
+                           codec=codec, local_streams=args.streams)
     attach_dp_routing(opt, named, replicate_group=group)
     elems = sum(m * n for _, m, n in shapes)
 
