@@ -975,6 +975,182 @@ __global__ void __launch_bounds__(256) triinv_kernel(const float* __restrict__ U
 }
 
 // ============================================================================
+// Small-factor kernels of the randomised Cholesky QR, one block per matrix.
+//
+// sketch_qr_inv_kernel: Householder QR (LAPACK dgeqr2/dlarfg sign convention)
+//   of the K x r sketch product S P held in REGISTERS -- lane l owns rows
+//   l + 64 s (s < RPL), wave w owns columns w + 4 cc (cc < CPW, cyclic, so the
+//   triangular work stays balanced).  Per pivot j the owning wave forms the
+//   reflector, publishes v and tau through LDS (double-buffered) and every wave
+//   updates its own columns with wave-level reductions: one barrier per pivot.
+//   A wave's consumed pivot column is shifted out so every register index is
+//   static.  Then R^-1 is formed in LDS (tri_inverse_lds) and written out.
+// chol_inv_kernel: upper Cholesky (dpotf2 order) of the r x r Gram matrix with
+//   one lane per column, then its inverse the same way.  A non-positive pivot
+//   poisons the inverse's columns from that pivot on with NaN (cholesky_ex
+//   does not raise; the fix-up's nan_to_num then zeroes those P columns).
+// ============================================================================
+template <typename XT>
+__device__ void tri_inverse_lds(const float* Rs, int rld, XT* Xs, int r, int tid) {
+  // X = R^-1 (upper): lane c = tid computes column c by back substitution;
+  // R is read by broadcast, X columns are lane-contiguous (conflict-free)
+  if (tid < r) {
+    const int c = tid;
+    for (int i = r - 1; i >= 0; --i) {
+      double acc = (i == c) ? 1.0 : 0.0;
+      for (int k = i + 1; k < r; ++k)
+        acc -= static_cast<double>(Rs[i * rld + k]) * static_cast<double>(Xs[k * r + c]);
+      Xs[i * r + c] = static_cast<XT>(acc / static_cast<double>(Rs[i * rld + i]));
+    }
+  }
+}
+
+template <int RPL, int CPW, typename XT>
+__global__ void __launch_bounds__(256) sketch_qr_inv_kernel(const float* __restrict__ SP, float* __restrict__ Rinv,
+                                                            int K, int r) {
+  extern __shared__ __attribute__((aligned(16))) char qsm[];
+  const int rld = r + 1;
+  float* vbuf = reinterpret_cast<float*>(qsm);         // 2 x 256
+  float* tsc = vbuf + 512;                             // 2 (+pad)
+  float* Rs = tsc + 8;                                 // r x rld
+  XT* Xs = reinterpret_cast<XT*>(qsm + ((sizeof(float) * (520 + r * rld) + 15) / 16) * 16);
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float* A0 = SP + static_cast<long>(b) * K * r;
+  for (int idx = tid; idx < r * rld; idx += blockDim.x) Rs[idx] = 0.f;
+  float A[RPL][CPW];
+#pragma unroll
+  for (int s = 0; s < RPL; ++s)
+#pragma unroll
+    for (int cc = 0; cc < CPW; ++cc) {
+      const int row = lane + 64 * s, col = w + 4 * cc;
+      A[s][cc] = (row < K && col < r) ? A0[static_cast<long>(row) * r + col] : 0.f;
+    }
+  const int n_w = (r > w) ? (r - w + 3) / 4 : 0;
+  int consumed = 0;
+  __syncthreads();
+  for (int j = 0; j < r; ++j) {
+    const int buf = j & 1;
+    if ((j & 3) == w) {
+      float xs[RPL];
+      float ss = 0.f;
+      float alpha_l = 0.f;
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) {
+        const int row = lane + 64 * s;
+        xs[s] = A[s][0];
+        if (row > j) ss += xs[s] * xs[s];
+        if (s == (j >> 6)) alpha_l = xs[s];
+      }
+      ss = wave_sum(ss);
+      const float alpha = __shfl(alpha_l, j & 63, 64);
+      const float xnorm = sqrtf(ss);
+      float tau, beta, scale;
+      if (xnorm == 0.f) {
+        tau = 0.f;
+        beta = alpha;
+        scale = 1.f;
+      } else {
+        beta = -copysignf(hypotf(alpha, xnorm), alpha);
+        tau = (beta - alpha) / beta;
+        scale = 1.f / (alpha - beta);
+      }
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) {
+        const int row = lane + 64 * s;
+        vbuf[buf * 256 + row] = (row > j) ? xs[s] * scale : (row == j ? 1.f : 0.f);
+        if (row < j) Rs[row * rld + j] = xs[s];
+        else if (row == j) Rs[row * rld + j] = beta;
+      }
+      if (lane == 0) tsc[buf] = tau;
+#pragma unroll
+      for (int s = 0; s < RPL; ++s) {
+#pragma unroll
+        for (int cc = 0; cc + 1 < CPW; ++cc) A[s][cc] = A[s][cc + 1];
+        A[s][CPW - 1] = 0.f;
+      }
+      ++consumed;
+    }
+    __syncthreads();
+    const float tau = tsc[buf];
+    float v[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; ++s) v[s] = vbuf[buf * 256 + lane + 64 * s];
+    const int rem = n_w - consumed;
+#pragma unroll
+    for (int cc = 0; cc < CPW; ++cc) {
+      if (cc < rem) {
+        float d = 0.f;
+#pragma unroll
+        for (int s = 0; s < RPL; ++s) d += v[s] * A[s][cc];
+        d = wave_sum(d) * tau;
+#pragma unroll
+        for (int s = 0; s < RPL; ++s) A[s][cc] -= d * v[s];
+      }
+    }
+  }
+  __syncthreads();
+  tri_inverse_lds<XT>(Rs, rld, Xs, r, tid);
+  __syncthreads();
+  float* O = Rinv + static_cast<long>(b) * r * r;
+  for (int idx = tid; idx < r * r; idx += blockDim.x) O[idx] = static_cast<float>(Xs[idx]);
+}
+
+template <typename XT>
+__global__ void __launch_bounds__(256) chol_inv_kernel(const float* __restrict__ G_in, float* __restrict__ Uinv,
+                                                       int r) {
+  extern __shared__ __attribute__((aligned(16))) char csm[];
+  const int ld = r + 1;
+  float* Us = reinterpret_cast<float*>(csm);       // r x ld
+  float* bc = Us + r * ld;                          // pivot broadcast (+pad)
+  XT* Xs = reinterpret_cast<XT*>(csm + ((sizeof(float) * (r * ld + 4) + 15) / 16) * 16);
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* Gm = G_in + static_cast<long>(b) * r * r;
+  for (int idx = tid; idx < r * r; idx += blockDim.x) {
+    const int i = idx / r, c = idx - i * r;
+    Us[i * ld + c] = Gm[idx];
+  }
+  __syncthreads();
+  int jf = r;
+  for (int j = 0; j < r; ++j) {
+    float sacc = 0.f;
+    if (tid < r && tid >= j) {
+      sacc = Us[j * ld + tid];
+      for (int k = 0; k < j; ++k) sacc -= Us[k * ld + j] * Us[k * ld + tid];
+    }
+    if (tid == j) bc[0] = sacc;
+    __syncthreads();
+    const float d = bc[0];
+    if (!(d > 0.f)) {  // uniform
+      jf = j;
+      break;
+    }
+    const float ujj = sqrtf(d);
+    const float inv = 1.f / ujj;
+    if (tid < r && tid > j) Us[j * ld + tid] = sacc * inv;
+    if (tid == j) Us[j * ld + j] = ujj;
+    __syncthreads();
+  }
+  // zero the strictly lower part, keep the factored rows
+  for (int idx = tid; idx < r * r; idx += blockDim.x) {
+    const int i = idx / r, c = idx - i * r;
+    if (i > c) Us[i * ld + c] = 0.f;
+    if (i >= jf && i <= c) Us[i * ld + c] = (i == c) ? 1.f : 0.f;  // placeholder rows, poisoned below
+  }
+  __syncthreads();
+  tri_inverse_lds<XT>(Us, ld, Xs, r, tid);
+  __syncthreads();
+  float* O = Uinv + static_cast<long>(b) * r * r;
+  for (int idx = tid; idx < r * r; idx += blockDim.x) {
+    const int c = idx % r;
+    O[idx] = (c >= jf) ? __builtin_nanf("") : static_cast<float>(Xs[idx]);
+  }
+}
+
+// ============================================================================
 // Fix-up + column normalisation + Q commit, one block per matrix.
 //   R <- z ? nan_to_num(Q) : nan_to_num(R);  Q <- R / (sqrt(sum_rows R^2) + eps)
 // Threads are grouped per column (tpc threads per column, fixed-order tree
@@ -1831,6 +2007,49 @@ int launch_triinv(const float* U, float* Uinv, int r, int batch, hipStream_t st)
   return check_launch("triinv");
 }
 
+int launch_sketch_qr_inv(const float* SP, float* Rinv, int K, int r, int batch, hipStream_t st) {
+  if (K > 256 || r > 128 || r > K) return fail(DION_E_UNSUPPORTED, "sketch QR %dx%d", K, r);
+  const bool dbl = r <= 64;
+  const size_t lds = ((sizeof(float) * (520 + static_cast<size_t>(r) * (r + 1)) + 15) / 16) * 16 +
+                     (dbl ? sizeof(double) : sizeof(float)) * static_cast<size_t>(r) * r;
+  auto go = [&](auto RPLc, auto CPWc, auto XTc) {
+    constexpr int RPLv = decltype(RPLc)::value;
+    constexpr int CPWv = decltype(CPWc)::value;
+    using XTv = typename decltype(XTc)::type;
+    int rc = allow_lds(sketch_qr_inv_kernel<RPLv, CPWv, XTv>, lds);
+    if (rc != DION_OK) return rc;
+    hipLaunchKernelGGL((sketch_qr_inv_kernel<RPLv, CPWv, XTv>), dim3(batch), dim3(256), lds, st, SP, Rinv, K, r);
+    return check_launch("sketch_qr_inv");
+  };
+  struct D { using type = double; };
+  struct F { using type = float; };
+  if (K <= 128) {
+    if (r <= 16) return go(std::integral_constant<int, 2>{}, std::integral_constant<int, 4>{}, D{});
+    if (r <= 32) return go(std::integral_constant<int, 2>{}, std::integral_constant<int, 8>{}, D{});
+    if (r <= 64) return go(std::integral_constant<int, 2>{}, std::integral_constant<int, 16>{}, D{});
+    return go(std::integral_constant<int, 2>{}, std::integral_constant<int, 32>{}, F{});
+  }
+  if (r <= 64) return go(std::integral_constant<int, 4>{}, std::integral_constant<int, 16>{}, D{});
+  return go(std::integral_constant<int, 4>{}, std::integral_constant<int, 32>{}, F{});
+}
+
+int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t st) {
+  const bool dbl = r <= 96;
+  const size_t lds = ((sizeof(float) * (static_cast<size_t>(r) * (r + 1) + 4) + 15) / 16) * 16 +
+                     (dbl ? sizeof(double) : sizeof(float)) * static_cast<size_t>(r) * r;
+  const int threads = r <= 64 ? 64 : (r <= 128 ? 128 : 256);
+  if (dbl) {
+    int rc = allow_lds(chol_inv_kernel<double>, lds);
+    if (rc != DION_OK) return rc;
+    hipLaunchKernelGGL((chol_inv_kernel<double>), dim3(batch), dim3(threads), lds, st, G, Uinv, r);
+  } else {
+    int rc = allow_lds(chol_inv_kernel<float>, lds);
+    if (rc != DION_OK) return rc;
+    hipLaunchKernelGGL((chol_inv_kernel<float>), dim3(batch), dim3(threads), lds, st, G, Uinv, r);
+  }
+  return check_launch("chol_inv");
+}
+
 // dst_b = src_b Uinv_b for every matrix (m_P x r times r x r), an MFMA row projection
 int apply_right(const float* src, float* dst, const float* Uinv, int mp, int r, int batch, hipStream_t st) {
   const Geo geo = rowproj_geo(mp, r, batch);
@@ -1998,26 +2217,21 @@ int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, u
     rc = run_panel(sketch ? 1 : 2, mp, K, r, nb, Pb, sketch ? sketch + static_cast<long>(b0) * K * mp : nullptr,
                    seed + 0x9E3779B97F4A7C15ull * static_cast<uint64_t>(b0), std_, sp, sk_slab, plan.sk, st);
     if (rc != DION_OK) return rc;
-    // (2) R1 = qr(S P).R
-    hipLaunchKernelGGL(householder_qr_kernel, dim3(nb), dim3(256), lds, st, sp, r1, nullptr, K, r, 0);
-    rc = check_launch("householder_qr(R)");
-    if (rc != DION_OK) return rc;
     float* uinv = reinterpret_cast<float*>(base + plan.off_inv);
     float* p1 = reinterpret_cast<float*>(base + plan.off_p1);
-    // (3) P1 = P R1^-1  (into workspace)
-    rc = launch_triinv(r1, uinv, r, nb, st);
+    // (2) R1^-1 with R1 = qr(S P).R, (3) P1 = P R1^-1  (into workspace)
+    rc = launch_sketch_qr_inv(sp, uinv, K, r, nb, st);
     if (rc != DION_OK) return rc;
+    (void)r1;
     rc = apply_right(Pb, p1, uinv, mp, r, nb, st);
     if (rc != DION_OK) return rc;
     // (4) Gram = P1^T P1, (5) R2 = chol_upper(Gram)
     rc = run_panel(0, mp, r, r, nb, p1, nullptr, 0, 0.f, gm, gslab, plan.gr, st);
     if (rc != DION_OK) return rc;
-    hipLaunchKernelGGL(cholesky_kernel, dim3(nb), dim3(256), sizeof(float) * (r * (r + 1) + 4), st, gm, r2, r);
-    rc = check_launch("cholesky");
+    // (5) R2^-1 with R2 = chol_upper(Gram), (6) P = P1 R2^-1  (back into the caller's buffer)
+    rc = launch_chol_inv(gm, uinv, r, nb, st);
     if (rc != DION_OK) return rc;
-    // (6) P = P1 R2^-1  (back into the caller's buffer)
-    rc = launch_triinv(r2, uinv, r, nb, st);
-    if (rc != DION_OK) return rc;
+    (void)r2;
     rc = apply_right(p1, Pb, uinv, mp, r, nb, st);
     if (rc != DION_OK) return rc;
   }
