@@ -39,8 +39,18 @@ def llama_shapes(layers):
     return [(f"layers.{i}.{n}.weight", m, k) for i in range(layers) for n, m, k in LLAMA3_8B_LAYER]
 
 
+# kernel instance behind each (codec call, orientation) on the Llama set (r = 64 -> RB = RU = 4);
+# ef_apply is two launches of the same instance (M, then W), each streaming 8 B per element
+KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
+             ("project_p", True): ("colproj_fast_kernel<4, 2>", 1),
+             ("project_r", False): ("colproj_fast_kernel<4, 0>", 1),
+             ("project_r", True): ("rowproj_fast_kernel<4, 0>", 1),
+             ("ef_apply", False): ("rank_update_kernel<4, false>", 2),
+             ("ef_apply", True): ("rank_update_kernel<4, true>", 2)}
+
+
 class TimedCodec:
-    """Wraps the HIP codec; records HIP events around each call on the launch stream."""
+    """Wraps the HIP codec; records HIP events around each call on the stream it launches on."""
 
     def __init__(self, inner):
         self.inner = inner
@@ -62,10 +72,11 @@ class TimedCodec:
             out = fn(*args, **kwargs)
             e.record(stream)
             elems = 0
+            transposed = bool(args[-1]) if item in BYTES_PER_ELEM else None
             if item in BYTES_PER_ELEM:
                 mats = args[1] if item == "project_p" else args[0]
                 elems = sum(int(t.numel()) for t in mats)
-            self.events.setdefault(item, []).append((s, e, elems))
+            self.events.setdefault((item, transposed), []).append((s, e, elems))
             return out
 
         return wrapped
@@ -75,8 +86,19 @@ class TimedCodec:
         for k, lst in self.events.items():
             ms = [s.elapsed_time(e) for s, e, _ in lst]
             elems = sum(n for _, _, n in lst)
-            out[k] = {"calls": len(lst), "total_ms": sum(ms), "avg_ms": sum(ms) / len(ms), "elems": elems}
+            out[k] = {"calls": len(lst), "total_ms": sum(ms), "elems": elems}
         return out
+
+
+def load_pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC pass (scripts/pmc_traffic.py), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            data = json.load(f)
+        return data["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def cpu_baseline(sample_layers=1, steps=1):
@@ -107,6 +129,29 @@ def cpu_baseline(sample_layers=1, steps=1):
                       f"r=64, best of {steps} step(s), {best:.2f} s, torch CPU fp32 with {cores} threads"}
 
 
+def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps):
+    """`roofline` of the dominant kernel (most probe time) + every kernel's rate + the step-level view."""
+    dominant = max(per_kernel, key=lambda k: per_kernel[k]["ms"])
+    d = per_kernel[dominant]
+    avg_launch_ms = d["ms"] / d["launches"]
+    bytes_per_launch = d["bytes"] / d["launches"]
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    traffic = load_pmc_traffic(dominant)
+    step_bytes = sum(BYTES_PER_ELEM.values()) * elems
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None if traffic is None else round(traffic),
+                "kernel": dominant, "bytes_per_launch": round(bytes_per_launch),
+                "avg_launch_ms": round(avg_launch_ms, 4), "probe_steps": probe_steps,
+                "kernels": {k: {"avg_launch_ms": round(v["ms"] / v["launches"], 4),
+                                "GB/s": round(v["bytes"] / v["launches"] / (v["ms"] / v["launches"] * 1e-3) / 1e9, 1)}
+                            for k, v in per_kernel.items()},
+                "step": {"algorithmic_bytes": step_bytes,
+                         "achieved": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                         "frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+    return roofline
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -115,6 +160,7 @@ def main():
     ap.add_argument("--layers", type=int, default=32, help="Llama-3-8B has 32; fewer only for debugging")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams for independent batches (N=1 path)")
+    ap.add_argument("--probe-steps", type=int, default=2, help="single-stream steps timed per kernel for `roofline`")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -150,7 +196,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    codec.enabled = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         opt.step()
@@ -159,7 +204,6 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    codec.enabled = False
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -167,15 +211,29 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = world * elems * 2 / (elapsed / args.steps) / 2 ** 30
 
+    # Roofline probe: a few extra steps on ONE stream (not part of `value`), HIP events around
+    # every codec call, so each kernel's duration is its own and not its share of a concurrent
+    # pair; `scripts/gpu_prof.sh` profiles the same single-stream configuration with rocprofv3.
+    opt._local_streams = 1
+    codec.enabled = True
+    for _ in range(args.probe_steps):
+        opt.step()
+    torch.cuda.synchronize()
+    codec.enabled = False
+    opt._local_streams = args.streams
     summ = codec.summary()
-    dominant = max(summ, key=lambda k: summ[k]["total_ms"])
-    d = summ[dominant]
-    bytes_per_launch = BYTES_PER_ELEM.get(dominant, 0.0) * d["elems"] / d["calls"]
-    achieved = bytes_per_launch / (d["avg_ms"] * 1e-3) / 1e9
-    roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(d["avg_ms"], 4),
-                "per_call_ms": {k: round(v["total_ms"] / args.steps, 3) for k, v in summ.items()}}
+    per_kernel = {}
+    for key, v in summ.items():
+        if key not in KERNEL_OF:
+            continue
+        kname, launches_per_call = KERNEL_OF[key]
+        agg = per_kernel.setdefault(kname, {"ms": 0.0, "bytes": 0.0, "launches": 0})
+        agg["ms"] += v["total_ms"]
+        agg["bytes"] += BYTES_PER_ELEM[key[0]] * v["elems"]
+        agg["launches"] += v["calls"] * launches_per_call
+    roofline = None
+    if per_kernel:
+        roofline = kernel_roofline(per_kernel, elems, ms_per_step, args.probe_steps)
 
     out = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,

@@ -218,6 +218,9 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
             if commit_updates[i] is not None:
                 commit_updates[i](params[i], momentums[i])
     optimizer._last_batch_factors = (P, R) if getattr(optimizer, "_keep_factors", False) else None
+    sink = getattr(optimizer, "_factor_sink", None)
+    if sink is not None:  # the compressed factors leaving the device (scripts/e2e_pcie.py)
+        sink(P[:real], R[:real])
 
 
 def run_dion_batch_async(optimizer, batch, sketches=None) -> Generator[None, None, None]:
