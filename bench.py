@@ -31,8 +31,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 LLAMA3_8B_LAYER = (("linear_qkv", 6144, 4096), ("linear_proj", 4096, 4096),
                    ("linear_fc1", 28672, 4096), ("linear_fc2", 4096, 14336))
 
-# algorithmic HBM bytes per matrix element of each codec call (DESIGN.md "bytes per unit")
-BYTES_PER_ELEM = {"project_p": 10.0, "project_r": 4.0, "ef_apply": 16.0}
+# algorithmic HBM bytes per matrix element of each codec call (DESIGN.md "bytes per unit");
+# "ef_apply_w" is the weight-only update of the deferred-EF schedule
+BYTES_PER_ELEM = {"project_p": 10.0, "project_p_ef": 10.0, "project_r": 4.0, "ef_apply": 16.0, "ef_apply_w": 8.0}
 
 
 def llama_shapes(layers):
@@ -43,8 +44,12 @@ def llama_shapes(layers):
 # ef_apply is two launches of the same instance (M, then W), each streaming 8 B per element
 KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("project_p", True): ("colproj_fast_kernel<4, 2>", 1),
-             ("project_r", False): ("colproj_fast_kernel<4, 0>", 1),
-             ("project_r", True): ("rowproj_fast_kernel<4, 0>", 1),
+             ("project_p_ef", False): ("rowproj_ef_kernel<4, 2>", 1),
+             ("project_p_ef", True): ("colproj_ef_kernel<4, 2>", 1),
+             ("ef_apply_w", False): ("rank_update_kernel<4, false>", 1),
+             ("ef_apply_w", True): ("rank_update_kernel<4, true>", 1),
+             ("project_r", False): ("colproj_x6_kernel<4>", 1),
+             ("project_r", True): ("rowproj_x6_kernel<4>", 1),
              ("ef_apply", False): ("rank_update_kernel<4, false>", 2),
              ("ef_apply", True): ("rank_update_kernel<4, true>", 2)}
 
@@ -60,7 +65,7 @@ class TimedCodec:
 
     def __getattr__(self, item):
         fn = getattr(self.inner, item)
-        if item not in ("project_p", "orthonormalize", "project_r", "fixup_colnorm", "ef_apply"):
+        if item not in ("project_p", "project_p_ef", "orthonormalize", "project_r", "fixup_colnorm", "ef_apply"):
             return fn
 
         def wrapped(*args, **kwargs):
@@ -72,11 +77,16 @@ class TimedCodec:
             out = fn(*args, **kwargs)
             e.record(stream)
             elems = 0
-            transposed = bool(args[-1]) if item in BYTES_PER_ELEM else None
-            if item in BYTES_PER_ELEM:
-                mats = args[1] if item == "project_p" else args[0]
+            key = item
+            if item == "ef_apply" and args[0] is None:
+                key = "ef_apply_w"
+            transposed = None
+            if key in BYTES_PER_ELEM:
+                transposed = bool(args[5] if item == "project_p_ef" else args[-1])
+                mats = args[1] if item in ("project_p", "project_p_ef") else (args[0] if args[0] is not None
+                                                                              else args[1])
                 elems = sum(int(t.numel()) for t in mats)
-            self.events.setdefault((item, transposed), []).append((s, e, elems))
+            self.events.setdefault((key, transposed), []).append((s, e, elems))
             return out
 
         return wrapped
@@ -129,7 +139,7 @@ def cpu_baseline(sample_layers=1, steps=1):
                       f"r=64, best of {steps} step(s), {best:.2f} s, torch CPU fp32 with {cores} threads"}
 
 
-def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps):
+def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps, deferred):
     """`roofline` of the dominant kernel (most probe time) + every kernel's rate + the step-level view."""
     dominant = max(per_kernel, key=lambda k: per_kernel[k]["ms"])
     d = per_kernel[dominant]
@@ -137,7 +147,9 @@ def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps):
     bytes_per_launch = d["bytes"] / d["launches"]
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
     traffic = load_pmc_traffic(dominant)
-    step_bytes = sum(BYTES_PER_ELEM.values()) * elems
+    # the schedule's own bytes: 30 B/elem eager, 22 B/elem with the deferred error feedback
+    # (the EF's M read + write rides on pass A)
+    step_bytes = (22.0 if deferred else 30.0) * elems
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else round(traffic),
@@ -148,7 +160,8 @@ def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps):
                             for k, v in per_kernel.items()},
                 "step": {"algorithmic_bytes": step_bytes,
                          "achieved": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
-                         "frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+                         "frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "eager_equivalent_GBps": round(30.0 * elems / (ms_per_step * 1e-3) / 1e9, 1)}}
     return roofline
 
 
@@ -161,6 +174,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams for independent batches (N=1 path)")
     ap.add_argument("--probe-steps", type=int, default=2, help="single-stream steps timed per kernel for `roofline`")
+    ap.add_argument("--eager-ef", action="store_true",
+                    help="apply each step's error feedback in its own pass (default: deferred into the next pass A)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -186,7 +201,7 @@ def main():
         named.append((name, w))
     codec = TimedCodec(HipDionCodec(dev))
     opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=1 / 64,
-                           codec=codec, local_streams=args.streams)
+                           codec=codec, local_streams=args.streams, defer_error_feedback=not args.eager_ef)
     attach_dp_routing(opt, named, replicate_group=group)
     elems = sum(m * n for _, m, n in shapes)
 
@@ -233,7 +248,7 @@ def main():
         agg["launches"] += v["calls"] * launches_per_call
     roofline = None
     if per_kernel:
-        roofline = kernel_roofline(per_kernel, elems, ms_per_step, args.probe_steps)
+        roofline = kernel_roofline(per_kernel, elems, ms_per_step, args.probe_steps, not args.eager_ef)
 
     out = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
@@ -241,6 +256,7 @@ def main():
            "data": "synthetic (random-init Llama-3-8B 2D weight shapes, bf16 grads N(0,1e-3^2))",
            "config": {"workload": "llama3-8b-2d-grad-set-r64", "matrices": len(shapes), "grad_elements": elems,
                       "rank": 64, "grad_dtype": "bf16", "state_dtype": "f32",
+                      "error_feedback": "eager" if args.eager_ef else "deferred (applied in the next step's pass A)",
                       "parallelism": f"dp{world} (replicate, low-rank P/R exchange)" if world > 1 else "dp1"},
            "roofline": roofline}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

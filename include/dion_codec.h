@@ -35,7 +35,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 2
+#define DION_ABI_VERSION 3
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -52,6 +52,7 @@ typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 #define DION_OP_ORTHONORMALIZE 2
 #define DION_OP_PROJECT_R 3
 #define DION_OP_FIXUP_COLNORM 4
+#define DION_OP_PROJECT_P_EF 5 /* DION_E_UNSUPPORTED: no fused kernel for this shape */
 
 typedef struct DionBatchDesc {
   int32_t batch;      /* matrices in this call (all the same shape)            */
@@ -86,6 +87,28 @@ int dion_workspace_bytes(const DionBatchDesc* desc, int op, size_t* bytes);
 int dion_project_p(const DionBatchDesc* desc, const void* const* G, float* const* M,
                    const float* const* Q, float* P, uint32_t* nonzero, void* ws,
                    size_t ws_bytes, dion_stream_t stream);
+
+/* The previous step's error feedback, not yet applied to M (see dion_project_p_ef). */
+typedef struct DionPendingEF {
+  const float* const* P; /* per matrix: its m_P x r factor P_b of the previous step, or NULL */
+  const float* const* R; /* per matrix: its n_Q x r factor R_b of the previous step, or NULL */
+  float alpha;           /* -(1 - mu) of that step */
+} DionPendingEF;
+
+/*
+ * Pass A with the previous step's error feedback folded in ("deferred EF"):
+ *   M_b <- (M_b + alpha (P_b R_b^T or R_b P_b^T)) + G_b ;  P = X_b Q_b ;  nonzero
+ * for every entry whose pending factors are non-NULL (the rest as dion_project_p).
+ * Same sums, same order as the eager schedule (error feedback of step t,
+ * kernels.py:54-154, then M += G of step t+1, runtime.py:1560-1566), but the
+ * momentum is read and written once instead of twice.  Returns
+ * DION_E_UNSUPPORTED (and enqueues nothing) for shapes without the fused kernel
+ * (query: dion_workspace_bytes(desc, DION_OP_PROJECT_P_EF, ...)); the caller then
+ * applies the pending EF with dion_ef_apply(W = NULL) and calls dion_project_p.
+ */
+int dion_project_p_ef(const DionBatchDesc* desc, const void* const* G, float* const* M,
+                      const float* const* Q, float* P, uint32_t* nonzero, const DionPendingEF* ef,
+                      void* ws, size_t ws_bytes, dion_stream_t stream);
 
 /*
  * Randomised Cholesky QR of every P_b (m_P x r), in place
@@ -124,7 +147,9 @@ int dion_fixup_colnorm(const DionBatchDesc* desc, float* P, float* R, float* con
  *   M_b += -(1-mu) * (P_b R_b^T  or  R_b P_b^T when transposed)
  *   W_b  = (wd > 0 ? (1 - lr*wd) : 1) * W_b - scaled_lr * (P_b Qn_b^T or Qn_b P_b^T)
  * Qn_b is the committed Q (output of dion_fixup_colnorm).  W may be NULL
- * (error feedback only).  Entries with nonzero[b] == 0 keep M and only decay W.
+ * (error feedback only); M may be NULL (weight update only, the deferred-EF
+ * schedule; DION_E_UNSUPPORTED for shapes without the rank-update kernel).
+ * Entries with nonzero[b] == 0 keep M and only decay W.
  */
 int dion_ef_apply(const DionBatchDesc* desc, float* const* M, float* const* W,
                   const float* P, const float* R, const float* const* Qn,

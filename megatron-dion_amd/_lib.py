@@ -11,7 +11,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "csrc", "libdion_codec.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -27,6 +27,7 @@ OP_PROJECT_P = 1
 OP_ORTHONORMALIZE = 2
 OP_PROJECT_R = 3
 OP_FIXUP_COLNORM = 4
+OP_PROJECT_P_EF = 5
 
 # every symbol include/dion_codec.h declares
 EXPORTED = (
@@ -34,6 +35,7 @@ EXPORTED = (
     "dion_last_error",
     "dion_workspace_bytes",
     "dion_project_p",
+    "dion_project_p_ef",
     "dion_orthonormalize",
     "dion_project_r",
     "dion_fixup_colnorm",
@@ -61,6 +63,11 @@ class DionBatchDesc(ctypes.Structure):
     ]
 
 
+class DionPendingEF(ctypes.Structure):
+    _fields_ = [("P", ctypes.POINTER(ctypes.c_void_p)), ("R", ctypes.POINTER(ctypes.c_void_p)),
+                ("alpha", ctypes.c_float)]
+
+
 _P = ctypes.c_void_p
 _PP = ctypes.POINTER(ctypes.c_void_p)
 _DESC = ctypes.POINTER(DionBatchDesc)
@@ -70,6 +77,8 @@ _SIGNATURES = {
     "dion_last_error": ([], ctypes.c_char_p),
     "dion_workspace_bytes": ([_DESC, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "dion_project_p": ([_DESC, _PP, _PP, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "dion_project_p_ef": ([_DESC, _PP, _PP, _PP, _P, _P, ctypes.POINTER(DionPendingEF), _P, ctypes.c_size_t, _P],
+                          ctypes.c_int),
     "dion_orthonormalize": ([_DESC, _P, _P, ctypes.c_uint64, ctypes.c_float, _P, ctypes.c_size_t, _P],
                             ctypes.c_int),
     "dion_project_r": ([_DESC, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),

@@ -56,6 +56,7 @@ class HipDionCodec:
         self.lib = _lib.load()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self._ws = {}  # per-stream scratch: batches may run concurrently on several streams
+        self._ef_ok = {}
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
@@ -113,6 +114,45 @@ class HipDionCodec:
                                      ws.numel(), self._stream())
         _lib.check(rc, "dion_project_p")
 
+    def supports_deferred_ef(self, m: int, n: int, r: int, transposed: bool) -> bool:
+        """True when the fused deferred-EF pass A exists for this shape (dion_project_p_ef)."""
+        key = (int(m), int(n), int(r), bool(transposed))
+        ok = self._ef_ok.get(key)
+        if ok is None:
+            d = self._desc(1, m, n, r, transposed)
+            nbytes = ctypes.c_size_t(0)
+            ok = self.lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P_EF, ctypes.byref(nbytes)) == 0
+            self._ef_ok[key] = ok
+        return ok
+
+    def project_p_ef(self, grads: Optional[List[torch.Tensor]], momentums: List[torch.Tensor],
+                     qs: List[torch.Tensor], P: torch.Tensor, nonzero: torch.Tensor, transposed: bool,
+                     ef_P: Sequence[Optional[torch.Tensor]], ef_R: Sequence[Optional[torch.Tensor]],
+                     alpha: float) -> None:
+        """M += alpha P' R'^T (pending error feedback of the previous step), M += G, P = X Q."""
+        B = len(momentums)
+        if B == 0:
+            return
+        m, n = self._check_batch(momentums)
+        r = int(qs[0].shape[1])
+        g0 = grads[0] if grads else None
+        if grads:
+            for g in grads:
+                if g.dtype != g0.dtype or tuple(g.shape) != (m, n) or g.stride() != g0.stride():
+                    raise RuntimeError("[DION_INCONSISTENT_GRADS]")
+        for t in list(ef_P) + list(ef_R):
+            if t is not None and (not t.is_contiguous() or t.dtype != torch.float32 or t.device != self.device):
+                raise RuntimeError(f"[DION_BAD_FACTOR] pending factor {tuple(t.shape)} {t.dtype} {t.stride()}")
+        d = self._desc(B, m, n, r, transposed, g=g0, M=momentums[0])
+        ws = self.workspace(d, _lib.OP_PROJECT_P_EF)
+        pp, rr = _ptrs(ef_P), _ptrs(ef_R)
+        ef = _lib.DionPendingEF(ctypes.cast(pp, ctypes.POINTER(ctypes.c_void_p)),
+                                ctypes.cast(rr, ctypes.POINTER(ctypes.c_void_p)), float(alpha))
+        rc = self.lib.dion_project_p_ef(ctypes.byref(d), _ptrs(grads) if grads else None, _ptrs(momentums),
+                                        _ptrs(qs), P.data_ptr(), nonzero.data_ptr(), ctypes.byref(ef),
+                                        ws.data_ptr(), ws.numel(), self._stream())
+        _lib.check(rc, "dion_project_p_ef")
+
     def orthonormalize(self, P: torch.Tensor, m: int, n: int, transposed: bool, seed: int,
                        oversample: float = 1.25, sketch: Optional[torch.Tensor] = None) -> None:
         """Randomised Cholesky QR of every P_b in place.  ortho.py:71-123."""
@@ -155,19 +195,28 @@ class HipDionCodec:
                                          self._stream())
         _lib.check(rc, "dion_fixup_colnorm")
 
-    def ef_apply(self, momentums: List[torch.Tensor], params: Optional[List[torch.Tensor]],
+    def ef_apply(self, momentums: Optional[List[torch.Tensor]], params: Optional[List[torch.Tensor]],
                  P: torch.Tensor, R: torch.Tensor, qs: List[torch.Tensor], nonzero: torch.Tensor,
                  mu: float, lr: float, wd: float, scaled_lr: float, transposed: bool) -> None:
-        """Error feedback and weight update.  kernels.py:54-154, runtime.py:1105-1113."""
-        B = len(momentums)
+        """Error feedback and weight update.  kernels.py:54-154, runtime.py:1105-1113.
+
+        `momentums=None` updates the weights only (deferred-EF schedule); `params=None`
+        applies the error feedback only."""
+        B = len(qs)
         if B == 0:
             return
-        m, n = self._check_batch(momentums)
+        if momentums is None and params is None:
+            raise RuntimeError("[DION_INTERNAL] ef_apply needs momentums or params")
+        m, n = self._check_batch(momentums if momentums is not None else params)
         if params is not None:
             self._check_batch(params)
         r = int(P.shape[2])
-        d = self._desc(B, m, n, r, transposed, M=momentums[0], W=params[0] if params else None)
-        rc = self.lib.dion_ef_apply(ctypes.byref(d), _ptrs(momentums), _ptrs(params) if params else None,
+        if not (P.is_contiguous() and R.is_contiguous()):
+            raise RuntimeError("[DION_BAD_FACTOR] P and R must be contiguous (batch, rows, r)")
+        d = self._desc(B, m, n, r, transposed, M=momentums[0] if momentums else None,
+                       W=params[0] if params else None)
+        rc = self.lib.dion_ef_apply(ctypes.byref(d), _ptrs(momentums) if momentums else None,
+                                    _ptrs(params) if params else None,
                                     P.data_ptr(), R.data_ptr(), _ptrs(qs), nonzero.data_ptr(), float(mu),
                                     float(lr), float(wd), float(scaled_lr), self._stream())
         _lib.check(rc, "dion_ef_apply")

@@ -37,6 +37,7 @@
 
 #include "../../include/dion_codec.h"
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -1745,6 +1746,694 @@ __global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const
 }
 
 // ============================================================================
+// Pass A with the previous step's error feedback folded in ("deferred EF").
+//   X = (M + alpha P'_b R'_b^T) + G      (transposed: alpha R'_b P'_b^T)
+//   M <- X ;  P = X Q  (or X^T Q) ;  nonzero flag
+// P'_b, R'_b are the previous step's factors of matrix b (after the fix-up);
+// alpha = -(1 - mu).  The sum order is the reference's: the step-t error
+// feedback lands on M before the step-(t+1) gradient (kernels.py:54-83 then
+// runtime.py:1560-1566), so M matches the eager schedule.  Saves the M read +
+// write of the separate error-feedback launch (8 of the 30 B per element).
+// The EF product is split-bf16 (bf16x6) on v_mfma_f32_16x16x32_bf16, laid out
+// so its accumulator is exactly the lane's slice of the M tile; the
+// projection stays fp32 MFMA.  The streamed factor rows (R' for the row
+// kernel, R' rows for the column kernel) are split once per block per step
+// into LDS; the wave's fixed factor is split once into registers.
+// ============================================================================
+struct EfProjArgs {
+  ProjArgs p;
+  const float* efp[MAXB];  // pending P'_b (m_P x r) or null (no pending EF for b)
+  const float* efr[MAXB];  // pending R'_b (n_Q x r)
+  float alpha;
+};
+
+__device__ __forceinline__ f32x4 mfma6_16(const Split3& A, const Split3& B, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A.mid, B.mid, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A.lo, B.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A.hi, B.lo, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A.mid, B.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A.hi, B.mid, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A.hi, B.hi, acc, 0, 0, 0);
+  return acc;
+}
+
+// streamed EF factor rows of one step: NROW16 x 16 rows by KK x 32 columns, one
+// 8-value run per item, split into [row16][kk][part][lane] bf16x8 in LDS
+template <int NROW16, int KK>
+struct EfStage {
+  static constexpr int kItems = NROW16 * KK * 64;
+  static constexpr int kPer = (kItems + 255) / 256;
+  f32x4 v[kPer][2];
+};
+
+template <int NROW16, int KK>
+__device__ __forceinline__ void ef_sload(EfStage<NROW16, KK>& E, const float* __restrict__ F, int row0, int tid) {
+  constexpr int R = 32 * KK;
+#pragma unroll
+  for (int it = 0; it < EfStage<NROW16, KK>::kPer; ++it) {
+    const int item = tid + 256 * it;
+    if (item < EfStage<NROW16, KK>::kItems) {
+      const int ck = item >> 6, ln = item & 63;
+      const int c = ck / KK, kk = ck - c * KK;
+      const float* src = F + static_cast<long>(row0 + 16 * c + (ln & 15)) * R + 32 * kk + 8 * (ln >> 4);
+      E.v[it][0] = *reinterpret_cast<const f32x4*>(src);
+      E.v[it][1] = *reinterpret_cast<const f32x4*>(src + 4);
+    }
+  }
+}
+
+template <int NROW16, int KK>
+__device__ __forceinline__ void ef_sstore(const EfStage<NROW16, KK>& E, bf16x8* rs, int tid) {
+#pragma unroll
+  for (int it = 0; it < EfStage<NROW16, KK>::kPer; ++it) {
+    const int item = tid + 256 * it;
+    if (item < EfStage<NROW16, KK>::kItems) {
+      const int ck = item >> 6, ln = item & 63;
+      Split3 sp;
+      split3(E.v[it][0], E.v[it][1], 1.f, sp);
+      rs[(ck * 3 + 0) * 64 + ln] = sp.hi;
+      rs[(ck * 3 + 1) * 64 + ln] = sp.mid;
+      rs[(ck * 3 + 2) * 64 + ln] = sp.lo;
+    }
+  }
+}
+
+__device__ __forceinline__ void ef_sread(const bf16x8* rs, int ck, int lane, Split3& A) {
+  A.hi = rs[(ck * 3 + 0) * 64 + lane];
+  A.mid = rs[(ck * 3 + 1) * 64 + lane];
+  A.lo = rs[(ck * 3 + 2) * 64 + lane];
+}
+
+// ---- row kernel (not transposed): wave = 2 x 16 rows, step = 32 columns;
+// lane (t, g) holds columns 16c + 4g .. +3 (c = 0, 1) of rows 16 rb + t.
+template <int GDT>
+struct RowStepE {
+  f32x4 x[kRB][2];
+  uint2 gb[kRB][2];
+  f32x4 gf[kRB][2];
+};
+
+template <int GDT>
+__device__ __forceinline__ void rpe_load(RowStepE<GDT>& S, const float* __restrict__ M, const void* __restrict__ G,
+                                         long ld_m, long ld_g, int j) {
+#pragma unroll
+  for (int rb = 0; rb < kRB; ++rb)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      S.x[rb][c] = *reinterpret_cast<const f32x4*>(M + rb * 16 * ld_m + j + 16 * c);
+      if constexpr (GDT == DION_DTYPE_BF16)
+        S.gb[rb][c] = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(G) + rb * 16 * ld_g + j + 16 * c);
+      else if constexpr (GDT == DION_DTYPE_F32)
+        S.gf[rb][c] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(G) + rb * 16 * ld_g + j + 16 * c);
+    }
+}
+
+template <int RB>
+__device__ __forceinline__ void rpe_tstore(const TStage<RB>& T, float* tl, int tid) {
+  constexpr int LDT = 16 * RB + 4;
+  float* dst = tl + (tid / 8) * LDT + (tid % 8) * 2 * RB;
+#pragma unroll
+  for (int u = 0; u < RB; ++u) *reinterpret_cast<float2*>(dst + 2 * u) = T.v[u];
+}
+
+template <int RB, int GDT>
+__device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRB][RB], const float* tl,
+                                            const bf16x8* rs, const Split3 (&F)[kRB][RB / 2], bool has_ef,
+                                            float* __restrict__ M, long ld_m, int j, int g, int t, int lane,
+                                            bool& nz) {
+  constexpr int KK = RB / 2;
+  constexpr int LDT = 16 * RB + 4;
+  if (has_ef) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 e[kRB];
+#pragma unroll
+      for (int rb = 0; rb < kRB; ++rb) e[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        Split3 A;
+        ef_sread(rs, c * KK + kk, lane, A);
+#pragma unroll
+        for (int rb = 0; rb < kRB; ++rb) e[rb] = mfma6_16(A, F[rb][kk], e[rb]);
+      }
+#pragma unroll
+      for (int rb = 0; rb < kRB; ++rb) S.x[rb][c] += e[rb];
+    }
+  }
+  if (GDT != DION_DTYPE_NONE || has_ef) {
+#pragma unroll
+    for (int rb = 0; rb < kRB; ++rb)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        if constexpr (GDT == DION_DTYPE_BF16) {
+          const uint2 gv = S.gb[rb][c];
+          S.x[rb][c][0] += __uint_as_float(gv.x << 16);
+          S.x[rb][c][1] += __uint_as_float(gv.x & 0xFFFF0000u);
+          S.x[rb][c][2] += __uint_as_float(gv.y << 16);
+          S.x[rb][c][3] += __uint_as_float(gv.y & 0xFFFF0000u);
+        } else if constexpr (GDT == DION_DTYPE_F32) {
+          S.x[rb][c] += S.gf[rb][c];
+        }
+        *reinterpret_cast<f32x4*>(M + rb * 16 * ld_m + j + 16 * c) = S.x[rb][c];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nz |= (S.x[rb][c][q] != 0.f);
+      }
+  }
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int col = 16 * (s >> 2) + 4 * g + (s & 3);
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      const float bv = tl[col * LDT + 16 * cb + t];
+#pragma unroll
+      for (int rb = 0; rb < kRB; ++rb)
+        acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(S.x[rb][s >> 2][s & 3], bv, acc[rb][cb], 0, 0, 0);
+    }
+  }
+}
+
+template <int RB, int GDT>
+__global__ void __launch_bounds__(256, 2) rowproj_ef_kernel(const EfProjArgs e) {
+  constexpr int R = 16 * RB;
+  constexpr int KK = RB / 2;
+  constexpr int LDT = R + 4;
+  __shared__ __attribute__((aligned(16))) float tl[2][32 * LDT];
+  __shared__ bf16x8 rs[2][2 * KK * 3 * 64];
+  const ProjArgs& a = e.p;
+  const int b = blockIdx.z;
+  const int kc = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int row_base = blockIdx.x * (64 * kRB) + wave * (16 * kRB);
+  const int j_begin = kc * a.kchunk;
+  const int j_end = min(a.cols, j_begin + a.kchunk);
+  float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 4 * g;
+  const void* G = nullptr;
+  if constexpr (GDT == DION_DTYPE_BF16)
+    G = static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 4 * g;
+  else if constexpr (GDT == DION_DTYPE_F32)
+    G = static_cast<const float*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 4 * g;
+  const float* __restrict__ Tp = a.thin[b];
+  const float* __restrict__ Rp = e.efr[b];
+  const bool has_ef = Rp != nullptr;
+
+  Split3 F[kRB][KK];
+  if (has_ef) {
+#pragma unroll
+    for (int rb = 0; rb < kRB; ++rb)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const float* src = e.efp[b] + static_cast<long>(row_base + 16 * rb + t) * R + 32 * kk + 8 * g;
+        split3(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), e.alpha, F[rb][kk]);
+      }
+  } else {
+#pragma unroll
+    for (int rb = 0; rb < kRB; ++rb)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) F[rb][kk] = Split3{};
+  }
+
+  f32x4 acc[kRB][RB];
+#pragma unroll
+  for (int rb = 0; rb < kRB; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bool nz = false;
+
+  RowStepE<GDT> SA, SB;
+  TStage<RB> TA;
+  EfStage<2, KK> EA;
+  rpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j_begin);
+  rp_tload<RB>(TA, Tp, j_begin, tid);
+  rpe_tstore<RB>(TA, tl[0], tid);
+  if (has_ef) {
+    ef_sload<2, KK>(EA, Rp, j_begin, tid);
+    ef_sstore<2, KK>(EA, rs[0], tid);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int j0 = j_begin; j0 < j_end; j0 += 64) {
+    const bool more = j0 + 32 < j_end;
+    if (more) {
+      rpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, j0 + 32);
+      rp_tload<RB>(TA, Tp, j0 + 32, tid);
+      if (has_ef) ef_sload<2, KK>(EA, Rp, j0 + 32, tid);
+    }
+    rpe_compute<RB, GDT>(SA, acc, tl[cur], rs[cur], F, has_ef, M, a.ld_m, j0, g, t, lane, nz);
+    if (!more) break;
+    rpe_tstore<RB>(TA, tl[cur ^ 1], tid);
+    if (has_ef) ef_sstore<2, KK>(EA, rs[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+    const bool more2 = j0 + 64 < j_end;
+    if (more2) {
+      rpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j0 + 64);
+      rp_tload<RB>(TA, Tp, j0 + 64, tid);
+      if (has_ef) ef_sload<2, KK>(EA, Rp, j0 + 64, tid);
+    }
+    rpe_compute<RB, GDT>(SB, acc, tl[cur], rs[cur], F, has_ef, M, a.ld_m, j0 + 32, g, t, lane, nz);
+    if (!more2) break;
+    rpe_tstore<RB>(TA, tl[cur ^ 1], tid);
+    if (has_ef) ef_sstore<2, KK>(EA, rs[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int rb = 0; rb < kRB; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        out[static_cast<long>(row_base + 16 * rb + 4 * g + q) * R + 16 * cb + t] = acc[rb][cb][q];
+  if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+}
+
+// ---- column kernel (transposed): block = 4 waves x 32 columns, step = 16 rows;
+// lane (t, g) holds columns 2t, 2t + 1 of rows 4g + q (q = 0..3).
+template <int GDT>
+struct ColStepE {
+  f32x2 x[4];
+  uint32_t gb[4];
+  f32x2 gf[4];
+};
+
+template <int GDT>
+__device__ __forceinline__ void cpe_load(ColStepE<GDT>& S, const float* __restrict__ M, const void* __restrict__ G,
+                                         long ld_m, long ld_g, int i0) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    S.x[q] = *reinterpret_cast<const f32x2*>(M + static_cast<long>(i0 + q) * ld_m);
+    if constexpr (GDT == DION_DTYPE_BF16)
+      S.gb[q] = *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(G) + static_cast<long>(i0 + q) * ld_g);
+    else if constexpr (GDT == DION_DTYPE_F32)
+      S.gf[q] = *reinterpret_cast<const f32x2*>(static_cast<const float*>(G) + static_cast<long>(i0 + q) * ld_g);
+  }
+}
+
+template <int RB>
+__device__ __forceinline__ void cpe_tstore(const CTStage<RB>& T, float* tl, int tid) {
+  constexpr int LDT = 16 * RB + 4;
+  float* dst = tl + (tid / 16) * LDT + (tid % 16) * RB;
+#pragma unroll
+  for (int u = 0; u < RB; ++u) dst[u] = T.v[u];
+}
+
+template <int RB, int GDT>
+__device__ __forceinline__ void cpe_compute(ColStepE<GDT>& S, f32x4 (&acc)[2][RB], const float* tl,
+                                            const bf16x8* rs, const Split3 (&F)[2][RB / 2], bool has_ef,
+                                            float* __restrict__ M, long ld_m, int i0, int g, int t, int lane,
+                                            bool& nz) {
+  constexpr int KK = RB / 2;
+  constexpr int LDT = 16 * RB + 4;
+  if (has_ef) {
+    f32x4 e[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      Split3 A;
+      ef_sread(rs, kk, lane, A);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) e[c] = mfma6_16(A, F[c][kk], e[c]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      S.x[q][0] += e[0][q];
+      S.x[q][1] += e[1][q];
+    }
+  }
+  if (GDT != DION_DTYPE_NONE || has_ef) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if constexpr (GDT == DION_DTYPE_BF16) {
+        S.x[q][0] += __uint_as_float(S.gb[q] << 16);
+        S.x[q][1] += __uint_as_float(S.gb[q] & 0xFFFF0000u);
+      } else if constexpr (GDT == DION_DTYPE_F32) {
+        S.x[q] += S.gf[q];
+      }
+      *reinterpret_cast<f32x2*>(M + static_cast<long>(i0 + q) * ld_m) = S.x[q];
+      nz |= (S.x[q][0] != 0.f) | (S.x[q][1] != 0.f);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      const float bv = tl[(4 * g + q) * LDT + 16 * cb + t];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        acc[c][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(S.x[q][c], bv, acc[c][cb], 0, 0, 0);
+    }
+  }
+}
+
+template <int RB, int GDT>
+__global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) {
+  constexpr int R = 16 * RB;
+  constexpr int KK = RB / 2;
+  constexpr int LDT = R + 4;
+  __shared__ __attribute__((aligned(16))) float tl[2][16 * LDT];
+  __shared__ bf16x8 rs[2][KK * 3 * 64];
+  const ProjArgs& a = e.p;
+  const int b = blockIdx.z;
+  const int kc = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int col_base = blockIdx.x * 128 + wave * 32;
+  const int i_begin = kc * a.kchunk;
+  const int i_end = min(a.rows, i_begin + a.kchunk);
+  float* __restrict__ M = a.m[b] + static_cast<long>(4 * g) * a.ld_m + col_base + 2 * t;
+  const void* G = nullptr;
+  if constexpr (GDT == DION_DTYPE_BF16)
+    G = static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(4 * g) * a.ld_g + col_base + 2 * t;
+  else if constexpr (GDT == DION_DTYPE_F32)
+    G = static_cast<const float*>(a.g[b]) + static_cast<long>(4 * g) * a.ld_g + col_base + 2 * t;
+  const float* __restrict__ Tp = a.thin[b];
+  const float* __restrict__ Rp = e.efr[b];
+  const bool has_ef = Rp != nullptr;
+
+  // fixed EF factor: P'[col_base + 2t + c][32 kk + 8 g ...] (B operand of tile c)
+  Split3 F[2][KK];
+  if (has_ef) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const float* src = e.efp[b] + static_cast<long>(col_base + 2 * t + c) * R + 32 * kk + 8 * g;
+        split3(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), e.alpha, F[c][kk]);
+      }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) F[c][kk] = Split3{};
+  }
+
+  f32x4 acc[2][RB];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bool nz = false;
+
+  ColStepE<GDT> SA, SB;
+  CTStage<RB> TA;
+  EfStage<1, KK> EA;
+  cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i_begin);
+  cp_tload<RB>(TA, Tp, i_begin, tid);
+  cpe_tstore<RB>(TA, tl[0], tid);
+  if (has_ef) {
+    ef_sload<1, KK>(EA, Rp, i_begin, tid);
+    ef_sstore<1, KK>(EA, rs[0], tid);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int i0 = i_begin; i0 < i_end; i0 += 32) {
+    const bool more = i0 + 16 < i_end;
+    if (more) {
+      cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 16);
+      cp_tload<RB>(TA, Tp, i0 + 16, tid);
+      if (has_ef) ef_sload<1, KK>(EA, Rp, i0 + 16, tid);
+    }
+    cpe_compute<RB, GDT>(SA, acc, tl[cur], rs[cur], F, has_ef, M, a.ld_m, i0, g, t, lane, nz);
+    if (!more) break;
+    cpe_tstore<RB>(TA, tl[cur ^ 1], tid);
+    if (has_ef) ef_sstore<1, KK>(EA, rs[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+    const bool more2 = i0 + 32 < i_end;
+    if (more2) {
+      cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 32);
+      cp_tload<RB>(TA, Tp, i0 + 32, tid);
+      if (has_ef) ef_sload<1, KK>(EA, Rp, i0 + 32, tid);
+    }
+    cpe_compute<RB, GDT>(SB, acc, tl[cur], rs[cur], F, has_ef, M, a.ld_m, i0 + 16, g, t, lane, nz);
+    if (!more2) break;
+    cpe_tstore<RB>(TA, tl[cur ^ 1], tid);
+    if (has_ef) ef_sstore<1, KK>(EA, rs[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        out[static_cast<long>(col_base + 2 * (4 * g + q) + c) * R + 16 * cb + t] = acc[c][cb][q];
+  if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+}
+
+// ============================================================================
+// Split-bf16 (bf16x6) projections.  The fp32 MFMA (v_mfma_f32_16x16x4f32,
+// 2 k per 16 cycles per SIMD) caps an r = 64 projection at 2 r flop per
+// element = 0.67 of the fp32 MFMA peak at 5 TB/s of a 4-byte stream, so pass B
+// was MFMA-bound.  Here X and the thin operand are split into hi/mid/lo bf16
+// (exact to ~2^-24 relative) and the six products of order <= 2 run on
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulation: 2.7x less MFMA time for an
+// fp32-level result.
+// The thin operand T (rows = the contraction index) is staged once per block
+// per K-step in LDS, already split, in the B-operand layout of the MFMA:
+// tq[cb][part][lane], lane (t, g) holding T[k(g, e)][16 cb + t], e = 0..7.
+// KMAP 0: k(g, e) = 8 g + e;  KMAP 1: k(g, e) = 16 (e >> 2) + 4 g + (e & 3).
+// ============================================================================
+template <int KMAP>
+__device__ __forceinline__ int kmap(int g, int e) {
+  return KMAP == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
+}
+
+template <int RB>
+struct ThinX6 {
+  static constexpr int kItems = RB * 64;
+  static constexpr int kPer = (kItems + 255) / 256;
+  float v[kPer][8];
+};
+
+template <int RB, int KMAP>
+__device__ __forceinline__ void thin_x6_load(ThinX6<RB>& T, const float* __restrict__ Tp, int k0, int tid) {
+  constexpr int R = 16 * RB;
+#pragma unroll
+  for (int it = 0; it < ThinX6<RB>::kPer; ++it) {
+    const int item = tid + 256 * it;
+    if (item < ThinX6<RB>::kItems) {
+      const int cb = item >> 6, ln = item & 63;
+      const float* src = Tp + 16 * cb + (ln & 15);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) T.v[it][e] = src[static_cast<long>(k0 + kmap<KMAP>(ln >> 4, e)) * R];
+    }
+  }
+}
+
+template <int RB>
+__device__ __forceinline__ void thin_x6_store(const ThinX6<RB>& T, bf16x8* tq, int tid) {
+#pragma unroll
+  for (int it = 0; it < ThinX6<RB>::kPer; ++it) {
+    const int item = tid + 256 * it;
+    if (item < ThinX6<RB>::kItems) {
+      const int cb = item >> 6, ln = item & 63;
+      Split3 sp;
+      split3(f32x4{T.v[it][0], T.v[it][1], T.v[it][2], T.v[it][3]},
+             f32x4{T.v[it][4], T.v[it][5], T.v[it][6], T.v[it][7]}, 1.f, sp);
+      tq[(cb * 3 + 0) * 64 + ln] = sp.hi;
+      tq[(cb * 3 + 1) * 64 + ln] = sp.mid;
+      tq[(cb * 3 + 2) * 64 + ln] = sp.lo;
+    }
+  }
+}
+
+// ---- row projection, no gradient (pass B, transposed: R = M P):
+// rowproj_fast's geometry and loads (lane (t, g): 8 consecutive columns 8g..
+// of rows 16 rb + t = the A operand as loaded), KMAP 0.
+template <int RB>
+__device__ __forceinline__ void rpx_compute(const RowStep<DION_DTYPE_NONE>& S, f32x4 (&acc)[kRB][RB],
+                                            const bf16x8* tq, int lane) {
+#pragma unroll
+  for (int rb = 0; rb < kRB; ++rb) {
+    Split3 A;
+    split3(S.x[rb][0], S.x[rb][1], 1.f, A);
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      Split3 B;
+      ef_sread(tq, cb, lane, B);
+      acc[rb][cb] = mfma6_16(A, B, acc[rb][cb]);
+    }
+  }
+}
+
+template <int RB>
+__global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const ProjArgs a) {
+  constexpr int R = 16 * RB;
+  __shared__ bf16x8 tq[2][RB * 3 * 64];
+  const int b = blockIdx.z;
+  const int kc = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int row_base = blockIdx.x * (64 * kRB) + wave * (16 * kRB);
+  const int j_begin = kc * a.kchunk;
+  const int j_end = min(a.cols, j_begin + a.kchunk);
+  const float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 8 * g;
+  const float* __restrict__ Tp = a.thin[b];
+
+  f32x4 acc[kRB][RB];
+#pragma unroll
+  for (int rb = 0; rb < kRB; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  RowStep<DION_DTYPE_NONE> SA, SB;
+  ThinX6<RB> TA;
+  rp_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, j_begin);
+  thin_x6_load<RB, 0>(TA, Tp, j_begin, tid);
+  thin_x6_store<RB>(TA, tq[0], tid);
+  __syncthreads();
+  int cur = 0;
+  for (int j0 = j_begin; j0 < j_end; j0 += 64) {
+    const bool more = j0 + 32 < j_end;
+    if (more) {
+      rp_load<DION_DTYPE_NONE>(SB, M, nullptr, a.ld_m, 0, j0 + 32);
+      thin_x6_load<RB, 0>(TA, Tp, j0 + 32, tid);
+    }
+    rpx_compute<RB>(SA, acc, tq[cur], lane);
+    if (!more) break;
+    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+    const bool more2 = j0 + 64 < j_end;
+    if (more2) {
+      rp_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, j0 + 64);
+      thin_x6_load<RB, 0>(TA, Tp, j0 + 64, tid);
+    }
+    rpx_compute<RB>(SB, acc, tq[cur], lane);
+    if (!more2) break;
+    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int rb = 0; rb < kRB; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        out[static_cast<long>(row_base + 16 * rb + 4 * g + q) * R + 16 * cb + t] = acc[rb][cb][q];
+}
+
+// ---- column projection, no gradient (pass B, not transposed: R = M^T P):
+// block = 4 waves x 16 CT columns, K-step = 32 rows; lane (t, g) loads the run
+// of columns CT t .. CT t + CT - 1 of rows 8g + e (e = 0..7): per tile c
+// (columns CT t + c) its 8 values are the A operand's k-run, KMAP 0.
+template <int CT>
+struct ColStepX6 {
+  typedef float vec __attribute__((ext_vector_type(CT)));
+  vec x[8];
+};
+
+template <int CT>
+__device__ __forceinline__ void cpx_load(ColStepX6<CT>& S, const float* __restrict__ M, long ld_m, int i0) {
+  typedef typename ColStepX6<CT>::vec vec;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) S.x[e] = *reinterpret_cast<const vec*>(M + static_cast<long>(i0 + e) * ld_m);
+}
+
+template <int RB, int CT>
+__device__ __forceinline__ void cpx_compute(const ColStepX6<CT>& S, f32x4 (&acc)[CT][RB], const bf16x8* tq,
+                                            int lane) {
+  // split the whole step first (the fp32 tile dies here), then one B read per cb
+  Split3 A[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+    split3(f32x4{S.x[0][c], S.x[1][c], S.x[2][c], S.x[3][c]}, f32x4{S.x[4][c], S.x[5][c], S.x[6][c], S.x[7][c]},
+           1.f, A[c]);
+#pragma unroll
+  for (int cb = 0; cb < RB; ++cb) {
+    Split3 B;
+    ef_sread(tq, cb, lane, B);
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc[c][cb] = mfma6_16(A[c], B, acc[c][cb]);
+  }
+}
+
+template <int RB>
+constexpr int colx6_ct() { return RB >= 4 ? 2 : 4; }
+
+template <int RB>
+__global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_x6_kernel(const ProjArgs a) {
+  constexpr int R = 16 * RB;
+  constexpr int CT = colx6_ct<RB>();
+  __shared__ bf16x8 tq[2][RB * 3 * 64];
+  const int b = blockIdx.z;
+  const int kc = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int col_base = blockIdx.x * (64 * CT) + wave * (16 * CT);
+  const int i_begin = kc * a.kchunk;
+  const int i_end = min(a.rows, i_begin + a.kchunk);
+  const float* __restrict__ M = a.m[b] + static_cast<long>(8 * g) * a.ld_m + col_base + CT * t;
+  const float* __restrict__ Tp = a.thin[b];
+
+  f32x4 acc[CT][RB];
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  ColStepX6<CT> SA, SB;
+  ThinX6<RB> TA;
+  cpx_load<CT>(SA, M, a.ld_m, i_begin);
+  thin_x6_load<RB, 0>(TA, Tp, i_begin, tid);
+  thin_x6_store<RB>(TA, tq[0], tid);
+  __syncthreads();
+  int cur = 0;
+  for (int i0 = i_begin; i0 < i_end; i0 += 64) {
+    const bool more = i0 + 32 < i_end;
+    if (more) {
+      cpx_load<CT>(SB, M, a.ld_m, i0 + 32);
+      thin_x6_load<RB, 0>(TA, Tp, i0 + 32, tid);
+    }
+    cpx_compute<RB, CT>(SA, acc, tq[cur], lane);
+    if (!more) break;
+    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+    const bool more2 = i0 + 64 < i_end;
+    if (more2) {
+      cpx_load<CT>(SA, M, a.ld_m, i0 + 64);
+      thin_x6_load<RB, 0>(TA, Tp, i0 + 64, tid);
+    }
+    cpx_compute<RB, CT>(SB, acc, tq[cur], lane);
+    if (!more2) break;
+    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        out[static_cast<long>(col_base + CT * (4 * g + q) + c) * R + 16 * cb + t] = acc[c][cb][q];
+}
+
+// ============================================================================
 // host side
 // ============================================================================
 namespace {
@@ -1795,14 +2484,28 @@ Geo rowproj_geo(int rows, int cols, int batch, int block_rows = 128) {
 }
 
 // column projection: X rows x cols, reduce over rows
-Geo colproj_geo(int rows, int cols, int batch, bool panel) {
+Geo colproj_geo(int rows, int cols, int batch, bool panel, int kalign = 16) {
   Geo g;
   g.gx = static_cast<int>(ceil_div(cols, panel ? 64 : 256));
   long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
   long maxc = ceil_div(rows, panel ? 512 : 256);
   long nc = want < maxc ? want : maxc;
   if (nc < 1) nc = 1;
-  g.kchunk = round_up(ceil_div(rows, nc), 16);
+  g.kchunk = round_up(ceil_div(rows, nc), kalign);
+  g.nchunk = static_cast<int>(ceil_div(rows, g.kchunk));
+  g.out_rows = cols;
+  return g;
+}
+
+// colproj_x6_kernel: 64 * CT columns per block (CT = 2 for r >= 64, else 4), 32-row K-steps
+Geo colx6_geo(int rows, int cols, int batch, int r) {
+  Geo g;
+  g.gx = static_cast<int>(ceil_div(cols, r >= 64 ? 128 : 256));
+  long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
+  long maxc = ceil_div(rows, 256);
+  long nc = want < maxc ? want : maxc;
+  if (nc < 1) nc = 1;
+  g.kchunk = round_up(ceil_div(rows, nc), 32);
   g.nchunk = static_cast<int>(ceil_div(rows, g.kchunk));
   g.out_rows = cols;
   return g;
@@ -1810,6 +2513,26 @@ Geo colproj_geo(int rows, int cols, int batch, bool panel) {
 
 bool rowproj_fast_ok(int rows, int cols, int r) { return rows % (64 * kRB) == 0 && cols % 32 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
 bool colproj_fast_ok(int rows, int cols, int r) { return cols % 256 == 0 && rows % 16 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
+
+// deferred-EF pass A (rowproj_ef_kernel / colproj_ef_kernel)
+bool proj_ef_ok(int m, int n, int r, bool transposed) {
+  if (r != 32 && r != 64) return false;
+  return transposed ? (n % 128 == 0 && m % 16 == 0) : (m % (64 * kRB) == 0 && n % 32 == 0);
+}
+
+Geo proj_ef_geo(int m, int n, int batch, bool transposed) {
+  if (!transposed) return rowproj_geo(m, n, batch, 64 * kRB);
+  Geo g;
+  g.gx = static_cast<int>(ceil_div(n, 128));
+  long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
+  long maxc = ceil_div(m, 256);
+  long nc = want < maxc ? want : maxc;
+  if (nc < 1) nc = 1;
+  g.kchunk = round_up(ceil_div(m, nc), 16);
+  g.nchunk = static_cast<int>(ceil_div(m, g.kchunk));
+  g.out_rows = n;
+  return g;
+}
 
 size_t slab_bytes(const Geo& g, int batch, int r) {
   return g.nchunk > 1 ? sizeof(float) * static_cast<size_t>(batch) * g.nchunk * g.out_rows * r : 0;
@@ -1893,7 +2616,11 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
   fast = fast && (ld_m % 8) == 0 && (gdt == DION_DTYPE_NONE || (ld_g % 8) == 0);
   for (int b = 0; b < batch && fast; ++b)
     fast = aligned16(M[b]) && aligned16(thin[b]) && (gdt == DION_DTYPE_NONE || aligned16(G[b]));
-  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, fast ? 64 * kRB : 128) : colproj_geo(rows, cols, batch, false);
+  // no gradient (pass B): split-bf16 MFMA kernels (the column one steps 32 rows)
+  const bool x6 = fast && gdt == DION_DTYPE_NONE && (row_mode || rows % 32 == 0);
+  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, fast ? 64 * kRB : 128)
+                 : x6      ? colx6_geo(rows, cols, batch, r)
+                           : colproj_geo(rows, cols, batch, false);
   const size_t need = slab_bytes(geo, batch, r);
   if (need > ws_bytes || (need > 0 && ws == nullptr))
     return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
@@ -1924,7 +2651,11 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     constexpr int RB = decltype(RBc)::value;
     return dispatch_gdt(gdt, [&](auto Gc) {
       constexpr int GD = decltype(Gc)::value;
-      if (fast && row_mode)
+      if (x6 && row_mode)
+        hipLaunchKernelGGL((rowproj_x6_kernel<RB>), grid, dim3(256), 0, st, a);
+      else if (x6)
+        hipLaunchKernelGGL((colproj_x6_kernel<RB>), grid, dim3(256), 0, st, a);
+      else if (fast && row_mode)
         hipLaunchKernelGGL((rowproj_fast_kernel<RB, GD>), grid, dim3(256), 0, st, a);
       else if (fast)
         hipLaunchKernelGGL((colproj_fast_kernel<RB, GD>), grid, dim3(256), 0, st, a);
@@ -2113,7 +2844,16 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
         if (row_mode) {
           const size_t nf = slab_bytes(rowproj_geo(d->m, d->n, chunk, 64 * kRB), chunk, d->r);
           if (nf > n) n = nf;
+        } else {
+          const size_t nx = slab_bytes(colx6_geo(d->m, d->n, chunk, d->r), chunk, d->r);
+          if (nx > n) n = nx;
         }
+        break;
+      }
+      case DION_OP_PROJECT_P_EF: {
+        if (!proj_ef_ok(d->m, d->n, d->r, d->transposed != 0))
+          return fail(DION_E_UNSUPPORTED, "no deferred-EF pass A for %dx%d r=%d", d->m, d->n, d->r);
+        n = slab_bytes(proj_ef_geo(d->m, d->n, chunk, d->transposed != 0), chunk, d->r);
         break;
       }
       case DION_OP_ORTHONORMALIZE: {
@@ -2151,6 +2891,81 @@ int dion_project_p(const DionBatchDesc* d, const void* const* G, float* const* M
                         d->g_dtype, P + static_cast<long>(b0) * mp * d->r, nonzero ? nonzero + b0 : nullptr, ws,
                         ws_bytes, st);
     if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const* M, const float* const* Q,
+                      float* P, uint32_t* nonzero, const DionPendingEF* ef, void* ws, size_t ws_bytes,
+                      dion_stream_t stream) {
+  if (ef == nullptr) return dion_project_p(d, G, M, Q, P, nonzero, ws, ws_bytes, stream);
+  int rc = validate(d);
+  if (rc != DION_OK) return rc;
+  if (M == nullptr || Q == nullptr || P == nullptr || ef->P == nullptr || ef->R == nullptr)
+    return fail(DION_E_INVALID, "null argument");
+  if (d->g_dtype != DION_DTYPE_NONE && G == nullptr) return fail(DION_E_INVALID, "G is null");
+  const bool tr = d->transposed != 0;
+  const int mp = tr ? d->n : d->m;
+  const long ld_m = ldv(d->ld_m, d->n), ld_g = ldv(d->ld_g, d->n);
+  if (!proj_ef_ok(d->m, d->n, d->r, tr) || ld_m % 8 != 0 || (d->g_dtype != DION_DTYPE_NONE && ld_g % 8 != 0))
+    return fail(DION_E_UNSUPPORTED, "no deferred-EF pass A for %dx%d r=%d", d->m, d->n, d->r);
+  for (int b = 0; b < d->batch; ++b) {
+    if (M[b] == nullptr || Q[b] == nullptr || (d->g_dtype != DION_DTYPE_NONE && G[b] == nullptr))
+      return fail(DION_E_INVALID, "null matrix pointer at entry %d", b);
+    if ((ef->P[b] == nullptr) != (ef->R[b] == nullptr))
+      return fail(DION_E_INVALID, "pending EF of entry %d has only one factor", b);
+    if (!aligned16(M[b]) || !aligned16(Q[b]) || (d->g_dtype != DION_DTYPE_NONE && !aligned16(G[b])) ||
+        (ef->P[b] && (!aligned16(ef->P[b]) || !aligned16(ef->R[b]))))
+      return fail(DION_E_UNSUPPORTED, "deferred-EF pass A needs 16-byte aligned operands (entry %d)", b);
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    const Geo geo = proj_ef_geo(d->m, d->n, nb, tr);
+    const size_t need = slab_bytes(geo, nb, d->r);
+    if (need > ws_bytes || (need > 0 && ws == nullptr))
+      return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
+    float* out = P + static_cast<long>(b0) * mp * d->r;
+    EfProjArgs e;
+    memset(&e, 0, sizeof(e));
+    ProjArgs& a = e.p;
+    for (int b = 0; b < nb; ++b) {
+      a.g[b] = G ? G[b0 + b] : nullptr;
+      a.m[b] = M[b0 + b];
+      a.thin[b] = Q[b0 + b];
+      e.efp[b] = ef->P[b0 + b];
+      e.efr[b] = ef->R[b0 + b];
+    }
+    e.alpha = ef->alpha;
+    a.out = geo.nchunk > 1 ? static_cast<float*>(ws) : out;
+    a.nonzero = nonzero ? nonzero + b0 : nullptr;
+    a.rows = d->m;
+    a.cols = d->n;
+    a.r = d->r;
+    a.ld_m = ld_m;
+    a.ld_g = ld_g;
+    a.kchunk = geo.kchunk;
+    a.nchunk = geo.nchunk;
+    a.out_rows = geo.out_rows;
+    a.vec = 1;
+    const dim3 grid(geo.gx, geo.nchunk, nb);
+    auto go = [&](auto RBc) {
+      constexpr int RB = decltype(RBc)::value;
+      return dispatch_gdt(d->g_dtype, [&](auto Gc) {
+        constexpr int GD = decltype(Gc)::value;
+        if (tr)
+          hipLaunchKernelGGL((colproj_ef_kernel<RB, GD>), grid, dim3(256), 0, st, e);
+        else
+          hipLaunchKernelGGL((rowproj_ef_kernel<RB, GD>), grid, dim3(256), 0, st, e);
+        return check_launch(tr ? "colproj_ef" : "rowproj_ef");
+      });
+    };
+    rc = d->r == 32 ? go(std::integral_constant<int, 2>{}) : go(std::integral_constant<int, 4>{});
+    if (rc != DION_OK) return rc;
+    if (geo.nchunk > 1) {
+      rc = launch_reduce(out, static_cast<const float*>(ws), geo.nchunk, static_cast<long>(geo.out_rows) * d->r, nb, st);
+      if (rc != DION_OK) return rc;
+    }
   }
   return DION_OK;
 }
@@ -2291,7 +3106,7 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
                   dion_stream_t stream) {
   int rc = validate(d);
   if (rc != DION_OK) return rc;
-  if (M == nullptr || P == nullptr || R == nullptr || Qn == nullptr || nonzero == nullptr)
+  if (P == nullptr || R == nullptr || Qn == nullptr || nonzero == nullptr || (M == nullptr && W == nullptr))
     return fail(DION_E_INVALID, "null argument");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int mp = d->transposed ? d->n : d->m;
@@ -2303,10 +3118,10 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
     EfArgs a;
     memset(&a, 0, sizeof(a));
     for (int b = 0; b < nb; ++b) {
-      a.m[b] = M[b0 + b];
+      a.m[b] = M ? M[b0 + b] : nullptr;
       a.w[b] = W ? W[b0 + b] : nullptr;
       a.qn[b] = Qn[b0 + b];
-      if (a.m[b] == nullptr || a.qn[b] == nullptr || (W && a.w[b] == nullptr))
+      if ((M && a.m[b] == nullptr) || a.qn[b] == nullptr || (W && a.w[b] == nullptr))
         return fail(DION_E_INVALID, "null pointer at entry %d", b0 + b);
     }
     a.P = P + static_cast<long>(b0) * mp * r;
@@ -2330,12 +3145,15 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
                     aligned16(a.P) && aligned16(a.R) && (ldv(d->ld_m, d->n) % 4 == 0) &&
                     (W == nullptr || ldv(d->ld_w, d->n) % 4 == 0);
     for (int b = 0; b < nb && split_ok; ++b) split_ok = aligned16(a.qn[b]);
+    if (M == nullptr && !split_ok)
+      return fail(DION_E_UNSUPPORTED, "weight-only update needs the rank-update kernel (%dx%d r=%d)", d->m, d->n, r);
     if (split_ok) {
       const int flen = d->transposed ? d->m : d->n;
       const int slen = d->transposed ? d->n : d->m;
       const dim3 grid(static_cast<unsigned>(ceil_div(flen, 128)), static_cast<unsigned>(ceil_div(slen, kEfStream)), nb);
       for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1 && W == nullptr) break;
+        if (pass == 0 && M == nullptr) continue;
         RankArgs ra;
         memset(&ra, 0, sizeof(ra));
         for (int b = 0; b < nb; ++b) {

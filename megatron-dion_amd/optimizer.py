@@ -24,7 +24,8 @@ import torch.distributed as dist
 from torch.optim.optimizer import Optimizer
 
 from .batches import build_dion_batches
-from .runtime import AsyncRuntime, coalesce_local_batches, is_replicated, run_dion_batch_async
+from .runtime import (AsyncRuntime, coalesce_local_batches, flush_pending_error_feedback, is_replicated,
+                      run_dion_batch_async)
 from .state import init_dion_state
 from .types import DionDistMeta, DionMixedPrecisionConfig, DionStepParam
 
@@ -39,7 +40,8 @@ class MegatronDion(Optimizer):
                  elementwise_lr_scale: float = 1.0, scale_mode: str = "spectral",
                  extra_scale_factor: float = 0.2, split_qkv: bool = False, split_linear: bool = False,
                  max_concurrent_tasks: Optional[int] = None, *, codec=None, sketch_seed: int = 0,
-                 coalesce_local: bool = True, local_streams: int = 2, coalesce_max_entries: int = 16):
+                 coalesce_local: bool = True, local_streams: int = 2, coalesce_max_entries: int = 16,
+                 defer_error_feedback: bool = False):
         if isinstance(params, (list, tuple)):
             for pg in params:
                 if isinstance(pg, dict) and "wd_mult" in pg:
@@ -74,6 +76,7 @@ class MegatronDion(Optimizer):
         self._coalesce_max = max(1, int(coalesce_max_entries))
         self._streams = None
         self._codec = codec
+        self._defer_ef = bool(defer_error_feedback)
         self._profile_records: List[Tuple[str, float]] = []
 
     # ------------------------------------------------------------------ backend
@@ -83,6 +86,22 @@ class MegatronDion(Optimizer):
             from .codec import HipDionCodec
             self._codec = HipDionCodec()
         return self._codec
+
+    # ------------------------------------------------------------------ deferred error feedback
+    @torch.no_grad()
+    def flush_error_feedback(self) -> int:
+        """Apply every deferred error feedback now, so `state[p]['momentum']` is the eager value.
+
+        With `defer_error_feedback=True` the step-t update M += -(1-mu) P R^T is
+        carried by the step-(t+1) pass A (dion_project_p_ef): same sums in the same
+        order, one M read/write less per step.  Anything that reads the momentum
+        between steps (checkpointing, inspection) calls this first; `state_dict()`
+        does so itself."""
+        return flush_pending_error_feedback(self, lambda: self.codec)
+
+    def state_dict(self):
+        self.flush_error_feedback()
+        return super().state_dict()
 
     # ------------------------------------------------------------------ plugin surface
     def enable_distributed_mode(self, *, route_step_params=None) -> None:

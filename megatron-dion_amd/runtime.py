@@ -148,7 +148,25 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     alloc = torch.empty if (W == 1 and real == B) else torch.zeros
     P = alloc((B, mp, r), dtype=torch.float32, device=dev)
     nonzero = torch.zeros((B,), dtype=torch.int32, device=dev)
-    codec.project_p(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed)
+    # deferred error feedback: the previous step's M += -(1-mu) P R^T rides on this pass A
+    defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
+             and (commit_updates is None or all(c is None for c in commit_updates[:real]))
+             and codec.supports_deferred_ef(m, n, r, transposed))
+    pending = [optimizer_states[i].pop(_PENDING_EF, None) if optimizer_states[i] is not None else None
+               for i in range(real)]
+    if any(p is not None for p in pending):
+        alphas = {p[2] for p in pending if p is not None}
+        if defer and len(alphas) == 1:
+            codec.project_p_ef(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed,
+                               [p[0] if p is not None else None for p in pending],
+                               [p[1] if p is not None else None for p in pending], alphas.pop())
+        else:
+            for i, p in enumerate(pending):
+                if p is not None:
+                    _apply_pending(codec, momentums[i], Qs[i], p, m, n, transposed)
+            codec.project_p(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed)
+    else:
+        codec.project_p(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed)
 
     def ortho(P_slice, entry):
         S = None if sketches is None else sketches.get(entry)
@@ -211,8 +229,14 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
                                  scale_mode=optimizer.defaults.get("scale_mode", "spectral"),
                                  rank_fraction=rank_fraction,
                                  extra_scale_factor=optimizer.defaults.get("extra_scale_factor", 0.2))
-    codec.ef_apply(list(momentums[:real]), list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd,
-                   scaled, transposed)
+    if defer:
+        # weights now; this step's error feedback waits for the next pass A (or a flush)
+        codec.ef_apply(None, list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd, scaled, transposed)
+        for i in range(real):
+            optimizer_states[i][_PENDING_EF] = (P[i], R[i], -(1.0 - mu))
+    else:
+        codec.ef_apply(list(momentums[:real]), list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd,
+                       scaled, transposed)
     if commit_updates is not None:
         for i in range(real):
             if commit_updates[i] is not None:
@@ -221,6 +245,37 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     sink = getattr(optimizer, "_factor_sink", None)
     if sink is not None:  # the compressed factors leaving the device (scripts/e2e_pcie.py)
         sink(P[:real], R[:real])
+
+
+# optimizer-state key of a pending (deferred) error feedback: (P_b, R_b, alpha).  The
+# leading underscore keeps it out of the reference's persistent checkpoint state
+# (distrib_dion/checkpoint_io.py:247-266); MegatronDion.flush_error_feedback()
+# applies it before any state is saved.
+_PENDING_EF = "_dion_pending_ef"
+
+
+def _apply_pending(codec, M, Q, pending, m, n, transposed):
+    """M += alpha P R^T (or alpha R P^T) for one matrix: the eager error feedback, late."""
+    Pb, Rb, alpha = pending
+    mu = 1.0 + float(alpha)
+    ones = torch.ones((1,), dtype=torch.int32, device=M.device)
+    codec.ef_apply([M], None, Pb.unsqueeze(0), Rb.unsqueeze(0), [Q], ones, mu, 0.0, 0.0, 0.0, transposed)
+
+
+def flush_pending_error_feedback(optimizer, get_codec) -> int:
+    """Apply every deferred error feedback held in `optimizer.state`; returns how many."""
+    count = 0
+    codec = None
+    for p, st in optimizer.state.items():
+        pend = st.pop(_PENDING_EF, None) if isinstance(st, dict) else None
+        if pend is None:
+            continue
+        codec = codec or get_codec()
+        M, Q = st["momentum"], st["Q"]
+        transposed = pend[0].shape[0] != M.shape[0]  # P has n rows iff transposed (m_P = n != m)
+        _apply_pending(codec, M, Q, pend, int(M.shape[0]), int(M.shape[1]), transposed)
+        count += 1
+    return count
 
 
 def run_dion_batch_async(optimizer, batch, sketches=None) -> Generator[None, None, None]:

@@ -13,8 +13,19 @@ from oracle import dion_oracle as O
 class OracleCodec:
     name = "oracle-cpu"
 
-    def __init__(self, sketch_lookup=None, hyper_eps=1e-8):
+    def __init__(self, sketch_lookup=None, hyper_eps=1e-8, deferred=False):
         self.sketch_lookup = sketch_lookup  # fn(P (1, m_P, r)) -> sketch (1, k, m_P) or None
+        self.deferred = deferred            # offer the deferred-EF pass A (host-logic tests)
+
+    def supports_deferred_ef(self, m, n, r, transposed):
+        return self.deferred
+
+    def project_p_ef(self, grads, momentums, qs, P, nonzero, transposed, ef_P, ef_R, alpha):
+        for b, M in enumerate(momentums):
+            if ef_P[b] is not None:
+                upd = (ef_R[b] @ ef_P[b].mT) if transposed else (ef_P[b] @ ef_R[b].mT)
+                M.add_(upd * alpha)
+        self.project_p(grads, momentums, qs, P, nonzero, transposed)
 
     def project_p(self, grads, momentums, qs, P, nonzero, transposed):
         for b, M in enumerate(momentums):
@@ -48,9 +59,10 @@ class OracleCodec:
             qs[b].copy_(Qn[b])
 
     def ef_apply(self, momentums, params, P, R, qs, nonzero, mu, lr, wd, scaled_lr, transposed):
-        for b, M in enumerate(momentums):
-            upd = (R[b] @ P[b].mT) if transposed else (P[b] @ R[b].mT)
-            M.add_(upd * (-(1.0 - mu)))
+        for b in range(len(qs)):
+            if momentums is not None:
+                upd = (R[b] @ P[b].mT) if transposed else (P[b] @ R[b].mT)
+                momentums[b].add_(upd * (-(1.0 - mu)))
             if params is not None:
                 W = params[b]
                 if wd > 0:

@@ -26,7 +26,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, name, out_dir):
+def _worker(rank, world, port, name, out_dir, deferred=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -41,10 +41,10 @@ def _worker(rank, world, port, name, out_dir):
     names = [n for n, _, _ in case.mats]
     params = {n: torch.nn.Parameter(case.t(rank, 0, f"{n}_W0").clone()) for n in names}
     state = {"step": 0}
-    codec = OracleCodec(sketch_lookup=lambda P: case.sketch_for(rank, state["step"], P))
+    codec = OracleCodec(sketch_lookup=lambda P: case.sketch_for(rank, state["step"], P), deferred=deferred)
     opt = mda.MegatronDion([params[n] for n in names], lr=h["lr"], mu=h["mu"], weight_decay=h["weight_decay"],
                            rank_fraction=case.rank_fraction, epsilon=h["epsilon"],
-                           rcqr_oversample=h["rcqr_oversample"], codec=codec)
+                           rcqr_oversample=h["rcqr_oversample"], codec=codec, defer_error_feedback=deferred)
     attach_dp_routing(opt, [(n, params[n]) for n in names], replicate_group=dist.group.WORLD)
     for n in names:
         opt.state[params[n]]["Q"].copy_(case.t(rank, 0, f"{n}_Q0"))
@@ -57,6 +57,8 @@ def _worker(rank, world, port, name, out_dir):
         results[f"s{step}_schedule"] = [([e.dist_meta.param_name if e.dist_meta else "<pad>"
                                           for e in b.entries], b.real_batch_size) for b in batches]
         opt.step()
+        if deferred and step == case.steps - 1:
+            opt.flush_error_feedback()
         for n in names:
             results[f"s{step}_{n}_W"] = params[n].detach().clone()
             results[f"s{step}_{n}_M"] = opt.state[params[n]]["momentum"].clone()
@@ -66,9 +68,9 @@ def _worker(rank, world, port, name, out_dir):
     dist.destroy_process_group()
 
 
-def _run(name, world=2):
+def _run(name, world=2, deferred=False):
     with tempfile.TemporaryDirectory() as tmp:
-        mp.start_processes(_worker, args=(world, _free_port(), name, tmp), nprocs=world, join=True,
+        mp.start_processes(_worker, args=(world, _free_port(), name, tmp, deferred), nprocs=world, join=True,
                            start_method="spawn")
         return [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(world)]
 
@@ -77,17 +79,21 @@ def _maxrel(a, b):
     return (a.double() - b.double()).abs().max().item() / max(b.double().abs().max().item(), 1e-30)
 
 
-def test_gloo_w2_matches_reference_single_batch():
+@pytest.mark.parametrize("deferred", [False, True], ids=["eager_ef", "deferred_ef"])
+def test_gloo_w2_matches_reference_single_batch(deferred):
     from tests._golden import Case
 
     case = Case("c8_w2_two_steps_T")
-    res = _run(case.name)
+    res = _run(case.name, deferred=deferred)
     names = [n for n, _, _ in case.mats]
     for rank in range(2):
         for step in range(case.steps):
             assert res[rank][f"s{step}_schedule"] == [(["x", "y"], 2)]
             for n in names:
-                for k, ref in (("W", "W1"), ("M", "M1"), ("Q", "Q1")):
+                keys = (("W", "W1"), ("Q", "Q1"))
+                if not deferred or step == case.steps - 1:
+                    keys += (("M", "M1"),)
+                for k, ref in keys:
                     err = _maxrel(res[rank][f"s{step}_{n}_{k}"], case.t(rank, step, f"{n}_{ref}"))
                     assert err <= 1e-6, (rank, step, n, k, err)
     # replicas agree bit-for-bit on W and Q; momentum stays rank-local

@@ -319,3 +319,110 @@ def test_llama_shape_properties(m, n):
         ew = (1 - 1e-4) * (W0.double() @ u) - s * (Pd @ (Qd.t() @ u))
     assert maxrel(M.double() @ u, em) <= 1e-5
     assert maxrel(W.double() @ u, ew) <= 1e-5
+
+
+# ---------------------------------------------------------------------------------------------- deferred EF
+@pytest.mark.parametrize("m,n,r,gdt", [(512, 384, 64, torch.bfloat16), (384, 1024, 64, torch.bfloat16),
+                                       (1024, 512, 32, torch.float32), (256, 2048, 32, torch.bfloat16)])
+def test_deferred_ef_pass_a_matches_eager_and_fp64(m, n, r, gdt):
+    """dion_project_p_ef == (dion_ef_apply on M, then dion_project_p), and both == fp64 math."""
+    from megatron_dion_amd.codec import HipDionCodec
+
+    dev = _dev()
+    codec = HipDionCodec(dev)
+    transposed = m < n
+    assert codec.supports_deferred_ef(m, n, r, transposed)
+    mp, nq = (n, m) if transposed else (m, n)
+    g = torch.Generator().manual_seed(m + n + r)
+    B = 3
+    Ms = [torch.randn(m, n, generator=g).to(dev) * 1e-3 for _ in range(B)]
+    Gs = [(torch.randn(m, n, generator=g) * 1e-3).to(gdt).to(dev) for _ in range(B)]
+    Qs = [torch.randn(nq, r, generator=g).to(dev) for _ in range(B)]
+    Pp = [torch.linalg.qr(torch.randn(mp, r, generator=g))[0].contiguous().to(dev) for _ in range(B)]
+    Rp = [(torch.randn(nq, r, generator=g) * 1e-2).to(dev) for _ in range(B)]
+    mu = 0.95
+    alpha = -(1.0 - mu)
+    has = [True, False, True]  # entry 1 has no pending update
+    # eager schedule
+    M1 = [M.clone() for M in Ms]
+    ones = torch.ones(1, dtype=torch.int32, device=dev)
+    for b in range(B):
+        if has[b]:
+            codec.ef_apply([M1[b]], None, Pp[b][None], Rp[b][None], [Qs[b]], ones, mu, 0.0, 0.0, 0.0, transposed)
+    P1 = torch.zeros(B, mp, r, device=dev)
+    nz1 = torch.zeros(B, dtype=torch.int32, device=dev)
+    codec.project_p(Gs, M1, Qs, P1, nz1, transposed)
+    # deferred schedule
+    M2 = [M.clone() for M in Ms]
+    P2 = torch.zeros(B, mp, r, device=dev)
+    nz2 = torch.zeros(B, dtype=torch.int32, device=dev)
+    codec.project_p_ef(Gs, M2, Qs, P2, nz2, transposed, [Pp[b] if has[b] else None for b in range(B)],
+                       [Rp[b] if has[b] else None for b in range(B)], alpha)
+    torch.cuda.synchronize()
+    assert nz1.tolist() == nz2.tolist() == [1] * B
+    for b in range(B):
+        ef = (Rp[b].double() @ Pp[b].double().t()) if transposed else (Pp[b].double() @ Rp[b].double().t())
+        Mref = Ms[b].double() + (alpha * ef if has[b] else 0.0) + Gs[b].double()
+        Xo = Mref.t() if transposed else Mref
+        Pref = Xo @ Qs[b].double()
+        assert maxrel(M2[b], Mref) <= 1e-6, (b, maxrel(M2[b], Mref))
+        assert maxrel(M2[b], M1[b]) <= 1e-6
+        assert maxrel(P2[b], Pref) <= 1e-5
+        assert maxrel(P2[b], P1[b]) <= 1e-5
+        if not has[b]:
+            assert torch.equal(M2[b], M1[b])
+
+
+@pytest.mark.parametrize("label,shapes,r", [("tall_bf16", [(512, 384)] * 3, 64),
+                                            ("wide_T_bf16", [(384, 1024)] * 2, 64),
+                                            ("mixed_fallback_r24", [(330, 200)] * 2, 24)])
+def test_deferred_ef_three_steps_match_oracle(label, shapes, r):
+    """The optimizer with defer_error_feedback=True over 3 steps (explicit sketches) against the
+    oracle's eager steps: W and Q every step, M after flush_error_feedback()."""
+    from megatron_dion_amd.runtime import _PENDING_EF
+
+    dev = _dev()
+    m, n = shapes[0]
+    transposed = m < n
+    mp = max(m, n)
+    k = O.sketch_rows(r)
+    hyper = O.DionHyper(rank_fraction=r / min(m, n))
+    gen = torch.Generator().manual_seed(21)
+    init = _make_case(shapes, r, 3)
+    steps = 3
+    grads = [[(torch.randn(m, n, generator=gen) * 1e-3).to(torch.bfloat16) for _ in shapes] for _ in range(steps)]
+    sk = [[torch.randn(k, mp, generator=gen) * math.sqrt(1.0 / k) for _ in shapes] for _ in range(steps)]
+
+    params = [torch.nn.Parameter(W.to(dev)) for W, _, _, _ in init]
+    opt = mda.MegatronDion(params, lr=hyper.lr, mu=hyper.mu, weight_decay=hyper.weight_decay,
+                           rank_fraction=hyper.rank_fraction, epsilon=hyper.epsilon, defer_error_feedback=True,
+                           coalesce_local=True)
+    named = [(f"w{i}", p) for i, p in enumerate(params)]
+    attach_dp_routing(opt, named)
+    for p, (W, M, Q, G) in zip(params, init):
+        opt.state[p]["momentum"].copy_(M.to(dev))
+        opt.state[p]["Q"].copy_(Q.to(dev))
+    mats = [O.DionMatrix(W=W.clone(), M=M.clone(), Q=Q.clone(), G=None, transposed=transposed,
+                         rank_fraction=hyper.rank_fraction) for W, M, Q, G in init]
+    cur = {"step": 0}
+    idx_of = {id(p): i for i, p in enumerate(params)}
+    opt._sketch_override = lambda b: {j: sk[cur["step"]][idx_of[id(bp)]].to(dev) for j, bp in enumerate(b.params)}
+    eligible = opt.codec.supports_deferred_ef(m, n, r, transposed)
+    for step in range(steps):
+        cur["step"] = step
+        for i, p in enumerate(params):
+            p.main_grad = grads[step][i].to(dev)
+        opt.step()
+        for i, mt in enumerate(mats):
+            mt.G = grads[step][i].float()
+            O.dion_batch_step_local([mt], hyper, sketch_fn=lambda j, P, _i=i: sk[step][_i][None])
+        torch.cuda.synchronize()
+        assert all((_PENDING_EF in opt.state[p]) == eligible for p in params)
+        for p, mt in zip(params, mats):
+            assert maxrel(p, mt.W) <= TOL_WM, (label, step, maxrel(p, mt.W))
+            assert maxrel(opt.state[p]["Q"], mt.Q) <= TOL_Q
+    opt.flush_error_feedback()
+    torch.cuda.synchronize()
+    for p, mt in zip(params, mats):
+        assert _PENDING_EF not in opt.state[p]
+        assert maxrel(opt.state[p]["momentum"], mt.M) <= TOL_WM, (label, maxrel(opt.state[p]["momentum"], mt.M))

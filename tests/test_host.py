@@ -25,11 +25,26 @@ def _header_symbols():
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     syms = _header_symbols()
-    assert len(syms) == 8
+    assert len(syms) == 9
     assert sorted(_lib.EXPORTED) == syms
     for s in syms:
         assert getattr(lib, s) is not None
     assert lib.dion_abi_version() == _lib.ABI_VERSION
+
+
+def test_deferred_ef_query_names_the_fused_shapes():
+    lib = _lib.load()
+    nbytes = ctypes.c_size_t(0)
+    for (m, n, r, tr), ok in (((4096, 4096, 64, 0), True), ((28672, 4096, 64, 0), True),
+                              ((4096, 14336, 64, 1), True), ((6144, 4096, 32, 0), True),
+                              ((64, 48, 8, 0), False), ((4096, 4096, 128, 0), False),
+                              ((4096, 14300, 64, 1), False)):
+        d = _lib.DionBatchDesc(batch=16, m=m, n=n, r=r, transposed=tr, g_dtype=_lib.DTYPE_BF16,
+                               m_dtype=_lib.DTYPE_F32, w_dtype=_lib.DTYPE_F32)
+        rc = lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P_EF, ctypes.byref(nbytes))
+        assert (rc == _lib.DION_OK) == ok, (m, n, r, tr, rc)
+        if not ok:
+            assert rc == _lib.DION_E_UNSUPPORTED
 
 
 def test_abi_rejects_bad_descriptors_without_gpu():
@@ -160,10 +175,14 @@ def test_product_path_fails_loudly_without_library(tmp_path):
         _lib.load(str(tmp_path / "missing.so"))
 
 
-def test_local_path_end_to_end_with_oracle_codec():
+@pytest.mark.parametrize("deferred", [False, True], ids=["eager_ef", "deferred_ef"])
+def test_local_path_end_to_end_with_oracle_codec(deferred):
     """Host runtime (W = 1, coalesced launch groups) reproduces the golden c7 (3 matrices, both
-    orientations, 2 steps) when the test-only oracle codec stands in for the kernels."""
+    orientations, 2 steps) when the test-only oracle codec stands in for the kernels.  With the
+    deferred error feedback the weights and Q match every step and the momentum matches once
+    the pending update is flushed (what state_dict() does)."""
     from megatron_dion_amd.optimizer import attach_dp_routing
+    from megatron_dion_amd.runtime import _PENDING_EF
     from tests._cpu_codec import OracleCodec
 
     case = Case("c7_two_steps_mixed")
@@ -173,7 +192,9 @@ def test_local_path_end_to_end_with_oracle_codec():
     cur = {"step": 0}
     opt = mda.MegatronDion([params[n] for n in names], lr=h["lr"], mu=h["mu"], weight_decay=h["weight_decay"],
                            rank_fraction=case.rank_fraction,
-                           codec=OracleCodec(sketch_lookup=lambda P: case.sketch_for(0, cur["step"], P)))
+                           codec=OracleCodec(sketch_lookup=lambda P: case.sketch_for(0, cur["step"], P),
+                                             deferred=deferred),
+                           defer_error_feedback=deferred)
     attach_dp_routing(opt, [(n, params[n]) for n in names])
     for n in names:
         opt.state[params[n]]["Q"].copy_(case.t(0, 0, f"{n}_Q0"))
@@ -182,8 +203,14 @@ def test_local_path_end_to_end_with_oracle_codec():
         for n in names:
             params[n].grad = case.t(0, step, f"{n}_G").clone()
         opt.step()
+        if deferred:
+            assert all(_PENDING_EF in opt.state[params[n]] for n in names)
+            if step == case.steps - 1:
+                assert opt.flush_error_feedback() == len(names)
         for n in names:
-            for got, key in ((params[n], "W1"), (opt.state[params[n]]["momentum"], "M1"),
-                             (opt.state[params[n]]["Q"], "Q1")):
+            checks = [(params[n], "W1"), (opt.state[params[n]]["Q"], "Q1")]
+            if not deferred or step == case.steps - 1:
+                checks.append((opt.state[params[n]]["momentum"], "M1"))
+            for got, key in checks:
                 ref = case.t(0, step, f"{n}_{key}")
                 assert (got.detach() - ref).abs().max().item() <= 1e-6 * ref.abs().max().item()
