@@ -1824,6 +1824,50 @@ __device__ __forceinline__ void ef_sread(const bf16x8* rs, int ck, int lane, Spl
   A.lo = rs[(ck * 3 + 2) * 64 + lane];
 }
 
+template <int KMAP>
+__device__ __forceinline__ int kmap(int g, int e) {
+  return KMAP == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
+}
+
+template <int RB>
+struct ThinX6 {
+  static constexpr int kItems = RB * 64;
+  static constexpr int kPer = (kItems + 255) / 256;
+  float v[kPer][8];
+};
+
+template <int RB, int KMAP>
+__device__ __forceinline__ void thin_x6_load(ThinX6<RB>& T, const float* __restrict__ Tp, int k0, int tid) {
+  constexpr int R = 16 * RB;
+#pragma unroll
+  for (int it = 0; it < ThinX6<RB>::kPer; ++it) {
+    const int item = tid + 256 * it;
+    if (item < ThinX6<RB>::kItems) {
+      const int cb = item >> 6, ln = item & 63;
+      const float* src = Tp + 16 * cb + (ln & 15);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) T.v[it][e] = src[static_cast<long>(k0 + kmap<KMAP>(ln >> 4, e)) * R];
+    }
+  }
+}
+
+template <int RB>
+__device__ __forceinline__ void thin_x6_store(const ThinX6<RB>& T, bf16x8* tq, int tid) {
+#pragma unroll
+  for (int it = 0; it < ThinX6<RB>::kPer; ++it) {
+    const int item = tid + 256 * it;
+    if (item < ThinX6<RB>::kItems) {
+      const int cb = item >> 6, ln = item & 63;
+      Split3 sp;
+      split3(f32x4{T.v[it][0], T.v[it][1], T.v[it][2], T.v[it][3]},
+             f32x4{T.v[it][4], T.v[it][5], T.v[it][6], T.v[it][7]}, 1.f, sp);
+      tq[(cb * 3 + 0) * 64 + ln] = sp.hi;
+      tq[(cb * 3 + 1) * 64 + ln] = sp.mid;
+      tq[(cb * 3 + 2) * 64 + ln] = sp.lo;
+    }
+  }
+}
+
 // ---- row kernel (not transposed): wave = 2 x 16 rows, step = 32 columns;
 // lane (t, g) holds columns 16c + 4g .. +3 (c = 0, 1) of rows 16 rb + t.
 template <int GDT>
@@ -1848,21 +1892,11 @@ __device__ __forceinline__ void rpe_load(RowStepE<GDT>& S, const float* __restri
     }
 }
 
-template <int RB>
-__device__ __forceinline__ void rpe_tstore(const TStage<RB>& T, float* tl, int tid) {
-  constexpr int LDT = 16 * RB + 4;
-  float* dst = tl + (tid / 8) * LDT + (tid % 8) * 2 * RB;
-#pragma unroll
-  for (int u = 0; u < RB; ++u) *reinterpret_cast<float2*>(dst + 2 * u) = T.v[u];
-}
-
 template <int RB, int GDT>
-__device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRB][RB], const float* tl,
+__device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRB][RB], const bf16x8* tq,
                                             const bf16x8* rs, const Split3 (&F)[kRB][RB / 2], bool has_ef,
-                                            float* __restrict__ M, long ld_m, int j, int g, int t, int lane,
-                                            bool& nz) {
+                                            float* __restrict__ M, long ld_m, int j, int lane, bool& nz) {
   constexpr int KK = RB / 2;
-  constexpr int LDT = 16 * RB + 4;
   if (has_ef) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -1899,16 +1933,16 @@ __device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRB][
         for (int q = 0; q < 4; ++q) nz |= (S.x[rb][c][q] != 0.f);
       }
   }
+  // P += X Q: the lane's 8 columns 16 (e >> 2) + 4 g + (e & 3) are the A operand's k-run (KMAP 1)
+  Split3 A[kRB];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const int col = 16 * (s >> 2) + 4 * g + (s & 3);
+  for (int rb = 0; rb < kRB; ++rb) split3(S.x[rb][0], S.x[rb][1], 1.f, A[rb]);
 #pragma unroll
-    for (int cb = 0; cb < RB; ++cb) {
-      const float bv = tl[col * LDT + 16 * cb + t];
+  for (int cb = 0; cb < RB; ++cb) {
+    Split3 B;
+    ef_sread(tq, cb, lane, B);
 #pragma unroll
-      for (int rb = 0; rb < kRB; ++rb)
-        acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(S.x[rb][s >> 2][s & 3], bv, acc[rb][cb], 0, 0, 0);
-    }
+    for (int rb = 0; rb < kRB; ++rb) acc[rb][cb] = mfma6_16(A[rb], B, acc[rb][cb]);
   }
 }
 
@@ -1916,8 +1950,7 @@ template <int RB, int GDT>
 __global__ void __launch_bounds__(256, 2) rowproj_ef_kernel(const EfProjArgs e) {
   constexpr int R = 16 * RB;
   constexpr int KK = RB / 2;
-  constexpr int LDT = R + 4;
-  __shared__ __attribute__((aligned(16))) float tl[2][32 * LDT];
+  __shared__ bf16x8 tq[2][RB * 3 * 64];
   __shared__ bf16x8 rs[2][2 * KK * 3 * 64];
   const ProjArgs& a = e.p;
   const int b = blockIdx.z;
@@ -1964,11 +1997,11 @@ __global__ void __launch_bounds__(256, 2) rowproj_ef_kernel(const EfProjArgs e) 
   bool nz = false;
 
   RowStepE<GDT> SA, SB;
-  TStage<RB> TA;
+  ThinX6<RB> TA;
   EfStage<2, KK> EA;
   rpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j_begin);
-  rp_tload<RB>(TA, Tp, j_begin, tid);
-  rpe_tstore<RB>(TA, tl[0], tid);
+  thin_x6_load<RB, 1>(TA, Tp, j_begin, tid);
+  thin_x6_store<RB>(TA, tq[0], tid);
   if (has_ef) {
     ef_sload<2, KK>(EA, Rp, j_begin, tid);
     ef_sstore<2, KK>(EA, rs[0], tid);
@@ -1979,24 +2012,24 @@ __global__ void __launch_bounds__(256, 2) rowproj_ef_kernel(const EfProjArgs e) 
     const bool more = j0 + 32 < j_end;
     if (more) {
       rpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, j0 + 32);
-      rp_tload<RB>(TA, Tp, j0 + 32, tid);
+      thin_x6_load<RB, 1>(TA, Tp, j0 + 32, tid);
       if (has_ef) ef_sload<2, KK>(EA, Rp, j0 + 32, tid);
     }
-    rpe_compute<RB, GDT>(SA, acc, tl[cur], rs[cur], F, has_ef, M, a.ld_m, j0, g, t, lane, nz);
+    rpe_compute<RB, GDT>(SA, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, j0, lane, nz);
     if (!more) break;
-    rpe_tstore<RB>(TA, tl[cur ^ 1], tid);
+    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
     if (has_ef) ef_sstore<2, KK>(EA, rs[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
     const bool more2 = j0 + 64 < j_end;
     if (more2) {
       rpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j0 + 64);
-      rp_tload<RB>(TA, Tp, j0 + 64, tid);
+      thin_x6_load<RB, 1>(TA, Tp, j0 + 64, tid);
       if (has_ef) ef_sload<2, KK>(EA, Rp, j0 + 64, tid);
     }
-    rpe_compute<RB, GDT>(SB, acc, tl[cur], rs[cur], F, has_ef, M, a.ld_m, j0 + 32, g, t, lane, nz);
+    rpe_compute<RB, GDT>(SB, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, j0 + 32, lane, nz);
     if (!more2) break;
-    rpe_tstore<RB>(TA, tl[cur ^ 1], tid);
+    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
     if (has_ef) ef_sstore<2, KK>(EA, rs[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
@@ -2013,80 +2046,82 @@ __global__ void __launch_bounds__(256, 2) rowproj_ef_kernel(const EfProjArgs e) 
   if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
 }
 
-// ---- column kernel (transposed): block = 4 waves x 32 columns, step = 16 rows;
-// lane (t, g) holds columns 2t, 2t + 1 of rows 4g + q (q = 0..3).
+// ---- column kernel (transposed): block = 4 waves x 32 columns, step = 32 rows;
+// lane (t, g) holds columns 2t, 2t + 1 of rows 16 h + 4 g + q (h = 0, 1; q = 0..3):
+// per half h that is the EF accumulator's slice, and per column the 8 rows are
+// the projection's k-run (KMAP 1).
 template <int GDT>
 struct ColStepE {
-  f32x2 x[4];
-  uint32_t gb[4];
-  f32x2 gf[4];
+  f32x2 x[2][4];
+  uint32_t gb[2][4];
+  f32x2 gf[2][4];
 };
 
 template <int GDT>
 __device__ __forceinline__ void cpe_load(ColStepE<GDT>& S, const float* __restrict__ M, const void* __restrict__ G,
                                          long ld_m, long ld_g, int i0) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    S.x[q] = *reinterpret_cast<const f32x2*>(M + static_cast<long>(i0 + q) * ld_m);
-    if constexpr (GDT == DION_DTYPE_BF16)
-      S.gb[q] = *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(G) + static_cast<long>(i0 + q) * ld_g);
-    else if constexpr (GDT == DION_DTYPE_F32)
-      S.gf[q] = *reinterpret_cast<const f32x2*>(static_cast<const float*>(G) + static_cast<long>(i0 + q) * ld_g);
-  }
-}
-
-template <int RB>
-__device__ __forceinline__ void cpe_tstore(const CTStage<RB>& T, float* tl, int tid) {
-  constexpr int LDT = 16 * RB + 4;
-  float* dst = tl + (tid / 16) * LDT + (tid % 16) * RB;
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-  for (int u = 0; u < RB; ++u) dst[u] = T.v[u];
+    for (int q = 0; q < 4; ++q) {
+      const long row = i0 + 16 * h + q;
+      S.x[h][q] = *reinterpret_cast<const f32x2*>(M + row * ld_m);
+      if constexpr (GDT == DION_DTYPE_BF16)
+        S.gb[h][q] = *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(G) + row * ld_g);
+      else if constexpr (GDT == DION_DTYPE_F32)
+        S.gf[h][q] = *reinterpret_cast<const f32x2*>(static_cast<const float*>(G) + row * ld_g);
+    }
 }
 
 template <int RB, int GDT>
-__device__ __forceinline__ void cpe_compute(ColStepE<GDT>& S, f32x4 (&acc)[2][RB], const float* tl,
+__device__ __forceinline__ void cpe_compute(ColStepE<GDT>& S, f32x4 (&acc)[2][RB], const bf16x8* tq,
                                             const bf16x8* rs, const Split3 (&F)[2][RB / 2], bool has_ef,
-                                            float* __restrict__ M, long ld_m, int i0, int g, int t, int lane,
-                                            bool& nz) {
+                                            float* __restrict__ M, long ld_m, int i0, int lane, bool& nz) {
   constexpr int KK = RB / 2;
-  constexpr int LDT = 16 * RB + 4;
   if (has_ef) {
-    f32x4 e[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      Split3 A;
-      ef_sread(rs, kk, lane, A);
+    for (int h = 0; h < 2; ++h) {
+      f32x4 e[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int c = 0; c < 2; ++c) e[c] = mfma6_16(A, F[c][kk], e[c]);
-    }
+      for (int kk = 0; kk < KK; ++kk) {
+        Split3 A;
+        ef_sread(rs, h * KK + kk, lane, A);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      S.x[q][0] += e[0][q];
-      S.x[q][1] += e[1][q];
+        for (int c = 0; c < 2; ++c) e[c] = mfma6_16(A, F[c][kk], e[c]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        S.x[h][q][0] += e[0][q];
+        S.x[h][q][1] += e[1][q];
+      }
     }
   }
   if (GDT != DION_DTYPE_NONE || has_ef) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if constexpr (GDT == DION_DTYPE_BF16) {
-        S.x[q][0] += __uint_as_float(S.gb[q] << 16);
-        S.x[q][1] += __uint_as_float(S.gb[q] & 0xFFFF0000u);
-      } else if constexpr (GDT == DION_DTYPE_F32) {
-        S.x[q] += S.gf[q];
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (GDT == DION_DTYPE_BF16) {
+          S.x[h][q][0] += __uint_as_float(S.gb[h][q] << 16);
+          S.x[h][q][1] += __uint_as_float(S.gb[h][q] & 0xFFFF0000u);
+        } else if constexpr (GDT == DION_DTYPE_F32) {
+          S.x[h][q] += S.gf[h][q];
+        }
+        *reinterpret_cast<f32x2*>(M + static_cast<long>(i0 + 16 * h + q) * ld_m) = S.x[h][q];
+        nz |= (S.x[h][q][0] != 0.f) | (S.x[h][q][1] != 0.f);
       }
-      *reinterpret_cast<f32x2*>(M + static_cast<long>(i0 + q) * ld_m) = S.x[q];
-      nz |= (S.x[q][0] != 0.f) | (S.x[q][1] != 0.f);
-    }
   }
+  Split3 A[2];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int c = 0; c < 2; ++c)
+    split3(f32x4{S.x[0][0][c], S.x[0][1][c], S.x[0][2][c], S.x[0][3][c]},
+           f32x4{S.x[1][0][c], S.x[1][1][c], S.x[1][2][c], S.x[1][3][c]}, 1.f, A[c]);
 #pragma unroll
-    for (int cb = 0; cb < RB; ++cb) {
-      const float bv = tl[(4 * g + q) * LDT + 16 * cb + t];
+  for (int cb = 0; cb < RB; ++cb) {
+    Split3 B;
+    ef_sread(tq, cb, lane, B);
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
-        acc[c][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(S.x[q][c], bv, acc[c][cb], 0, 0, 0);
-    }
+    for (int c = 0; c < 2; ++c) acc[c][cb] = mfma6_16(A[c], B, acc[c][cb]);
   }
 }
 
@@ -2094,9 +2129,8 @@ template <int RB, int GDT>
 __global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) {
   constexpr int R = 16 * RB;
   constexpr int KK = RB / 2;
-  constexpr int LDT = R + 4;
-  __shared__ __attribute__((aligned(16))) float tl[2][16 * LDT];
-  __shared__ bf16x8 rs[2][KK * 3 * 64];
+  __shared__ bf16x8 tq[2][RB * 3 * 64];
+  __shared__ bf16x8 rs[2][2 * KK * 3 * 64];
   const ProjArgs& a = e.p;
   const int b = blockIdx.z;
   const int kc = blockIdx.y;
@@ -2143,40 +2177,40 @@ __global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) 
   bool nz = false;
 
   ColStepE<GDT> SA, SB;
-  CTStage<RB> TA;
-  EfStage<1, KK> EA;
+  ThinX6<RB> TA;
+  EfStage<2, KK> EA;
   cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i_begin);
-  cp_tload<RB>(TA, Tp, i_begin, tid);
-  cpe_tstore<RB>(TA, tl[0], tid);
+  thin_x6_load<RB, 1>(TA, Tp, i_begin, tid);
+  thin_x6_store<RB>(TA, tq[0], tid);
   if (has_ef) {
-    ef_sload<1, KK>(EA, Rp, i_begin, tid);
-    ef_sstore<1, KK>(EA, rs[0], tid);
+    ef_sload<2, KK>(EA, Rp, i_begin, tid);
+    ef_sstore<2, KK>(EA, rs[0], tid);
   }
   __syncthreads();
   int cur = 0;
-  for (int i0 = i_begin; i0 < i_end; i0 += 32) {
-    const bool more = i0 + 16 < i_end;
+  for (int i0 = i_begin; i0 < i_end; i0 += 64) {
+    const bool more = i0 + 32 < i_end;
     if (more) {
-      cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 16);
-      cp_tload<RB>(TA, Tp, i0 + 16, tid);
-      if (has_ef) ef_sload<1, KK>(EA, Rp, i0 + 16, tid);
+      cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
+      thin_x6_load<RB, 1>(TA, Tp, i0 + 32, tid);
+      if (has_ef) ef_sload<2, KK>(EA, Rp, i0 + 32, tid);
     }
-    cpe_compute<RB, GDT>(SA, acc, tl[cur], rs[cur], F, has_ef, M, a.ld_m, i0, g, t, lane, nz);
+    cpe_compute<RB, GDT>(SA, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, i0, lane, nz);
     if (!more) break;
-    cpe_tstore<RB>(TA, tl[cur ^ 1], tid);
-    if (has_ef) ef_sstore<1, KK>(EA, rs[cur ^ 1], tid);
+    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
+    if (has_ef) ef_sstore<2, KK>(EA, rs[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
-    const bool more2 = i0 + 32 < i_end;
+    const bool more2 = i0 + 64 < i_end;
     if (more2) {
-      cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 32);
-      cp_tload<RB>(TA, Tp, i0 + 32, tid);
-      if (has_ef) ef_sload<1, KK>(EA, Rp, i0 + 32, tid);
+      cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
+      thin_x6_load<RB, 1>(TA, Tp, i0 + 64, tid);
+      if (has_ef) ef_sload<2, KK>(EA, Rp, i0 + 64, tid);
     }
-    cpe_compute<RB, GDT>(SB, acc, tl[cur], rs[cur], F, has_ef, M, a.ld_m, i0 + 16, g, t, lane, nz);
+    cpe_compute<RB, GDT>(SB, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, i0 + 32, lane, nz);
     if (!more2) break;
-    cpe_tstore<RB>(TA, tl[cur ^ 1], tid);
-    if (has_ef) ef_sstore<1, KK>(EA, rs[cur ^ 1], tid);
+    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
+    if (has_ef) ef_sstore<2, KK>(EA, rs[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
   }
@@ -2190,63 +2224,6 @@ __global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) 
       for (int q = 0; q < 4; ++q)
         out[static_cast<long>(col_base + 2 * (4 * g + q) + c) * R + 16 * cb + t] = acc[c][cb][q];
   if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
-}
-
-// ============================================================================
-// Split-bf16 (bf16x6) projections.  The fp32 MFMA (v_mfma_f32_16x16x4f32,
-// 2 k per 16 cycles per SIMD) caps an r = 64 projection at 2 r flop per
-// element = 0.67 of the fp32 MFMA peak at 5 TB/s of a 4-byte stream, so pass B
-// was MFMA-bound.  Here X and the thin operand are split into hi/mid/lo bf16
-// (exact to ~2^-24 relative) and the six products of order <= 2 run on
-// v_mfma_f32_16x16x32_bf16 with fp32 accumulation: 2.7x less MFMA time for an
-// fp32-level result.
-// The thin operand T (rows = the contraction index) is staged once per block
-// per K-step in LDS, already split, in the B-operand layout of the MFMA:
-// tq[cb][part][lane], lane (t, g) holding T[k(g, e)][16 cb + t], e = 0..7.
-// KMAP 0: k(g, e) = 8 g + e;  KMAP 1: k(g, e) = 16 (e >> 2) + 4 g + (e & 3).
-// ============================================================================
-template <int KMAP>
-__device__ __forceinline__ int kmap(int g, int e) {
-  return KMAP == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
-}
-
-template <int RB>
-struct ThinX6 {
-  static constexpr int kItems = RB * 64;
-  static constexpr int kPer = (kItems + 255) / 256;
-  float v[kPer][8];
-};
-
-template <int RB, int KMAP>
-__device__ __forceinline__ void thin_x6_load(ThinX6<RB>& T, const float* __restrict__ Tp, int k0, int tid) {
-  constexpr int R = 16 * RB;
-#pragma unroll
-  for (int it = 0; it < ThinX6<RB>::kPer; ++it) {
-    const int item = tid + 256 * it;
-    if (item < ThinX6<RB>::kItems) {
-      const int cb = item >> 6, ln = item & 63;
-      const float* src = Tp + 16 * cb + (ln & 15);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) T.v[it][e] = src[static_cast<long>(k0 + kmap<KMAP>(ln >> 4, e)) * R];
-    }
-  }
-}
-
-template <int RB>
-__device__ __forceinline__ void thin_x6_store(const ThinX6<RB>& T, bf16x8* tq, int tid) {
-#pragma unroll
-  for (int it = 0; it < ThinX6<RB>::kPer; ++it) {
-    const int item = tid + 256 * it;
-    if (item < ThinX6<RB>::kItems) {
-      const int cb = item >> 6, ln = item & 63;
-      Split3 sp;
-      split3(f32x4{T.v[it][0], T.v[it][1], T.v[it][2], T.v[it][3]},
-             f32x4{T.v[it][4], T.v[it][5], T.v[it][6], T.v[it][7]}, 1.f, sp);
-      tq[(cb * 3 + 0) * 64 + ln] = sp.hi;
-      tq[(cb * 3 + 1) * 64 + ln] = sp.mid;
-      tq[(cb * 3 + 2) * 64 + ln] = sp.lo;
-    }
-  }
 }
 
 // ---- row projection, no gradient (pass B, transposed: R = M P):
@@ -2517,7 +2494,7 @@ bool colproj_fast_ok(int rows, int cols, int r) { return cols % 256 == 0 && rows
 // deferred-EF pass A (rowproj_ef_kernel / colproj_ef_kernel)
 bool proj_ef_ok(int m, int n, int r, bool transposed) {
   if (r != 32 && r != 64) return false;
-  return transposed ? (n % 128 == 0 && m % 16 == 0) : (m % (64 * kRB) == 0 && n % 32 == 0);
+  return transposed ? (n % 128 == 0 && m % 32 == 0) : (m % (64 * kRB) == 0 && n % 32 == 0);
 }
 
 Geo proj_ef_geo(int m, int n, int batch, bool transposed) {
@@ -2528,7 +2505,7 @@ Geo proj_ef_geo(int m, int n, int batch, bool transposed) {
   long maxc = ceil_div(m, 256);
   long nc = want < maxc ? want : maxc;
   if (nc < 1) nc = 1;
-  g.kchunk = round_up(ceil_div(m, nc), 16);
+  g.kchunk = round_up(ceil_div(m, nc), 32);
   g.nchunk = static_cast<int>(ceil_div(m, g.kchunk));
   g.out_rows = n;
   return g;
