@@ -38,6 +38,7 @@
 #include "../../include/dion_codec.h"
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -1764,8 +1765,89 @@ struct EfProjArgs {
   ProjArgs p;
   const float* efp[MAXB];  // pending P'_b (m_P x r) or null (no pending EF for b)
   const float* efr[MAXB];  // pending R'_b (n_Q x r)
+  const u32x4* qsplit;     // Q_b pre-split, B-operand layout (KMAP 1), split_stride 16-byte units per matrix
+  const u32x4* rsplit;     // R'_b pre-split, A-operand layout
+  long split_stride;
   float alpha;
 };
+
+// Pre-split of a small factor (rows x r fp32) into hi/mid/lo bf16, laid out so a
+// K-step's operands are one contiguous run: dst[(grp * 3 + part) * 64 + lane].
+//   layout 0 (B operand):  grp = (row / 32) * RB + cb, lane (t, g) <- rows 32 blk + kmap(g, e), column 16 cb + t
+//   layout 1 (A operand):  grp = (row / 16) * KK + kk, lane (t, g) <- row 16 blk + t, columns 32 kk + 8 g + e
+struct PresplitArgs {
+  const float* src[MAXB];
+  u32x4* dst;
+  long stride;  // 16-byte units per matrix
+  int rows, r, layout, kmap;
+};
+
+__global__ void __launch_bounds__(256) presplit_kernel(const PresplitArgs a) {
+  const int b = blockIdx.y;
+  const float* __restrict__ src = a.src[b];
+  if (src == nullptr) return;
+  const long items = static_cast<long>(a.rows) * a.r / 8;
+  const long item = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
+  if (item >= items) return;
+  const int ln = static_cast<int>(item & 63);
+  const long grp = item >> 6;
+  const int t = ln & 15, g = ln >> 4;
+  float v[8];
+  if (a.layout == 0) {
+    const int RB = a.r / 16;
+    const long blk = grp / RB;
+    const int cb = static_cast<int>(grp - blk * RB);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = a.kmap == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
+      v[e] = src[(blk * 32 + k) * a.r + 16 * cb + t];
+    }
+  } else {
+    const int KK = a.r / 32;
+    const long blk = grp / KK;
+    const int kk = static_cast<int>(grp - blk * KK);
+    const float* p = src + (blk * 16 + t) * a.r + 32 * kk + 8 * g;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = p[e];
+  }
+  Split3 sp;
+  split3(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, 1.f, sp);
+  u32x4* d = a.dst + b * a.stride + (grp * 3) * 64 + ln;
+  d[0] = __builtin_bit_cast(u32x4, sp.hi);
+  d[64] = __builtin_bit_cast(u32x4, sp.mid);
+  d[128] = __builtin_bit_cast(u32x4, sp.lo);
+}
+
+// Copy of one K-step's pre-split operands (NU <= 768 u32x4, contiguous) into LDS;
+// three named registers per thread so nothing is indexed dynamically.
+template <int NU>
+struct SplitCopy {
+  static_assert(NU <= 768, "staging covers at most 3 x 256 u32x4");
+  u32x4 v0, v1, v2;
+};
+
+template <int NU>
+__device__ __forceinline__ void split_copy_load(SplitCopy<NU>& C, const u32x4* __restrict__ src, int tid) {
+  if (NU >= 256 || tid < NU) C.v0 = src[tid];
+  if constexpr (NU > 256) {
+    if (NU >= 512 || tid + 256 < NU) C.v1 = src[tid + 256];
+  }
+  if constexpr (NU > 512) {
+    if (NU >= 768 || tid + 512 < NU) C.v2 = src[tid + 512];
+  }
+}
+
+template <int NU>
+__device__ __forceinline__ void split_copy_store(const SplitCopy<NU>& C, bf16x8* dst, int tid) {
+  u32x4* d = reinterpret_cast<u32x4*>(dst);
+  if (NU >= 256 || tid < NU) d[tid] = C.v0;
+  if constexpr (NU > 256) {
+    if (NU >= 512 || tid + 256 < NU) d[tid + 256] = C.v1;
+  }
+  if constexpr (NU > 512) {
+    if (NU >= 768 || tid + 512 < NU) d[tid + 512] = C.v2;
+  }
+}
 
 __device__ __forceinline__ f32x4 mfma6_16(const Split3& A, const Split3& B, f32x4 acc) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A.mid, B.mid, acc, 0, 0, 0);
@@ -1868,20 +1950,22 @@ __device__ __forceinline__ void thin_x6_store(const ThinX6<RB>& T, bf16x8* tq, i
   }
 }
 
-// ---- row kernel (not transposed): wave = 2 x 16 rows, step = 32 columns;
+constexpr int kRBE = 1;   // 16-row blocks per wave in the fused row kernel
+
+// ---- row kernel (not transposed): wave = kRBE x 16 rows, step = 32 columns;
 // lane (t, g) holds columns 16c + 4g .. +3 (c = 0, 1) of rows 16 rb + t.
 template <int GDT>
 struct RowStepE {
-  f32x4 x[kRB][2];
-  uint2 gb[kRB][2];
-  f32x4 gf[kRB][2];
+  f32x4 x[kRBE][2];
+  uint2 gb[kRBE][2];
+  f32x4 gf[kRBE][2];
 };
 
 template <int GDT>
 __device__ __forceinline__ void rpe_load(RowStepE<GDT>& S, const float* __restrict__ M, const void* __restrict__ G,
                                          long ld_m, long ld_g, int j) {
 #pragma unroll
-  for (int rb = 0; rb < kRB; ++rb)
+  for (int rb = 0; rb < kRBE; ++rb)
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       S.x[rb][c] = *reinterpret_cast<const f32x4*>(M + rb * 16 * ld_m + j + 16 * c);
@@ -1893,30 +1977,30 @@ __device__ __forceinline__ void rpe_load(RowStepE<GDT>& S, const float* __restri
 }
 
 template <int RB, int GDT>
-__device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRB][RB], const bf16x8* tq,
-                                            const bf16x8* rs, const Split3 (&F)[kRB][RB / 2], bool has_ef,
-                                            float* __restrict__ M, long ld_m, int j, int lane, bool& nz) {
+__device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRBE][RB], const bf16x8* tq,
+                                            const bf16x8* rs, const Split3 (&F)[kRBE][RB / 2], bool has_ef,
+                                            float* __restrict__ M, long ld_m, int j, int lane, uint32_t& nzb) {
   constexpr int KK = RB / 2;
   if (has_ef) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      f32x4 e[kRB];
+      f32x4 e[kRBE];
 #pragma unroll
-      for (int rb = 0; rb < kRB; ++rb) e[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int rb = 0; rb < kRBE; ++rb) e[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
         Split3 A;
         ef_sread(rs, c * KK + kk, lane, A);
 #pragma unroll
-        for (int rb = 0; rb < kRB; ++rb) e[rb] = mfma6_16(A, F[rb][kk], e[rb]);
+        for (int rb = 0; rb < kRBE; ++rb) e[rb] = mfma6_16(A, F[rb][kk], e[rb]);
       }
 #pragma unroll
-      for (int rb = 0; rb < kRB; ++rb) S.x[rb][c] += e[rb];
+      for (int rb = 0; rb < kRBE; ++rb) S.x[rb][c] += e[rb];
     }
   }
   if (GDT != DION_DTYPE_NONE || has_ef) {
 #pragma unroll
-    for (int rb = 0; rb < kRB; ++rb)
+    for (int rb = 0; rb < kRBE; ++rb)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         if constexpr (GDT == DION_DTYPE_BF16) {
@@ -1929,20 +2013,24 @@ __device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRB][
           S.x[rb][c] += S.gf[rb][c];
         }
         *reinterpret_cast<f32x4*>(M + rb * 16 * ld_m + j + 16 * c) = S.x[rb][c];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) nz |= (S.x[rb][c][q] != 0.f);
       }
   }
-  // P += X Q: the lane's 8 columns 16 (e >> 2) + 4 g + (e & 3) are the A operand's k-run (KMAP 1)
-  Split3 A[kRB];
 #pragma unroll
-  for (int rb = 0; rb < kRB; ++rb) split3(S.x[rb][0], S.x[rb][1], 1.f, A[rb]);
+  for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      nzb |= __float_as_uint(S.x[rb][c][0]) | __float_as_uint(S.x[rb][c][1]) | __float_as_uint(S.x[rb][c][2]) |
+             __float_as_uint(S.x[rb][c][3]);
+  // P += X Q: the lane's 8 columns 16 (e >> 2) + 4 g + (e & 3) are the A operand's k-run (KMAP 1)
+  Split3 A[kRBE];
+#pragma unroll
+  for (int rb = 0; rb < kRBE; ++rb) split3(S.x[rb][0], S.x[rb][1], 1.f, A[rb]);
 #pragma unroll
   for (int cb = 0; cb < RB; ++cb) {
     Split3 B;
     ef_sread(tq, cb, lane, B);
 #pragma unroll
-    for (int rb = 0; rb < kRB; ++rb) acc[rb][cb] = mfma6_16(A[rb], B, acc[rb][cb]);
+    for (int rb = 0; rb < kRBE; ++rb) acc[rb][cb] = mfma6_16(A[rb], B, acc[rb][cb]);
   }
 }
 
@@ -1960,7 +2048,7 @@ __global__ void __launch_bounds__(256, 2) rowproj_ef_kernel(const EfProjArgs e) 
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
-  const int row_base = blockIdx.x * (64 * kRB) + wave * (16 * kRB);
+  const int row_base = blockIdx.x * (64 * kRBE) + wave * (16 * kRBE);
   const int j_begin = kc * a.kchunk;
   const int j_end = min(a.cols, j_begin + a.kchunk);
   float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 4 * g;
@@ -1973,10 +2061,10 @@ __global__ void __launch_bounds__(256, 2) rowproj_ef_kernel(const EfProjArgs e) 
   const float* __restrict__ Rp = e.efr[b];
   const bool has_ef = Rp != nullptr;
 
-  Split3 F[kRB][KK];
+  Split3 F[kRBE][KK];
   if (has_ef) {
 #pragma unroll
-    for (int rb = 0; rb < kRB; ++rb)
+    for (int rb = 0; rb < kRBE; ++rb)
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
         const float* src = e.efp[b] + static_cast<long>(row_base + 16 * rb + t) * R + 32 * kk + 8 * g;
@@ -1984,27 +2072,32 @@ __global__ void __launch_bounds__(256, 2) rowproj_ef_kernel(const EfProjArgs e) 
       }
   } else {
 #pragma unroll
-    for (int rb = 0; rb < kRB; ++rb)
+    for (int rb = 0; rb < kRBE; ++rb)
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) F[rb][kk] = Split3{};
   }
 
-  f32x4 acc[kRB][RB];
+  f32x4 acc[kRBE][RB];
 #pragma unroll
-  for (int rb = 0; rb < kRB; ++rb)
+  for (int rb = 0; rb < kRBE; ++rb)
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bool nz = false;
+  uint32_t nzb = 0;  // OR of the written bit patterns: nonzero iff some |x| > 0 (or NaN)
 
+  // the K-step's thin (Q) and streamed EF (R') operands arrive pre-split
+  // (presplit_kernel); staging them is a 16-byte copy into double-buffered LDS
+  constexpr int NQ = RB * 3 * 64, NR = 2 * KK * 3 * 64;
+  const u32x4* qs = e.qsplit + b * e.split_stride;
+  const u32x4* rsp = e.rsplit + b * e.split_stride;
   RowStepE<GDT> SA, SB;
-  ThinX6<RB> TA;
-  EfStage<2, KK> EA;
+  SplitCopy<NQ> TA;
+  SplitCopy<NR> EA;
   rpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j_begin);
-  thin_x6_load<RB, 1>(TA, Tp, j_begin, tid);
-  thin_x6_store<RB>(TA, tq[0], tid);
+  split_copy_load<NQ>(TA, qs + static_cast<long>(j_begin / 32) * NQ, tid);
+  split_copy_store<NQ>(TA, tq[0], tid);
   if (has_ef) {
-    ef_sload<2, KK>(EA, Rp, j_begin, tid);
-    ef_sstore<2, KK>(EA, rs[0], tid);
+    split_copy_load<NR>(EA, rsp + static_cast<long>(j_begin / 32) * NR, tid);
+    split_copy_store<NR>(EA, rs[0], tid);
   }
   __syncthreads();
   int cur = 0;
@@ -2012,38 +2105,38 @@ __global__ void __launch_bounds__(256, 2) rowproj_ef_kernel(const EfProjArgs e) 
     const bool more = j0 + 32 < j_end;
     if (more) {
       rpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, j0 + 32);
-      thin_x6_load<RB, 1>(TA, Tp, j0 + 32, tid);
-      if (has_ef) ef_sload<2, KK>(EA, Rp, j0 + 32, tid);
+      split_copy_load<NQ>(TA, qs + static_cast<long>(j0 / 32 + 1) * NQ, tid);
+      if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(j0 / 32 + 1) * NR, tid);
     }
-    rpe_compute<RB, GDT>(SA, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, j0, lane, nz);
+    rpe_compute<RB, GDT>(SA, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, j0, lane, nzb);
     if (!more) break;
-    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
-    if (has_ef) ef_sstore<2, KK>(EA, rs[cur ^ 1], tid);
+    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
+    if (has_ef) split_copy_store<NR>(EA, rs[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
     const bool more2 = j0 + 64 < j_end;
     if (more2) {
       rpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j0 + 64);
-      thin_x6_load<RB, 1>(TA, Tp, j0 + 64, tid);
-      if (has_ef) ef_sload<2, KK>(EA, Rp, j0 + 64, tid);
+      split_copy_load<NQ>(TA, qs + static_cast<long>(j0 / 32 + 2) * NQ, tid);
+      if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(j0 / 32 + 2) * NR, tid);
     }
-    rpe_compute<RB, GDT>(SB, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, j0 + 32, lane, nz);
+    rpe_compute<RB, GDT>(SB, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, j0 + 32, lane, nzb);
     if (!more2) break;
-    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
-    if (has_ef) ef_sstore<2, KK>(EA, rs[cur ^ 1], tid);
+    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
+    if (has_ef) split_copy_store<NR>(EA, rs[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
   }
 
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
 #pragma unroll
-  for (int rb = 0; rb < kRB; ++rb)
+  for (int rb = 0; rb < kRBE; ++rb)
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         out[static_cast<long>(row_base + 16 * rb + 4 * g + q) * R + 16 * cb + t] = acc[rb][cb][q];
-  if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+  if (a.nonzero != nullptr && __any((nzb & 0x7FFFFFFFu) != 0u) && lane == 0) atomicOr(&a.nonzero[b], 1u);
 }
 
 // ---- column kernel (transposed): block = 4 waves x 32 columns, step = 32 rows;
@@ -2076,7 +2169,7 @@ __device__ __forceinline__ void cpe_load(ColStepE<GDT>& S, const float* __restri
 template <int RB, int GDT>
 __device__ __forceinline__ void cpe_compute(ColStepE<GDT>& S, f32x4 (&acc)[2][RB], const bf16x8* tq,
                                             const bf16x8* rs, const Split3 (&F)[2][RB / 2], bool has_ef,
-                                            float* __restrict__ M, long ld_m, int i0, int lane, bool& nz) {
+                                            float* __restrict__ M, long ld_m, int i0, int lane, uint32_t& nzb) {
   constexpr int KK = RB / 2;
   if (has_ef) {
 #pragma unroll
@@ -2108,9 +2201,12 @@ __device__ __forceinline__ void cpe_compute(ColStepE<GDT>& S, f32x4 (&acc)[2][RB
           S.x[h][q] += S.gf[h][q];
         }
         *reinterpret_cast<f32x2*>(M + static_cast<long>(i0 + 16 * h + q) * ld_m) = S.x[h][q];
-        nz |= (S.x[h][q][0] != 0.f) | (S.x[h][q][1] != 0.f);
       }
   }
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) nzb |= __float_as_uint(S.x[h][q][0]) | __float_as_uint(S.x[h][q][1]);
   Split3 A[2];
 #pragma unroll
   for (int c = 0; c < 2; ++c)
@@ -2174,17 +2270,22 @@ __global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) 
   for (int c = 0; c < 2; ++c)
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bool nz = false;
+  uint32_t nzb = 0;
 
+  // the K-step's thin (Q) and streamed EF (R') operands arrive pre-split
+  // (presplit_kernel); staging them is a 16-byte copy into double-buffered LDS
+  constexpr int NQ = RB * 3 * 64, NR = 2 * KK * 3 * 64;
+  const u32x4* qs = e.qsplit + b * e.split_stride;
+  const u32x4* rsp = e.rsplit + b * e.split_stride;
   ColStepE<GDT> SA, SB;
-  ThinX6<RB> TA;
-  EfStage<2, KK> EA;
+  SplitCopy<NQ> TA;
+  SplitCopy<NR> EA;
   cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i_begin);
-  thin_x6_load<RB, 1>(TA, Tp, i_begin, tid);
-  thin_x6_store<RB>(TA, tq[0], tid);
+  split_copy_load<NQ>(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
+  split_copy_store<NQ>(TA, tq[0], tid);
   if (has_ef) {
-    ef_sload<2, KK>(EA, Rp, i_begin, tid);
-    ef_sstore<2, KK>(EA, rs[0], tid);
+    split_copy_load<NR>(EA, rsp + static_cast<long>(i_begin / 32) * NR, tid);
+    split_copy_store<NR>(EA, rs[0], tid);
   }
   __syncthreads();
   int cur = 0;
@@ -2192,25 +2293,25 @@ __global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) 
     const bool more = i0 + 32 < i_end;
     if (more) {
       cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
-      thin_x6_load<RB, 1>(TA, Tp, i0 + 32, tid);
-      if (has_ef) ef_sload<2, KK>(EA, Rp, i0 + 32, tid);
+      split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 1) * NQ, tid);
+      if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 1) * NR, tid);
     }
-    cpe_compute<RB, GDT>(SA, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, i0, lane, nz);
+    cpe_compute<RB, GDT>(SA, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, i0, lane, nzb);
     if (!more) break;
-    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
-    if (has_ef) ef_sstore<2, KK>(EA, rs[cur ^ 1], tid);
+    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
+    if (has_ef) split_copy_store<NR>(EA, rs[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
     const bool more2 = i0 + 64 < i_end;
     if (more2) {
       cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
-      thin_x6_load<RB, 1>(TA, Tp, i0 + 64, tid);
-      if (has_ef) ef_sload<2, KK>(EA, Rp, i0 + 64, tid);
+      split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 2) * NQ, tid);
+      if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 2) * NR, tid);
     }
-    cpe_compute<RB, GDT>(SB, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, i0 + 32, lane, nz);
+    cpe_compute<RB, GDT>(SB, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, i0 + 32, lane, nzb);
     if (!more2) break;
-    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
-    if (has_ef) ef_sstore<2, KK>(EA, rs[cur ^ 1], tid);
+    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
+    if (has_ef) split_copy_store<NR>(EA, rs[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
   }
@@ -2223,7 +2324,7 @@ __global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) 
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         out[static_cast<long>(col_base + 2 * (4 * g + q) + c) * R + 16 * cb + t] = acc[c][cb][q];
-  if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+  if (a.nonzero != nullptr && __any((nzb & 0x7FFFFFFFu) != 0u) && lane == 0) atomicOr(&a.nonzero[b], 1u);
 }
 
 // ---- row projection, no gradient (pass B, transposed: R = M P):
@@ -2491,14 +2592,18 @@ Geo colx6_geo(int rows, int cols, int batch, int r) {
 bool rowproj_fast_ok(int rows, int cols, int r) { return rows % (64 * kRB) == 0 && cols % 32 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
 bool colproj_fast_ok(int rows, int cols, int r) { return cols % 256 == 0 && rows % 16 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
 
+// two pre-split operand buffers (Q and R', n_Q x r each) of dion_project_p_ef, after the slabs
+size_t presplit_stride(int nq, int r) { return static_cast<size_t>(nq) * r * 3 / 8; }  // uint4 per matrix
+size_t presplit_bytes(int nq, int r, int batch) { return 2 * 16 * presplit_stride(nq, r) * batch + 256; }
+
 // deferred-EF pass A (rowproj_ef_kernel / colproj_ef_kernel)
 bool proj_ef_ok(int m, int n, int r, bool transposed) {
   if (r != 32 && r != 64) return false;
-  return transposed ? (n % 128 == 0 && m % 32 == 0) : (m % (64 * kRB) == 0 && n % 32 == 0);
+  return transposed ? (n % 128 == 0 && m % 32 == 0) : (m % (64 * kRBE) == 0 && n % 32 == 0);
 }
 
 Geo proj_ef_geo(int m, int n, int batch, bool transposed) {
-  if (!transposed) return rowproj_geo(m, n, batch, 64 * kRB);
+  if (!transposed) return rowproj_geo(m, n, batch, 64 * kRBE);
   Geo g;
   g.gx = static_cast<int>(ceil_div(n, 128));
   long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
@@ -2830,7 +2935,8 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
       case DION_OP_PROJECT_P_EF: {
         if (!proj_ef_ok(d->m, d->n, d->r, d->transposed != 0))
           return fail(DION_E_UNSUPPORTED, "no deferred-EF pass A for %dx%d r=%d", d->m, d->n, d->r);
-        n = slab_bytes(proj_ef_geo(d->m, d->n, chunk, d->transposed != 0), chunk, d->r);
+        n = slab_bytes(proj_ef_geo(d->m, d->n, chunk, d->transposed != 0), chunk, d->r) +
+            presplit_bytes(nq, d->r, chunk);
         break;
       }
       case DION_OP_ORTHONORMALIZE: {
@@ -2899,9 +3005,34 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
   for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
     const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
     const Geo geo = proj_ef_geo(d->m, d->n, nb, tr);
-    const size_t need = slab_bytes(geo, nb, d->r);
-    if (need > ws_bytes || (need > 0 && ws == nullptr))
+    const int nq = tr ? d->m : d->n;
+    const size_t slab = (slab_bytes(geo, nb, d->r) + 255) / 256 * 256;
+    const size_t need = slab + presplit_bytes(nq, d->r, nb);
+    if (need > ws_bytes || ws == nullptr)
       return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
+    const long sstride = static_cast<long>(presplit_stride(nq, d->r));
+    u32x4* qsplit = reinterpret_cast<u32x4*>(static_cast<char*>(ws) + slab);
+    u32x4* rsplit = qsplit + sstride * nb;
+    {
+      PresplitArgs pa;
+      memset(&pa, 0, sizeof(pa));
+      pa.rows = nq;
+      pa.r = d->r;
+      pa.stride = sstride;
+      const dim3 pgrid(static_cast<unsigned>(ceil_div(static_cast<long>(nq) * d->r / 8, 256)), nb);
+      for (int b = 0; b < nb; ++b) pa.src[b] = Q[b0 + b];
+      pa.dst = qsplit;
+      pa.layout = 0;
+      pa.kmap = 1;
+      hipLaunchKernelGGL(presplit_kernel, pgrid, dim3(256), 0, st, pa);
+      for (int b = 0; b < nb; ++b) pa.src[b] = ef->R[b0 + b];
+      pa.dst = rsplit;
+      pa.layout = 1;
+      pa.kmap = 0;
+      hipLaunchKernelGGL(presplit_kernel, pgrid, dim3(256), 0, st, pa);
+      rc = check_launch("presplit");
+      if (rc != DION_OK) return rc;
+    }
     float* out = P + static_cast<long>(b0) * mp * d->r;
     EfProjArgs e;
     memset(&e, 0, sizeof(e));
@@ -2914,6 +3045,9 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
       e.efr[b] = ef->R[b0 + b];
     }
     e.alpha = ef->alpha;
+    e.qsplit = qsplit;
+    e.rsplit = rsplit;
+    e.split_stride = sstride;
     a.out = geo.nchunk > 1 ? static_cast<float*>(ws) : out;
     a.nonzero = nonzero ? nonzero + b0 : nullptr;
     a.rows = d->m;

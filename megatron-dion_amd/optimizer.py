@@ -75,6 +75,7 @@ class MegatronDion(Optimizer):
         self._local_streams = max(1, int(local_streams))
         self._coalesce_max = max(1, int(coalesce_max_entries))
         self._streams = None
+        self._rstreams = None
         self._codec = codec
         self._defer_ef = bool(defer_error_feedback)
         self._profile_records: List[Tuple[str, float]] = []
@@ -145,6 +146,17 @@ class MegatronDion(Optimizer):
             main.wait_stream(s)
         return True
 
+    def _replica_streams(self, batches, width):
+        """One HIP stream per AsyncRuntime slot for replicated (W > 1) batches on the GPU."""
+        if self._local_streams <= 1 or not torch.cuda.is_available() or not batches:
+            return None
+        if not all(getattr(b.params[0], "is_cuda", False) for b in batches if b.params):
+            return None
+        dev = batches[0].params[0].device
+        if self._rstreams is None or len(self._rstreams) != width or self._rstreams[0].device != dev:
+            self._rstreams = [torch.cuda.Stream(device=dev) for _ in range(width)]
+        return self._rstreams
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -164,8 +176,14 @@ class MegatronDion(Optimizer):
         sketches = getattr(self, "_sketch_override", None)
         batches = self._batches()
         if not self._run_local_overlapped(batches, sketches):
+            streams = self._replica_streams(batches, width)
+            main = torch.cuda.current_stream(streams[0].device) if streams else None
+            for s in streams or ():
+                s.wait_stream(main)
             AsyncRuntime((run_dion_batch_async(self, b, sketches=sketches(b) if sketches else None)
-                          for b in batches), width).run()
+                          for b in batches), width, streams=streams).run()
+            for s in streams or ():
+                main.wait_stream(s)
         if profile:
             torch.cuda.synchronize()
             self._profile_records.append(("step", time.perf_counter() - t0))

@@ -26,16 +26,23 @@ from .kernels import scaled_lr_for_shape
 class AsyncRuntime:
     """Round-robin driver of batch generators with bounded width."""
 
-    def __init__(self, tasks: Iterable[Generator], max_concurrent_tasks: int = 3):
+    def __init__(self, tasks: Iterable[Generator], max_concurrent_tasks: int = 3, streams=None):
         if int(max_concurrent_tasks) <= 0:
             raise ValueError(f"Invalid max_concurrent_tasks={max_concurrent_tasks}")
         self.tasks = tasks
         self.width = int(max_concurrent_tasks)
+        # optional HIP streams: the k-th admitted task always runs on streams[k % len], so a
+        # batch's latency-bound orthonormalisation overlaps the other batches' streaming passes
+        self.streams = list(streams) if streams else None
 
     @staticmethod
-    def _advance(gen) -> bool:
+    def _advance(gen, stream=None) -> bool:
         try:
-            next(gen)
+            if stream is None:
+                next(gen)
+            else:
+                with torch.cuda.stream(stream):
+                    next(gen)
             return True
         except StopIteration:
             return False
@@ -43,18 +50,22 @@ class AsyncRuntime:
     def run(self) -> None:
         pending = iter(self.tasks)
         more = True
-        live: List[Generator] = []
+        admitted = 0
+        live: List[tuple] = []
         while more or live:
-            nxt: List[Generator] = []
+            nxt: List[tuple] = []
             if more and len(live) < self.width:
                 gen = next(pending, None)
                 if gen is None:
                     more = False
-                elif self._advance(gen):
-                    nxt.append(gen)
-            for gen in live:
-                if self._advance(gen):
-                    nxt.append(gen)
+                else:
+                    stream = self.streams[admitted % len(self.streams)] if self.streams else None
+                    admitted += 1
+                    if self._advance(gen, stream):
+                        nxt.append((gen, stream))
+            for gen, stream in live:
+                if self._advance(gen, stream):
+                    nxt.append((gen, stream))
             live = nxt
 
 
