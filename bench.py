@@ -46,12 +46,12 @@ KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("project_p", True): ("colproj_fast_kernel<4, 2>", 1),
              ("project_p_ef", False): ("rowproj_ef_kernel<4, 2>", 1),
              ("project_p_ef", True): ("colproj_ef_kernel<4, 2>", 1),
-             ("ef_apply_w", False): ("rank_update_kernel<4, false>", 1),
-             ("ef_apply_w", True): ("rank_update_kernel<4, true>", 1),
+             ("ef_apply_w", False): ("rank_update_kernel<4, false, true>", 1),
+             ("ef_apply_w", True): ("rank_update_kernel<4, true, true>", 1),
              ("project_r", False): ("colproj_x6_kernel<4>", 1),
              ("project_r", True): ("rowproj_x6_kernel<4>", 1),
-             ("ef_apply", False): ("rank_update_kernel<4, false>", 2),
-             ("ef_apply", True): ("rank_update_kernel<4, true>", 2)}
+             ("ef_apply", False): ("rank_update_kernel<4, false, true>", 2),
+             ("ef_apply", True): ("rank_update_kernel<4, true, true>", 2)}
 
 
 class TimedCodec:
@@ -174,6 +174,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams for independent batches (N=1 path)")
     ap.add_argument("--probe-steps", type=int, default=2, help="single-stream steps timed per kernel for `roofline`")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="collective backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     ap.add_argument("--eager-ef", action="store_true",
                     help="apply each step's error feedback in its own pass (default: deferred into the next pass A)")
     args = ap.parse_args()
@@ -181,11 +183,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":
+        # rehearsal of the multi-rank path on fewer GPUs than ranks (gloo exchanges through the host)
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         group = dist.group.WORLD
 
     import megatron_dion_amd as mda

@@ -35,7 +35,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 3
+#define DION_ABI_VERSION 4
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -53,6 +53,7 @@ typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 #define DION_OP_PROJECT_R 3
 #define DION_OP_FIXUP_COLNORM 4
 #define DION_OP_PROJECT_P_EF 5 /* DION_E_UNSUPPORTED: no fused kernel for this shape */
+#define DION_OP_EF_APPLY 6     /* optional: pre-split P for the rank-update kernels   */
 
 typedef struct DionBatchDesc {
   int32_t batch;      /* matrices in this call (all the same shape)            */
@@ -150,11 +151,13 @@ int dion_fixup_colnorm(const DionBatchDesc* desc, float* P, float* R, float* con
  * (error feedback only); M may be NULL (weight update only, the deferred-EF
  * schedule; DION_E_UNSUPPORTED for shapes without the rank-update kernel).
  * Entries with nonzero[b] == 0 keep M and only decay W.
+ * `ws` is optional: with dion_workspace_bytes(desc, DION_OP_EF_APPLY) bytes the
+ * streamed factor P is split into bf16 limbs once per call instead of per tile.
  */
 int dion_ef_apply(const DionBatchDesc* desc, float* const* M, float* const* W,
                   const float* P, const float* R, const float* const* Qn,
                   const uint32_t* nonzero, float mu, float lr, float wd, float scaled_lr,
-                  dion_stream_t stream);
+                  void* ws, size_t ws_bytes, dion_stream_t stream);
 
 #ifdef __cplusplus
 }

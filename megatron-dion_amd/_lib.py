@@ -11,7 +11,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "csrc", "libdion_codec.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -28,6 +28,7 @@ OP_ORTHONORMALIZE = 2
 OP_PROJECT_R = 3
 OP_FIXUP_COLNORM = 4
 OP_PROJECT_P_EF = 5
+OP_EF_APPLY = 6
 
 # every symbol include/dion_codec.h declares
 EXPORTED = (
@@ -84,7 +85,7 @@ _SIGNATURES = {
     "dion_project_r": ([_DESC, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_fixup_colnorm": ([_DESC, _P, _P, _PP, _P, ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_ef_apply": ([_DESC, _PP, _PP, _P, _P, _PP, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
-                       ctypes.c_float, _P], ctypes.c_int),
+                       ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
 }
 
 _lib = None

@@ -1605,6 +1605,9 @@ struct RankArgs {
   float* x[MAXB];            // M or W per matrix
   const float* fixed[MAXB];  // factor indexed by the fixed strip (R_b or Qn_b)
   const float* S;            // streamed factor base: P (batch, len, r)
+  const u32x4* Ssplit;       // P pre-split (presplit_kernel layout 2), or null
+  long ss_stride;            // 16-byte units per matrix of Ssplit
+  int s_len;                 // streamed extent per block (multiple of 64)
   const uint32_t* nonzero;
   long s_stride;             // elements between consecutive P_b
   int rows, cols;
@@ -1643,13 +1646,19 @@ __device__ __forceinline__ f32x16 mfma6(const Split3& A, const Split3& B, f32x16
   return acc;
 }
 
-template <int RU>
+template <int RU, bool PRE>
 struct RTile {
-  f32x4 s[RU][2];  // streamed factor row: 8 consecutive values per k-step
+  f32x4 s[RU][2];  // streamed factor row: 8 consecutive values per k-step (fp32, split per tile)
   f32x16 x;        // X tile (accumulator layout)
 };
 
-template <int RU, bool ROWFIX>
+template <int RU>
+struct RTile<RU, true> {
+  u32x4 s[RU][3];  // streamed factor row, pre-split hi / mid / lo (presplit_kernel layout 2)
+  f32x16 x;
+};
+
+template <int RU, bool ROWFIX, bool PRE>
 __global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const RankArgs a) {
   constexpr int R = 16 * RU;
   const int b = blockIdx.z;
@@ -1661,8 +1670,8 @@ __global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const
   if (a.skip_zero && __builtin_amdgcn_readfirstlane(a.nonzero[b]) == 0u) return;
   const int fbase = blockIdx.x * 128 + wave * 32;
   if (fbase >= (ROWFIX ? rows : cols)) return;
-  const int s_begin = blockIdx.y * kEfStream;
-  const int s_end = min(ROWFIX ? cols : rows, s_begin + kEfStream);
+  const int s_begin = blockIdx.y * a.s_len;
+  const int s_end = min(ROWFIX ? cols : rows, s_begin + a.s_len);
   const int ld = static_cast<int>(a.ld);
   const float* Sb = a.S + static_cast<long>(b) * a.s_stride;
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
@@ -1681,12 +1690,21 @@ __global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const
              a.scale, F[u]);
   }
 
-  auto load = [&](int s0, RTile<RU>& T) {
-    const float* sp = Sb + static_cast<long>(s0 + t) * R + 8 * h;
+  const u32x4* Sq = PRE ? a.Ssplit + b * a.ss_stride + lane : nullptr;
+  auto load = [&](int s0, RTile<RU, PRE>& T) {
+    if constexpr (PRE) {
+      const u32x4* sq = Sq + static_cast<long>(s0 / 32) * RU * 3 * 64;
 #pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      T.s[u][0] = *reinterpret_cast<const f32x4*>(sp + 16 * u);
-      T.s[u][1] = *reinterpret_cast<const f32x4*>(sp + 16 * u + 4);
+      for (int u = 0; u < RU; ++u)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) T.s[u][p] = sq[(u * 3 + p) * 64];
+    } else {
+      const float* sp = Sb + static_cast<long>(s0 + t) * R + 8 * h;
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        T.s[u][0] = *reinterpret_cast<const f32x4*>(sp + 16 * u);
+        T.s[u][1] = *reinterpret_cast<const f32x4*>(sp + 16 * u + 4);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     const int row0 = ROWFIX ? fbase : s0;
@@ -1696,14 +1714,20 @@ __global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const
     for (int q = 0; q < 16; ++q)
       T.x[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff[q], so, 0));
   };
-  auto compute = [&](int s0, RTile<RU>& T) {
+  auto compute = [&](int s0, RTile<RU, PRE>& T) {
     f32x16 acc;
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       Split3 Sp;
-      split3(T.s[u][0], T.s[u][1], 1.f, Sp);
+      if constexpr (PRE) {
+        Sp.hi = __builtin_bit_cast(bf16x8, T.s[u][0]);
+        Sp.mid = __builtin_bit_cast(bf16x8, T.s[u][1]);
+        Sp.lo = __builtin_bit_cast(bf16x8, T.s[u][2]);
+      } else {
+        split3(T.s[u][0], T.s[u][1], 1.f, Sp);
+      }
       acc = ROWFIX ? mfma6(F[u], Sp, acc) : mfma6(Sp, F[u], acc);
     }
     const int row0 = ROWFIX ? fbase : s0;
@@ -1715,15 +1739,16 @@ __global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[q], so, 0);
     }
   };
-  auto touch_s = [&](RTile<RU>& T) {
+  auto touch_s = [&](RTile<RU, PRE>& T) {
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       asm volatile("" ::"v"(T.s[u][0]));
       asm volatile("" ::"v"(T.s[u][1]));
+      if constexpr (PRE) asm volatile("" ::"v"(T.s[u][2]));
     }
   };
 
-  RTile<RU> A, B;
+  RTile<RU, PRE> A, B;
   load(s_begin, A);
   touch_s(A);
   __builtin_amdgcn_sched_barrier(0);
@@ -1802,11 +1827,20 @@ __global__ void __launch_bounds__(256) presplit_kernel(const PresplitArgs a) {
       const int k = a.kmap == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
       v[e] = src[(blk * 32 + k) * a.r + 16 * cb + t];
     }
-  } else {
+  } else if (a.layout == 1) {
     const int KK = a.r / 32;
     const long blk = grp / KK;
     const int kk = static_cast<int>(grp - blk * KK);
     const float* p = src + (blk * 16 + t) * a.r + 32 * kk + 8 * g;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = p[e];
+  } else {
+    // layout 2 (32x32x16 operand of rank_update_kernel): grp = (row / 32) * RU + u,
+    // lane (t5 = lane & 31, h = lane >> 5) <- row 32 blk + t5, columns 16 u + 8 h + e
+    const int RU = a.r / 16;
+    const long blk = grp / RU;
+    const int u = static_cast<int>(grp - blk * RU);
+    const float* p = src + (blk * 32 + (ln & 31)) * a.r + 16 * u + 8 * (ln >> 5);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = p[e];
   }
@@ -2592,6 +2626,19 @@ Geo colx6_geo(int rows, int cols, int batch, int r) {
 bool rowproj_fast_ok(int rows, int cols, int r) { return rows % (64 * kRB) == 0 && cols % 32 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
 bool colproj_fast_ok(int rows, int cols, int r) { return cols % 256 == 0 && rows % 16 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
 
+// rows (or columns) one rank-update block streams; DION_RANK_STREAM overrides (tuning)
+int rank_stream_len() {
+  static const int v = [] {
+    const char* e = getenv("DION_RANK_STREAM");
+    const int x = e ? atoi(e) : 0;
+    return (x >= 64 && x % 64 == 0) ? x : 512;
+  }();
+  return v;
+}
+
+// pre-split streamed factor P (m_P x r per matrix) of the rank-update kernels
+size_t ef_presplit_bytes(int mp, int r, int batch) { return static_cast<size_t>(mp) * r * 6 * batch; }
+
 // two pre-split operand buffers (Q and R', n_Q x r each) of dion_project_p_ef, after the slabs
 size_t presplit_stride(int nq, int r) { return static_cast<size_t>(nq) * r * 3 / 8; }  // uint4 per matrix
 size_t presplit_bytes(int nq, int r, int batch) { return 2 * 16 * presplit_stride(nq, r) * batch + 256; }
@@ -2939,6 +2986,9 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
             presplit_bytes(nq, d->r, chunk);
         break;
       }
+      case DION_OP_EF_APPLY:
+        n = ef_presplit_bytes(mp, d->r, chunk);
+        break;
       case DION_OP_ORTHONORMALIZE: {
         // k = ceil(oversample r / 128) * 128 is bounded by the value at oversample 2
         n = ortho_plan(mp, d->r, chunk, 2.0f).total;
@@ -3214,7 +3264,7 @@ int dion_fixup_colnorm(const DionBatchDesc* d, float* P, float* R, float* const*
 
 int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, const float* P, const float* R,
                   const float* const* Qn, const uint32_t* nonzero, float mu, float lr, float wd, float scaled_lr,
-                  dion_stream_t stream) {
+                  void* ws, size_t ws_bytes, dion_stream_t stream) {
   int rc = validate(d);
   if (rc != DION_OK) return rc;
   if (P == nullptr || R == nullptr || Qn == nullptr || nonzero == nullptr || (M == nullptr && W == nullptr))
@@ -3261,7 +3311,27 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
     if (split_ok) {
       const int flen = d->transposed ? d->m : d->n;
       const int slen = d->transposed ? d->n : d->m;
-      const dim3 grid(static_cast<unsigned>(ceil_div(flen, 128)), static_cast<unsigned>(ceil_div(slen, kEfStream)), nb);
+      const int s_len = rank_stream_len();
+      const dim3 grid(static_cast<unsigned>(ceil_div(flen, 128)), static_cast<unsigned>(ceil_div(slen, s_len)), nb);
+      // the streamed factor P split once per call (instead of once per tile per wave) when the
+      // caller gave the workspace dion_workspace_bytes(DION_OP_EF_APPLY) asks for
+      const long sstride = static_cast<long>(mp) * r * 3 / 8;
+      const bool pre = ws != nullptr && ws_bytes >= ef_presplit_bytes(mp, r, nb) && (mp % 32 == 0);
+      u32x4* ssplit = static_cast<u32x4*>(ws);
+      if (pre) {
+        PresplitArgs pa;
+        memset(&pa, 0, sizeof(pa));
+        for (int b = 0; b < nb; ++b) pa.src[b] = a.P + static_cast<long>(b) * mp * r;
+        pa.dst = ssplit;
+        pa.stride = sstride;
+        pa.rows = mp;
+        pa.r = r;
+        pa.layout = 2;
+        const dim3 pgrid(static_cast<unsigned>(ceil_div(static_cast<long>(mp) * r / 8, 256)), nb);
+        hipLaunchKernelGGL(presplit_kernel, pgrid, dim3(256), 0, st, pa);
+        rc = check_launch("presplit(P)");
+        if (rc != DION_OK) return rc;
+      }
       for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1 && W == nullptr) break;
         if (pass == 0 && M == nullptr) continue;
@@ -3273,6 +3343,9 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
         }
         ra.S = a.P;
         ra.s_stride = static_cast<long>(mp) * r;
+        ra.Ssplit = pre ? ssplit : nullptr;
+        ra.s_len = s_len;
+        ra.ss_stride = sstride;
         ra.nonzero = a.nonzero;
         ra.rows = d->m;
         ra.cols = d->n;
@@ -3282,10 +3355,14 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
         ra.skip_zero = pass == 0 ? 1 : 0;
         auto launch = [&](auto RUc) {
           constexpr int RUv = decltype(RUc)::value;
-          if (d->transposed)
-            hipLaunchKernelGGL((rank_update_kernel<RUv, true>), grid, dim3(256), 0, st, ra);
+          if (pre && d->transposed)
+            hipLaunchKernelGGL((rank_update_kernel<RUv, true, true>), grid, dim3(256), 0, st, ra);
+          else if (pre)
+            hipLaunchKernelGGL((rank_update_kernel<RUv, false, true>), grid, dim3(256), 0, st, ra);
+          else if (d->transposed)
+            hipLaunchKernelGGL((rank_update_kernel<RUv, true, false>), grid, dim3(256), 0, st, ra);
           else
-            hipLaunchKernelGGL((rank_update_kernel<RUv, false>), grid, dim3(256), 0, st, ra);
+            hipLaunchKernelGGL((rank_update_kernel<RUv, false, false>), grid, dim3(256), 0, st, ra);
         };
         switch (r / 16) {
           case 1: launch(std::integral_constant<int, 1>{}); break;

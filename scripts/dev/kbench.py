@@ -11,6 +11,7 @@ B, r = 16 if not T else 16, 64
 mp, nq = (n, m) if T else (m, n)
 dev = torch.device("cuda", 0)
 codec = HipDionCodec(dev)
+codec.ef_presplit = "nopre" not in op
 torch.manual_seed(0)
 Ms = [torch.randn(m, n, device=dev) * 1e-3 for _ in range(B)]
 Gs = [(torch.randn(m, n, device=dev) * 1e-3).to(torch.bfloat16) for _ in range(B)]
@@ -33,9 +34,15 @@ def run():
     elif op.startswith("efm"):
         codec.ef_apply(Ms, None, P, R, Qs, nz, 0.95, 0.01, 0.01, 0.5, T)
 run(); torch.cuda.synchronize()
-t0 = time.perf_counter()
-for _ in range(reps):
-    run()
-torch.cuda.synchronize()
-dt = (time.perf_counter() - t0) / reps
-print(f"{op}: {dt*1e3:.3f} ms per call, {B*m*n/dt/1e9:.1f} Gelem/s")
+variants = [op] if len(sys.argv) <= 3 else sys.argv[3].split(",")
+for rnd in range(3):
+    for v in variants:
+        op = v
+        codec.ef_presplit = "nopre" not in op
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        print(f"round {rnd} {op}: {dt*1e3:.3f} ms per call, {B*m*n/dt/1e9:.1f} Gelem/s")
