@@ -46,12 +46,12 @@ KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("project_p", True): ("colproj_fast_kernel<4, 2>", 1),
              ("project_p_ef", False): ("rowproj_ef_kernel<4, 2>", 1),
              ("project_p_ef", True): ("colproj_ef_kernel<4, 2>", 1),
-             ("ef_apply_w", False): ("rank_update_kernel<4, false, true>", 1),
-             ("ef_apply_w", True): ("rank_update_kernel<4, true, true>", 1),
+             ("ef_apply_w", False): ("rank_update_kernel<4, false, false>", 1),
+             ("ef_apply_w", True): ("rank_update_kernel<4, true, false>", 1),
              ("project_r", False): ("colproj_x6_kernel<4>", 1),
              ("project_r", True): ("rowproj_x6_kernel<4>", 1),
-             ("ef_apply", False): ("rank_update_kernel<4, false, true>", 2),
-             ("ef_apply", True): ("rank_update_kernel<4, true, true>", 2)}
+             ("ef_apply", False): ("rank_update_kernel<4, false, false>", 2),
+             ("ef_apply", True): ("rank_update_kernel<4, true, false>", 2)}
 
 
 class TimedCodec:
@@ -174,6 +174,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams for independent batches (N=1 path)")
     ap.add_argument("--probe-steps", type=int, default=2, help="single-stream steps timed per kernel for `roofline`")
+    ap.add_argument("--coalesce", type=int, default=16, help="matrices per launch group at N = 1")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="collective backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     ap.add_argument("--eager-ef", action="store_true",
@@ -209,7 +210,8 @@ def main():
         named.append((name, w))
     codec = TimedCodec(HipDionCodec(dev))
     opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=1 / 64,
-                           codec=codec, local_streams=args.streams, defer_error_feedback=not args.eager_ef)
+                           codec=codec, local_streams=args.streams, defer_error_feedback=not args.eager_ef,
+                           coalesce_max_entries=args.coalesce)
     attach_dp_routing(opt, named, replicate_group=group)
     elems = sum(m * n for _, m, n in shapes)
 

@@ -10,7 +10,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "csrc", "libdion_codec.so")
+# DION_LIB_PATH: load another build of the same ABI (kernel-variant A/B runs during tuning)
+LIB_PATH = os.environ.get("DION_LIB_PATH") or os.path.join(HERE, "csrc", "libdion_codec.so")
 ABI_VERSION = 4
 
 DION_OK = 0

@@ -1984,7 +1984,10 @@ __device__ __forceinline__ void thin_x6_store(const ThinX6<RB>& T, bf16x8* tq, i
   }
 }
 
-constexpr int kRBE = 1;   // 16-row blocks per wave in the fused row kernel
+#ifndef DION_KRBE
+#define DION_KRBE 2
+#endif
+constexpr int kRBE = DION_KRBE;   // 16-row blocks per wave in the fused row kernel (tuning knob)
 
 // ---- row kernel (not transposed): wave = kRBE x 16 rows, step = 32 columns;
 // lane (t, g) holds columns 16c + 4g .. +3 (c = 0, 1) of rows 16 rb + t.
