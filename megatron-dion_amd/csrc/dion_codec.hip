@@ -112,6 +112,8 @@ struct ProjArgs {
   long ld_m, ld_g;
   int kchunk, nchunk, out_rows;
   int vec;                 // 16-byte loads allowed
+  const void* tsplit;      // thin operand pre-split (presplit_kernel layout 0, KMAP 0) for the x6 kernels
+  long ts_stride;          // 16-byte units per matrix of tsplit
 };
 
 // ============================================================================
@@ -1852,35 +1854,26 @@ __global__ void __launch_bounds__(256) presplit_kernel(const PresplitArgs a) {
   d[128] = __builtin_bit_cast(u32x4, sp.lo);
 }
 
-// Copy of one K-step's pre-split operands (NU <= 768 u32x4, contiguous) into LDS;
-// three named registers per thread so nothing is indexed dynamically.
+// Copy of one K-step's pre-split operands (NU 16-byte units, contiguous) into LDS.
 template <int NU>
 struct SplitCopy {
-  static_assert(NU <= 768, "staging covers at most 3 x 256 u32x4");
-  u32x4 v0, v1, v2;
+  static constexpr int kPer = (NU + 255) / 256;
+  u32x4 v[kPer];
 };
 
 template <int NU>
 __device__ __forceinline__ void split_copy_load(SplitCopy<NU>& C, const u32x4* __restrict__ src, int tid) {
-  if (NU >= 256 || tid < NU) C.v0 = src[tid];
-  if constexpr (NU > 256) {
-    if (NU >= 512 || tid + 256 < NU) C.v1 = src[tid + 256];
-  }
-  if constexpr (NU > 512) {
-    if (NU >= 768 || tid + 512 < NU) C.v2 = src[tid + 512];
-  }
+#pragma unroll
+  for (int it = 0; it < SplitCopy<NU>::kPer; ++it)
+    if (NU % 256 == 0 || tid + 256 * it < NU) C.v[it] = src[tid + 256 * it];
 }
 
 template <int NU>
 __device__ __forceinline__ void split_copy_store(const SplitCopy<NU>& C, bf16x8* dst, int tid) {
   u32x4* d = reinterpret_cast<u32x4*>(dst);
-  if (NU >= 256 || tid < NU) d[tid] = C.v0;
-  if constexpr (NU > 256) {
-    if (NU >= 512 || tid + 256 < NU) d[tid + 256] = C.v1;
-  }
-  if constexpr (NU > 512) {
-    if (NU >= 768 || tid + 512 < NU) d[tid + 512] = C.v2;
-  }
+#pragma unroll
+  for (int it = 0; it < SplitCopy<NU>::kPer; ++it)
+    if (NU % 256 == 0 || tid + 256 * it < NU) d[tid + 256 * it] = C.v[it];
 }
 
 __device__ __forceinline__ f32x4 mfma6_16(const Split3& A, const Split3& B, f32x4 acc) {
@@ -2407,31 +2400,33 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
     for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   RowStep<DION_DTYPE_NONE> SA, SB;
-  ThinX6<RB> TA;
+  constexpr int NQ = RB * 3 * 64;
+  const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
+  SplitCopy<NQ> TA;
   rp_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, j_begin);
-  thin_x6_load<RB, 0>(TA, Tp, j_begin, tid);
-  thin_x6_store<RB>(TA, tq[0], tid);
+  split_copy_load<NQ>(TA, qs + static_cast<long>(j_begin / 32) * NQ, tid);
+  split_copy_store<NQ>(TA, tq[0], tid);
   __syncthreads();
   int cur = 0;
   for (int j0 = j_begin; j0 < j_end; j0 += 64) {
     const bool more = j0 + 32 < j_end;
     if (more) {
       rp_load<DION_DTYPE_NONE>(SB, M, nullptr, a.ld_m, 0, j0 + 32);
-      thin_x6_load<RB, 0>(TA, Tp, j0 + 32, tid);
+      split_copy_load<NQ>(TA, qs + static_cast<long>(j0 / 32 + 1) * NQ, tid);
     }
     rpx_compute<RB>(SA, acc, tq[cur], lane);
     if (!more) break;
-    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
+    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
     const bool more2 = j0 + 64 < j_end;
     if (more2) {
       rp_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, j0 + 64);
-      thin_x6_load<RB, 0>(TA, Tp, j0 + 64, tid);
+      split_copy_load<NQ>(TA, qs + static_cast<long>(j0 / 32 + 2) * NQ, tid);
     }
     rpx_compute<RB>(SB, acc, tq[cur], lane);
     if (!more2) break;
-    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
+    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
   }
@@ -2509,31 +2504,33 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_x6_kernel(const 
     for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   ColStepX6<CT> SA, SB;
-  ThinX6<RB> TA;
+  constexpr int NQ = RB * 3 * 64;
+  const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
+  SplitCopy<NQ> TA;
   cpx_load<CT>(SA, M, a.ld_m, i_begin);
-  thin_x6_load<RB, 0>(TA, Tp, i_begin, tid);
-  thin_x6_store<RB>(TA, tq[0], tid);
+  split_copy_load<NQ>(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
+  split_copy_store<NQ>(TA, tq[0], tid);
   __syncthreads();
   int cur = 0;
   for (int i0 = i_begin; i0 < i_end; i0 += 64) {
     const bool more = i0 + 32 < i_end;
     if (more) {
       cpx_load<CT>(SB, M, a.ld_m, i0 + 32);
-      thin_x6_load<RB, 0>(TA, Tp, i0 + 32, tid);
+      split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 1) * NQ, tid);
     }
     cpx_compute<RB, CT>(SA, acc, tq[cur], lane);
     if (!more) break;
-    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
+    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
     const bool more2 = i0 + 64 < i_end;
     if (more2) {
       cpx_load<CT>(SA, M, a.ld_m, i0 + 64);
-      thin_x6_load<RB, 0>(TA, Tp, i0 + 64, tid);
+      split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 2) * NQ, tid);
     }
     cpx_compute<RB, CT>(SB, acc, tq[cur], lane);
     if (!more2) break;
-    thin_x6_store<RB>(TA, tq[cur ^ 1], tid);
+    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
   }
@@ -2638,6 +2635,9 @@ int rank_stream_len() {
   }();
   return v;
 }
+
+// pre-split thin operand of the x6 projections (rows = the contraction index)
+size_t thin_presplit_bytes(int rows, int r, int batch) { return static_cast<size_t>(rows) * r * 6 * batch; }
 
 // pre-split streamed factor P (m_P x r per matrix) of the rank-update kernels
 size_t ef_presplit_bytes(int mp, int r, int batch) { return static_cast<size_t>(mp) * r * 6 * batch; }
@@ -2753,11 +2753,31 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
   const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, fast ? 64 * kRB : 128)
                  : x6      ? colx6_geo(rows, cols, batch, r)
                            : colproj_geo(rows, cols, batch, false);
-  const size_t need = slab_bytes(geo, batch, r);
+  const size_t slab = (slab_bytes(geo, batch, r) + 255) / 256 * 256;
+  const int thin_rows = row_mode ? cols : rows;  // the contraction index
+  const size_t need = slab + (x6 ? thin_presplit_bytes(thin_rows, r, batch) : 0);
   if (need > ws_bytes || (need > 0 && ws == nullptr))
     return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
   ProjArgs a;
   memset(&a, 0, sizeof(a));
+  if (x6) {
+    // the thin operand split into bf16 limbs once per call, in the MFMA B-operand layout
+    PresplitArgs pa;
+    memset(&pa, 0, sizeof(pa));
+    for (int b = 0; b < batch; ++b) pa.src[b] = thin[b];
+    pa.dst = reinterpret_cast<u32x4*>(static_cast<char*>(ws) + slab);
+    pa.stride = static_cast<long>(thin_rows) * r * 3 / 8;
+    pa.rows = thin_rows;
+    pa.r = r;
+    pa.layout = 0;
+    pa.kmap = 0;
+    const dim3 pgrid(static_cast<unsigned>(ceil_div(static_cast<long>(thin_rows) * r / 8, 256)), batch);
+    hipLaunchKernelGGL(presplit_kernel, pgrid, dim3(256), 0, st, pa);
+    int rc = check_launch("presplit(thin)");
+    if (rc != DION_OK) return rc;
+    a.tsplit = pa.dst;
+    a.ts_stride = pa.stride;
+  }
   bool vec = (ld_m % 4) == 0 && (gdt == DION_DTYPE_NONE || (ld_g % (gdt == DION_DTYPE_BF16 ? 8 : 4)) == 0);
   for (int b = 0; b < batch; ++b) {
     a.g[b] = G ? G[b] : nullptr;
@@ -2980,6 +3000,8 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
           const size_t nx = slab_bytes(colx6_geo(d->m, d->n, chunk, d->r), chunk, d->r);
           if (nx > n) n = nx;
         }
+        if (op == DION_OP_PROJECT_R)
+          n = (n + 255) / 256 * 256 + thin_presplit_bytes(row_mode ? d->n : d->m, d->r, chunk);
         break;
       }
       case DION_OP_PROJECT_P_EF: {
