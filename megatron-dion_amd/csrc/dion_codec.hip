@@ -2358,21 +2358,20 @@ __global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) 
 }
 
 // ---- row projection, no gradient (pass B, transposed: R = M P):
-// rowproj_fast's geometry and loads (lane (t, g): 8 consecutive columns 8g..
-// of rows 16 rb + t = the A operand as loaded), KMAP 0.
+// the fused row kernel's geometry and loads (lane (t, g): columns 16 c + 4 g .. +3,
+// c = 0, 1, of rows 16 rb + t = the A operand's k-run), KMAP 1.
 template <int RB>
-__device__ __forceinline__ void rpx_compute(const RowStep<DION_DTYPE_NONE>& S, f32x4 (&acc)[kRB][RB],
+__device__ __forceinline__ void rpx_compute(const RowStepE<DION_DTYPE_NONE>& S, f32x4 (&acc)[kRBE][RB],
                                             const bf16x8* tq, int lane) {
+  Split3 A[kRBE];
 #pragma unroll
-  for (int rb = 0; rb < kRB; ++rb) {
-    Split3 A;
-    split3(S.x[rb][0], S.x[rb][1], 1.f, A);
+  for (int rb = 0; rb < kRBE; ++rb) split3(S.x[rb][0], S.x[rb][1], 1.f, A[rb]);
 #pragma unroll
-    for (int cb = 0; cb < RB; ++cb) {
-      Split3 B;
-      ef_sread(tq, cb, lane, B);
-      acc[rb][cb] = mfma6_16(A, B, acc[rb][cb]);
-    }
+  for (int cb = 0; cb < RB; ++cb) {
+    Split3 B;
+    ef_sread(tq, cb, lane, B);
+#pragma unroll
+    for (int rb = 0; rb < kRBE; ++rb) acc[rb][cb] = mfma6_16(A[rb], B, acc[rb][cb]);
   }
 }
 
@@ -2387,23 +2386,22 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
-  const int row_base = blockIdx.x * (64 * kRB) + wave * (16 * kRB);
+  const int row_base = blockIdx.x * (64 * kRBE) + wave * (16 * kRBE);
   const int j_begin = kc * a.kchunk;
   const int j_end = min(a.cols, j_begin + a.kchunk);
-  const float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 8 * g;
-  const float* __restrict__ Tp = a.thin[b];
+  const float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 4 * g;
 
-  f32x4 acc[kRB][RB];
+  f32x4 acc[kRBE][RB];
 #pragma unroll
-  for (int rb = 0; rb < kRB; ++rb)
+  for (int rb = 0; rb < kRBE; ++rb)
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  RowStep<DION_DTYPE_NONE> SA, SB;
+  RowStepE<DION_DTYPE_NONE> SA, SB;
   constexpr int NQ = RB * 3 * 64;
   const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
   SplitCopy<NQ> TA;
-  rp_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, j_begin);
+  rpe_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, j_begin);
   split_copy_load<NQ>(TA, qs + static_cast<long>(j_begin / 32) * NQ, tid);
   split_copy_store<NQ>(TA, tq[0], tid);
   __syncthreads();
@@ -2411,7 +2409,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
   for (int j0 = j_begin; j0 < j_end; j0 += 64) {
     const bool more = j0 + 32 < j_end;
     if (more) {
-      rp_load<DION_DTYPE_NONE>(SB, M, nullptr, a.ld_m, 0, j0 + 32);
+      rpe_load<DION_DTYPE_NONE>(SB, M, nullptr, a.ld_m, 0, j0 + 32);
       split_copy_load<NQ>(TA, qs + static_cast<long>(j0 / 32 + 1) * NQ, tid);
     }
     rpx_compute<RB>(SA, acc, tq[cur], lane);
@@ -2421,7 +2419,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
     cur ^= 1;
     const bool more2 = j0 + 64 < j_end;
     if (more2) {
-      rp_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, j0 + 64);
+      rpe_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, j0 + 64);
       split_copy_load<NQ>(TA, qs + static_cast<long>(j0 / 32 + 2) * NQ, tid);
     }
     rpx_compute<RB>(SB, acc, tq[cur], lane);
@@ -2433,7 +2431,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
 
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
 #pragma unroll
-  for (int rb = 0; rb < kRB; ++rb)
+  for (int rb = 0; rb < kRBE; ++rb)
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb)
 #pragma unroll
@@ -2749,8 +2747,8 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
   for (int b = 0; b < batch && fast; ++b)
     fast = aligned16(M[b]) && aligned16(thin[b]) && (gdt == DION_DTYPE_NONE || aligned16(G[b]));
   // no gradient (pass B): split-bf16 MFMA kernels (the column one steps 32 rows)
-  const bool x6 = fast && gdt == DION_DTYPE_NONE && (row_mode || rows % 32 == 0);
-  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, fast ? 64 * kRB : 128)
+  const bool x6 = fast && gdt == DION_DTYPE_NONE && (row_mode ? rows % (64 * kRBE) == 0 : rows % 32 == 0);
+  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, x6 ? 64 * kRBE : (fast ? 64 * kRB : 128))
                  : x6      ? colx6_geo(rows, cols, batch, r)
                            : colproj_geo(rows, cols, batch, false);
   const size_t slab = (slab_bytes(geo, batch, r) + 255) / 256 * 256;
@@ -2770,7 +2768,7 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     pa.rows = thin_rows;
     pa.r = r;
     pa.layout = 0;
-    pa.kmap = 0;
+    pa.kmap = row_mode ? 1 : 0;  // rowproj_x6 loads columns 16c + 4g (KMAP 1), colproj_x6 rows 8g + e
     const dim3 pgrid(static_cast<unsigned>(ceil_div(static_cast<long>(thin_rows) * r / 8, 256)), batch);
     hipLaunchKernelGGL(presplit_kernel, pgrid, dim3(256), 0, st, pa);
     int rc = check_launch("presplit(thin)");
@@ -2996,6 +2994,8 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
         if (row_mode) {
           const size_t nf = slab_bytes(rowproj_geo(d->m, d->n, chunk, 64 * kRB), chunk, d->r);
           if (nf > n) n = nf;
+          const size_t ne = slab_bytes(rowproj_geo(d->m, d->n, chunk, 64 * kRBE), chunk, d->r);
+          if (ne > n) n = ne;
         } else {
           const size_t nx = slab_bytes(colx6_geo(d->m, d->n, chunk, d->r), chunk, d->r);
           if (nx > n) n = nx;
