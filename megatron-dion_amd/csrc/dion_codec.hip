@@ -44,6 +44,46 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define MAXB 64  // matrices per launch (pointer arrays live in kernel arguments)
 
+// Cache policy of the big once-touched streams (G, M, W): non-temporal ("nt") loads
+// and stores.  Measured on MI355X (scripts/ubench/stream_modes.hip): an in-place
+// read-modify-write stream rises from 5.2 to 5.8 TB/s and a read-only stream from
+// 6.3 to 7.0 TB/s with nt on both sides.  Small factors (P, Q, R) keep the default
+// policy: every block re-reads them from L2.
+#ifndef DION_NT
+#define DION_NT 1
+#endif
+constexpr int kStreamAux = DION_NT ? 2 : 0;  // buffer-op cache-policy bits (nt)
+
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+  if constexpr (DION_NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+// Row-kernel accesses cover a 128-B line in two instructions (64-B segments per
+// row); nt on those re-fetches the line (measured 18 % slower on pass A), so they
+// keep the default policy.
+template <typename T>
+__device__ __forceinline__ T ld_part(const T* p) { return *p; }
+template <typename T>
+__device__ __forceinline__ void st_part(T* p, const T& v) { *p = v; }
+
+typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ld_stream(const uint4* p) {
+  const u32x4 v = ld_stream(reinterpret_cast<const u32x4*>(p));
+  return uint4{v[0], v[1], v[2], v[3]};
+}
+__device__ __forceinline__ uint2 ld_stream(const uint2* p) {
+  const u32x2_ v = ld_stream(reinterpret_cast<const u32x2_*>(p));
+  return uint2{v[0], v[1]};
+}
+
+template <typename T>
+__device__ __forceinline__ void st_stream(T* p, const T& v) {
+  if constexpr (DION_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 // ----------------------------------------------------------------------------- errors
 static thread_local char g_err[512];
 
@@ -431,14 +471,14 @@ __device__ __forceinline__ void rp_load(RowStep<GDT>& S, const float* __restrict
 #pragma unroll
   for (int rb = 0; rb < kRB; ++rb) {
     const float* p = M + rb * 16 * ld_m + j;
-    S.x[rb][0] = *reinterpret_cast<const f32x4*>(p);
-    S.x[rb][1] = *reinterpret_cast<const f32x4*>(p + 4);
+    S.x[rb][0] = ld_part(reinterpret_cast<const f32x4*>(p));
+    S.x[rb][1] = ld_part(reinterpret_cast<const f32x4*>(p + 4));
     if constexpr (GDT == DION_DTYPE_BF16) {
-      S.gb[rb] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(G) + rb * 16 * ld_g + j);
+      S.gb[rb] = ld_part(reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(G) + rb * 16 * ld_g + j));
     } else if constexpr (GDT == DION_DTYPE_F32) {
       const float* gp = static_cast<const float*>(G) + rb * 16 * ld_g + j;
-      S.gf[rb][0] = *reinterpret_cast<const f32x4*>(gp);
-      S.gf[rb][1] = *reinterpret_cast<const f32x4*>(gp + 4);
+      S.gf[rb][0] = ld_part(reinterpret_cast<const f32x4*>(gp));
+      S.gf[rb][1] = ld_part(reinterpret_cast<const f32x4*>(gp + 4));
     }
   }
 }
@@ -486,8 +526,8 @@ __device__ __forceinline__ void rp_compute(RowStep<GDT>& S, f32x4 (&acc)[kRB][RB
         S.x[rb][1] += S.gf[rb][1];
       }
       float* p = M + rb * 16 * ld_m + j;
-      *reinterpret_cast<f32x4*>(p) = S.x[rb][0];
-      *reinterpret_cast<f32x4*>(p + 4) = S.x[rb][1];
+      st_part(reinterpret_cast<f32x4*>(p), S.x[rb][0]);
+      st_part(reinterpret_cast<f32x4*>(p + 4), S.x[rb][1]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) nz |= (S.x[rb][0][e] != 0.f) | (S.x[rb][1][e] != 0.f);
     }
@@ -594,11 +634,11 @@ __device__ __forceinline__ void cp_load(ColStep<GDT>& S, const float* __restrict
                                         long ld_m, long ld_g, int i0) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    S.x[k] = *reinterpret_cast<const f32x4*>(M + static_cast<long>(i0 + 4 * k) * ld_m);
+    S.x[k] = ld_stream(reinterpret_cast<const f32x4*>(M + static_cast<long>(i0 + 4 * k) * ld_m));
     if constexpr (GDT == DION_DTYPE_BF16)
-      S.gb[k] = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(G) + static_cast<long>(i0 + 4 * k) * ld_g);
+      S.gb[k] = ld_stream(reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(G) + static_cast<long>(i0 + 4 * k) * ld_g));
     else if constexpr (GDT == DION_DTYPE_F32)
-      S.gf[k] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(G) + static_cast<long>(i0 + 4 * k) * ld_g);
+      S.gf[k] = ld_stream(reinterpret_cast<const f32x4*>(static_cast<const float*>(G) + static_cast<long>(i0 + 4 * k) * ld_g));
   }
 }
 
@@ -640,7 +680,7 @@ __device__ __forceinline__ void cp_compute(ColStep<GDT>& S, f32x4 (&acc)[4][RB],
       } else {
         S.x[k] += S.gf[k];
       }
-      *reinterpret_cast<f32x4*>(M + static_cast<long>(i0 + 4 * k) * ld_m) = S.x[k];
+      st_stream(reinterpret_cast<f32x4*>(M + static_cast<long>(i0 + 4 * k) * ld_m), S.x[k]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) nz |= (S.x[k][e] != 0.f);
     }
@@ -1520,8 +1560,8 @@ __global__ void __launch_bounds__(256, (RH >= 64 ? 1 : 2)) ef_fast_kernel(const 
     const int so = tile_soff(s0);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      if (DO_M) am[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rm, voff[q], so, 0));
-      aw[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, voff[q], so, 0));
+      if (DO_M) am[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rm, voff[q], so, kStreamAux));
+      aw[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, voff[q], so, kStreamAux));
     }
   };
   auto compute_store = [&](int s0, const float (&sp)[RH], f32x16& am, f32x16& aw) {
@@ -1533,7 +1573,7 @@ __global__ void __launch_bounds__(256, (RH >= 64 ? 1 : 2)) ef_fast_kernel(const 
                     : __builtin_amdgcn_mfma_f32_32x32x2f32(sp[s], fm[s], am, 0, 0, 0);
 #pragma unroll
       for (int q = 0; q < 16; ++q)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(am[q]), rm, voff[q], so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(am[q]), rm, voff[q], so, kStreamAux);
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) aw[q] *= a.decay;
@@ -1545,7 +1585,7 @@ __global__ void __launch_bounds__(256, (RH >= 64 ? 1 : 2)) ef_fast_kernel(const 
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q)
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(aw[q]), rw, voff[q], so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(aw[q]), rw, voff[q], so, kStreamAux);
   };
 
   // Order per tile: wait for this tile's loads (an empty asm "use" makes the
@@ -1714,7 +1754,7 @@ __global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const
     const int so = (row0 * ld + col0) * 4;
 #pragma unroll
     for (int q = 0; q < 16; ++q)
-      T.x[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff[q], so, 0));
+      T.x[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff[q], so, kStreamAux));
   };
   auto compute = [&](int s0, RTile<RU, PRE>& T) {
     f32x16 acc;
@@ -1738,7 +1778,7 @@ __global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float v = T.x[q] * a.decay + acc[q];
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[q], so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[q], so, kStreamAux);
     }
   };
   auto touch_s = [&](RTile<RU, PRE>& T) {
@@ -1998,11 +2038,11 @@ __device__ __forceinline__ void rpe_load(RowStepE<GDT>& S, const float* __restri
   for (int rb = 0; rb < kRBE; ++rb)
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      S.x[rb][c] = *reinterpret_cast<const f32x4*>(M + rb * 16 * ld_m + j + 16 * c);
+      S.x[rb][c] = ld_part(reinterpret_cast<const f32x4*>(M + rb * 16 * ld_m + j + 16 * c));
       if constexpr (GDT == DION_DTYPE_BF16)
-        S.gb[rb][c] = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(G) + rb * 16 * ld_g + j + 16 * c);
+        S.gb[rb][c] = ld_part(reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(G) + rb * 16 * ld_g + j + 16 * c));
       else if constexpr (GDT == DION_DTYPE_F32)
-        S.gf[rb][c] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(G) + rb * 16 * ld_g + j + 16 * c);
+        S.gf[rb][c] = ld_part(reinterpret_cast<const f32x4*>(static_cast<const float*>(G) + rb * 16 * ld_g + j + 16 * c));
     }
 }
 
@@ -2042,7 +2082,7 @@ __device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRBE]
         } else if constexpr (GDT == DION_DTYPE_F32) {
           S.x[rb][c] += S.gf[rb][c];
         }
-        *reinterpret_cast<f32x4*>(M + rb * 16 * ld_m + j + 16 * c) = S.x[rb][c];
+        st_part(reinterpret_cast<f32x4*>(M + rb * 16 * ld_m + j + 16 * c), S.x[rb][c]);
       }
   }
 #pragma unroll
@@ -2188,11 +2228,11 @@ __device__ __forceinline__ void cpe_load(ColStepE<GDT>& S, const float* __restri
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const long row = i0 + 16 * h + q;
-      S.x[h][q] = *reinterpret_cast<const f32x2*>(M + row * ld_m);
+      S.x[h][q] = ld_stream(reinterpret_cast<const f32x2*>(M + row * ld_m));
       if constexpr (GDT == DION_DTYPE_BF16)
-        S.gb[h][q] = *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(G) + row * ld_g);
+        S.gb[h][q] = ld_stream(reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(G) + row * ld_g));
       else if constexpr (GDT == DION_DTYPE_F32)
-        S.gf[h][q] = *reinterpret_cast<const f32x2*>(static_cast<const float*>(G) + row * ld_g);
+        S.gf[h][q] = ld_stream(reinterpret_cast<const f32x2*>(static_cast<const float*>(G) + row * ld_g));
     }
 }
 
@@ -2230,7 +2270,7 @@ __device__ __forceinline__ void cpe_compute(ColStepE<GDT>& S, f32x4 (&acc)[2][RB
         } else if constexpr (GDT == DION_DTYPE_F32) {
           S.x[h][q] += S.gf[h][q];
         }
-        *reinterpret_cast<f32x2*>(M + static_cast<long>(i0 + 16 * h + q) * ld_m) = S.x[h][q];
+        st_stream(reinterpret_cast<f32x2*>(M + static_cast<long>(i0 + 16 * h + q) * ld_m), S.x[h][q]);
       }
   }
 #pragma unroll
@@ -2453,7 +2493,7 @@ template <int CT>
 __device__ __forceinline__ void cpx_load(ColStepX6<CT>& S, const float* __restrict__ M, long ld_m, int i0) {
   typedef typename ColStepX6<CT>::vec vec;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) S.x[e] = *reinterpret_cast<const vec*>(M + static_cast<long>(i0 + e) * ld_m);
+  for (int e = 0; e < 8; ++e) S.x[e] = ld_stream(reinterpret_cast<const vec*>(M + static_cast<long>(i0 + e) * ld_m));
 }
 
 template <int RB, int CT>
