@@ -46,12 +46,12 @@ KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("project_p", True): ("colproj_fast_kernel<4, 2>", 1),
              ("project_p_ef", False): ("rowproj_ef_kernel<4, 2>", 1),
              ("project_p_ef", True): ("colproj_ef_kernel<4, 2>", 1),
-             ("ef_apply_w", False): ("rank_update_kernel<4, false, false>", 1),
-             ("ef_apply_w", True): ("rank_update_kernel<4, true, false>", 1),
+             ("ef_apply_w", False): ("rank_stream_kernel<4, false, 8, 2>", 1),
+             ("ef_apply_w", True): ("rank_stream_kernel<4, false, 8, 2>", 1),
              ("project_r", False): ("colproj_x6_kernel<4>", 1),
              ("project_r", True): ("rowproj_x6_kernel<4>", 1),
-             ("ef_apply", False): ("rank_update_kernel<4, false, false>", 2),
-             ("ef_apply", True): ("rank_update_kernel<4, true, false>", 2)}
+             ("ef_apply", False): ("rank_stream_kernel<4, false, 8, 2>", 2),
+             ("ef_apply", True): ("rank_stream_kernel<4, false, 8, 2>", 2)}
 
 
 class TimedCodec:

@@ -1647,6 +1647,7 @@ struct RankArgs {
   float* x[MAXB];            // M or W per matrix
   const float* fixed[MAXB];  // factor indexed by the fixed strip (R_b or Qn_b)
   const float* S;            // streamed factor base: P (batch, len, r)
+  const float* sptr[MAXB];   // rank_stream_kernel: per-matrix streamed factor (overrides S when set)
   const u32x4* Ssplit;       // P pre-split (presplit_kernel layout 2), or null
   long ss_stride;            // 16-byte units per matrix of Ssplit
   int s_len;                 // streamed extent per block (multiple of 64)
@@ -1810,6 +1811,143 @@ __global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const
     __builtin_amdgcn_sched_barrier(0);
     if (more2) touch_s(A);
     __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// ============================================================================
+// Rank-r update, block-shared streamed factor ("rank_stream"): the production
+// weight / error-feedback path.  Same arithmetic and order as rank_update_kernel
+// (bf16x6 on v_mfma_f32_32x32x16_bf16, accumulator from zero, X*decay + acc), but
+//  - the NW waves of a block own NW adjacent 32-wide strips of the fixed side and
+//    walk the same 32-long steps of the streamed side, so a step's streamed
+//    factor rows (32 x r fp32) are loaded and split ONCE per block into LDS
+//    (double-buffered, one barrier per step) instead of once per wave: the L2
+//    factor traffic drops NW-fold and so does the split's VALU work;
+//  - each wave keeps D X tiles in flight (register ring), with nt loads/stores.
+// LDS layout of a step: [u][part][lane] bf16x8 (the 32x32x16 operand run of lane
+// (t, h): factor row t, columns 16 u + 8 h .. +7), conflict-free ds_read_b128.
+// ============================================================================
+template <int RU, bool ROWFIX, int NW, int D>
+__global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_stream_kernel(const RankArgs a) {
+  constexpr int R = 16 * RU;
+  constexpr int NT = 64 * NW;
+  constexpr int kGroups = RU * 64;                   // 8-value groups of one 32-row step
+  constexpr int kPer = (kGroups + NT - 1) / NT;      // groups per thread
+  __shared__ bf16x8 sp[2][RU * 3 * 64];
+  const int b = blockIdx.z;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(tid >> 6));
+  const int lane = tid & 63;
+  const int t = lane & 31;
+  const int h = lane >> 5;
+  const int rows = a.rows, cols = a.cols;
+  if (a.skip_zero && __builtin_amdgcn_readfirstlane(a.nonzero[b]) == 0u) return;
+  const int flen = ROWFIX ? rows : cols;
+  const int fbase = blockIdx.x * (32 * NW) + wave * 32;
+  const bool active = fbase < flen;  // a wave past the edge still joins the block's staging and barriers
+  const int s_begin = blockIdx.y * a.s_len;
+  const int s_end = min(ROWFIX ? cols : rows, s_begin + a.s_len);
+  const int ld = static_cast<int>(a.ld);
+  const float* Sb = a.sptr[b] != nullptr ? a.sptr[b] : a.S + static_cast<long>(b) * a.s_stride;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      a.x[b], static_cast<short>(0), static_cast<int>(min(static_cast<long>(rows) * ld * 4, 0x7FFFFFF0L)), 0x00020000);
+  int voff[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) voff[q] = (((q & 3) + 8 * (q >> 2) + 4 * h) * ld + t) * 4;
+
+  Split3 F[RU];
+  if (active) {
+    const float* fp = a.fixed[b] + static_cast<long>(fbase + t) * R + 8 * h;
+#pragma unroll
+    for (int u = 0; u < RU; ++u)
+      split3(*reinterpret_cast<const f32x4*>(fp + 16 * u), *reinterpret_cast<const f32x4*>(fp + 16 * u + 4),
+             a.scale, F[u]);
+  }
+
+  // staging of one step's streamed rows: thread item g = tid + NT * it -> (u, lane') =
+  // (g / 64, g % 64): row s0 + lane' % 32, columns 16 u + 8 (lane' / 32) .. +7
+  f32x4 pv[kPer][2];
+  auto p_load = [&](int s0) {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int g = tid + NT * it;
+      if (g < kGroups) {
+        const int u = g >> 6, l = g & 63;
+        const float* src = Sb + static_cast<long>(s0 + (l & 31)) * R + 16 * u + 8 * (l >> 5);
+        pv[it][0] = *reinterpret_cast<const f32x4*>(src);
+        pv[it][1] = *reinterpret_cast<const f32x4*>(src + 4);
+      }
+    }
+  };
+  auto p_store = [&](bf16x8* dst) {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int g = tid + NT * it;
+      if (g < kGroups) {
+        const int u = g >> 6, l = g & 63;
+        Split3 o;
+        split3(pv[it][0], pv[it][1], 1.f, o);
+        dst[(u * 3 + 0) * 64 + l] = o.hi;
+        dst[(u * 3 + 1) * 64 + l] = o.mid;
+        dst[(u * 3 + 2) * 64 + l] = o.lo;
+      }
+    }
+  };
+
+  f32x16 X[D];
+  auto x_load = [&](int s0, f32x16& T) {
+    const int row0 = ROWFIX ? fbase : s0;
+    const int col0 = ROWFIX ? s0 : fbase;
+    const int so = (row0 * ld + col0) * 4;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) T[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff[q], so, kStreamAux));
+  };
+  auto compute_store = [&](int s0, const f32x16& T, const bf16x8* src) {
+    f32x16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      Split3 Sp;
+      Sp.hi = src[(u * 3 + 0) * 64 + lane];
+      Sp.mid = src[(u * 3 + 1) * 64 + lane];
+      Sp.lo = src[(u * 3 + 2) * 64 + lane];
+      acc = ROWFIX ? mfma6(F[u], Sp, acc) : mfma6(Sp, F[u], acc);
+    }
+    const int row0 = ROWFIX ? fbase : s0;
+    const int col0 = ROWFIX ? s0 : fbase;
+    const int so = (row0 * ld + col0) * 4;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float v = T[q] * a.decay + acc[q];
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[q], so, kStreamAux);
+    }
+  };
+
+  // prologue: step 0's factor rows into LDS, X tiles of steps 0 .. D-2 in flight
+  p_load(s_begin);
+  if (active) {
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k)
+      if (s_begin + 32 * k < s_end) x_load(s_begin + 32 * k, X[k]);
+  }
+  p_store(sp[0]);
+  __syncthreads();
+  int cur = 0;
+  for (int s0 = s_begin; s0 < s_end; s0 += 32 * D) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int s = s0 + 32 * k;
+      if (s >= s_end) break;
+      const bool more = s + 32 < s_end;
+      if (more) p_load(s + 32);
+      if (active && s + 32 * (D - 1) < s_end) x_load(s + 32 * (D - 1), X[(k + D - 1) % D]);
+      if (active) compute_store(s, X[k], sp[cur]);
+      if (!more) break;
+      p_store(sp[cur ^ 1]);
+      __syncthreads();
+      cur ^= 1;
+    }
   }
 }
 
@@ -2674,6 +2812,17 @@ int rank_stream_len() {
   return v;
 }
 
+// rank-update kernel choice: 0 = per-wave factor (rank_update_kernel), 1..4 =
+// rank_stream_kernel with (NW, D) = (4, 2), (4, 3), (8, 2), (8, 3); DION_RANK_VARIANT overrides
+int rank_stream_variant() {
+  static const int v = [] {
+    const char* e = getenv("DION_RANK_VARIANT");
+    const int x = e ? atoi(e) : 3;
+    return (x >= 0 && x <= 4) ? x : 3;
+  }();
+  return v;
+}
+
 // pre-split thin operand of the x6 projections (rows = the contraction index)
 size_t thin_presplit_bytes(int rows, int r, int batch) { return static_cast<size_t>(rows) * r * 6 * batch; }
 
@@ -3420,6 +3569,39 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
         ra.skip_zero = pass == 0 ? 1 : 0;
         auto launch = [&](auto RUc) {
           constexpr int RUv = decltype(RUc)::value;
+          const int variant = pre ? 0 : rank_stream_variant();
+          if (variant != 0) {
+            // rank_stream_kernel: NW-wave blocks share the split streamed factor through LDS
+            ra.s_len = s_len;
+            // Both orientations run with the 32-wide strips across X's columns and the
+            // steps down its rows (a block's accesses are 32 x NW-wide rows of 1 KB runs).
+            // Transposed (X += s Fq P^T, Fq = R or Qn indexed by X's rows): the fixed
+            // strip factor is P (indexed by X's columns), the staged one Fq; the scale
+            // moves with the fixed factor.
+            if (d->transposed) {
+              for (int b = 0; b < nb; ++b) {
+                ra.sptr[b] = ra.fixed[b];
+                ra.fixed[b] = a.P + static_cast<long>(b) * mp * r;
+              }
+            }
+            auto go = [&](auto NWc, auto Dc) {
+              constexpr int NWv = decltype(NWc)::value, Dv = decltype(Dc)::value;
+              const dim3 g2(static_cast<unsigned>(ceil_div(d->n, 32 * NWv)),
+                            static_cast<unsigned>(ceil_div(d->m, s_len)), grid.z);
+              hipLaunchKernelGGL((rank_stream_kernel<RUv, false, NWv, Dv>), g2, dim3(64 * NWv), 0, st, ra);
+            };
+            using I4 = std::integral_constant<int, 4>;
+            using I8 = std::integral_constant<int, 8>;
+            using I2 = std::integral_constant<int, 2>;
+            using I3 = std::integral_constant<int, 3>;
+            switch (variant) {
+              case 1: go(I4{}, I2{}); break;
+              case 2: go(I4{}, I3{}); break;
+              case 3: go(I8{}, I2{}); break;
+              default: go(I8{}, I3{}); break;
+            }
+            return;
+          }
           if (pre && d->transposed)
             hipLaunchKernelGGL((rank_update_kernel<RUv, true, true>), grid, dim3(256), 0, st, ra);
           else if (pre)
