@@ -44,11 +44,11 @@ def llama_shapes(layers):
 # ef_apply is two launches of the same instance (M, then W), each streaming 8 B per element
 KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("project_p", True): ("colproj_fast_kernel<4, 2>", 1),
-             ("project_p_ef", False): ("rowproj_ef_kernel<4, 2>", 1),
+             ("project_p_ef", False): ("rowproj_ef_kernel<4, 2, 2, true>", 1),
              ("project_p_ef", True): ("colproj_ef_kernel<4, 2>", 1),
              ("ef_apply_w", False): ("rank_stream_kernel<4, false, 8, 2>", 1),
              ("ef_apply_w", True): ("rank_stream_kernel<4, false, 8, 2>", 1),
-             ("project_r", False): ("colproj_x6_kernel<4>", 1),
+             ("project_r", False): ("colproj_x6_kernel<4, 4>", 1),
              ("project_r", True): ("rowproj_x6_kernel<4>", 1),
              ("ef_apply", False): ("rank_stream_kernel<4, false, 8, 2>", 2),
              ("ef_apply", True): ("rank_stream_kernel<4, false, 8, 2>", 2)}

@@ -52,6 +52,13 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DION_NT
 #define DION_NT 1
 #endif
+// waves per block of the pass-B column kernel and its min-blocks-per-CU hint (tuning knobs)
+#ifndef DION_COLX6_NW
+#define DION_COLX6_NW 4
+#endif
+#ifndef DION_COLX6_MINB
+#define DION_COLX6_MINB 1
+#endif
 constexpr int kStreamAux = DION_NT ? 2 : 0;  // buffer-op cache-policy bits (nt)
 
 template <typename T>
@@ -544,21 +551,78 @@ __device__ __forceinline__ void rp_compute(RowStep<GDT>& S, f32x4 (&acc)[kRB][RB
   }
 }
 
+// XCD-aware block order of the row kernels (rowproj_fast / rowproj_ef / rowproj_x6).
+// Workgroups land on the 8 XCDs round-robin by linear id, and each XCD has its own
+// 4 MiB L2.  In launch order, the ~64 blocks resident on one XCD would belong to 3-4
+// matrices, whose pre-split thin operands (n x r x 6 B: 1.5 MiB each for Q at
+// n = 4096) then fight the M/G stream for L2 and are refetched from memory (PMC:
+// 1.7x the algorithmic bytes).  Remapped, XCD x walks the contiguous range
+// [x T/8, (x+1) T/8) of the logical blocks, so its resident blocks are neighbouring
+// row blocks of one matrix that read the same thin rows at the same time.
+// waves per block of the fused pass-A row kernel (rowproj_ef_kernel), tuning knob
+#ifndef DION_PA_NW
+#define DION_PA_NW 4
+#endif
+constexpr int kPaNW = DION_PA_NW;
+
+#ifndef DION_XCD_REMAP
+#define DION_XCD_REMAP 1
+#endif
+// column-walk rotation of the row kernels: 0 none, 1 per block, 2 per XCD (tuning knob)
+#ifndef DION_ROW_ROT
+#define DION_ROW_ROT 0
+#endif
+struct BlockXYZ {
+  int x, y, z, xcd;
+};
+
+__device__ __forceinline__ BlockXYZ xcd_block() {
+  const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+  const int id = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  if (!DION_XCD_REMAP) return {static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y),
+                               static_cast<int>(blockIdx.z), id & 7};
+  const int T = gx * gy * gz;
+  const int xcd = id & 7, slot = id >> 3;
+  const int L = xcd * (T >> 3) + min(xcd, T & 7) + slot;
+  return {L % gx, (L / gx) % gy, L / (gx * gy), xcd};
+}
+
+// the same remap for the column kernels (colproj_x6 / colproj_ef), whose thin rows are
+// shared by the blocks of one (K chunk, matrix); DION_XCD_REMAP_COL=0 turns it off
+#ifndef DION_XCD_REMAP_COL
+#define DION_XCD_REMAP_COL 1
+#endif
+__device__ __forceinline__ BlockXYZ xcd_block_col() {
+  if (DION_XCD_REMAP_COL) return xcd_block();
+  return {static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y), static_cast<int>(blockIdx.z), 0};
+}
+
+// K-walk start offset (multiple of 32 columns) of a row-kernel block
+__device__ __forceinline__ int walk_rotation(const BlockXYZ& B, int j_len) {
+  if (DION_ROW_ROT == 1) return static_cast<int>((static_cast<long>(B.x + 7 * B.z) * 32) % j_len) & ~31;
+  if (DION_ROW_ROT == 2) return static_cast<int>((static_cast<long>(B.xcd) * 160) % j_len) & ~31;
+  return 0;
+}
+
 template <int RB, int GDT>
 __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_fast_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int LDT = R + 2;
   __shared__ __attribute__((aligned(16))) float tl[2][32 * LDT];
-  const int b = blockIdx.z;
-  const int kc = blockIdx.y;
+  const BlockXYZ blk = xcd_block();
+  const int b = blk.z;
+  const int kc = blk.y;
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
-  const int row_base = blockIdx.x * (64 * kRB) + wave * (16 * kRB);
+  const int row_base = blk.x * (64 * kRB) + wave * (16 * kRB);
   const int j_begin = kc * a.kchunk;
   const int j_end = min(a.cols, j_begin + a.kchunk);
+  const int j_len = j_end - j_begin;
+  const int j_rot = walk_rotation(blk, j_len);
+  auto cj = [&](int j) { const int x = j - j_begin + j_rot; return j_begin + (x >= j_len ? x - j_len : x); };
   float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 8 * g;
   const void* G = nullptr;
   if constexpr (GDT == DION_DTYPE_BF16)
@@ -576,28 +640,28 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_fast_kernel(cons
 
   RowStep<GDT> SA, SB;
   TStage<RB> TA;
-  rp_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j_begin);
-  rp_tload<RB>(TA, Tp, j_begin, tid);
+  rp_load<GDT>(SA, M, G, a.ld_m, a.ld_g, cj(j_begin));
+  rp_tload<RB>(TA, Tp, cj(j_begin), tid);
   rp_tstore<RB>(TA, tl[0], tid);
   __syncthreads();
   int cur = 0;
   for (int j0 = j_begin; j0 < j_end; j0 += 64) {
     const bool more = j0 + 32 < j_end;
     if (more) {
-      rp_load<GDT>(SB, M, G, a.ld_m, a.ld_g, j0 + 32);
-      rp_tload<RB>(TA, Tp, j0 + 32, tid);
+      rp_load<GDT>(SB, M, G, a.ld_m, a.ld_g, cj(j0 + 32));
+      rp_tload<RB>(TA, Tp, cj(j0 + 32), tid);
     }
-    rp_compute<RB, GDT>(SA, acc, tl[cur], M, a.ld_m, j0, g, t, nz);
+    rp_compute<RB, GDT>(SA, acc, tl[cur], M, a.ld_m, cj(j0), g, t, nz);
     if (!more) break;
     rp_tstore<RB>(TA, tl[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
     const bool more2 = j0 + 64 < j_end;
     if (more2) {
-      rp_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j0 + 64);
-      rp_tload<RB>(TA, Tp, j0 + 64, tid);
+      rp_load<GDT>(SA, M, G, a.ld_m, a.ld_g, cj(j0 + 64));
+      rp_tload<RB>(TA, Tp, cj(j0 + 64), tid);
     }
-    rp_compute<RB, GDT>(SB, acc, tl[cur], M, a.ld_m, j0 + 32, g, t, nz);
+    rp_compute<RB, GDT>(SB, acc, tl[cur], M, a.ld_m, cj(j0 + 32), g, t, nz);
     if (!more2) break;
     rp_tstore<RB>(TA, tl[cur ^ 1], tid);
     __syncthreads();
@@ -2054,6 +2118,28 @@ __device__ __forceinline__ void split_copy_store(const SplitCopy<NU>& C, bf16x8*
     if (NU % 256 == 0 || tid + 256 * it < NU) d[tid + 256 * it] = C.v[it];
 }
 
+// the same staging copy for blocks of NT threads
+template <int NU, int NT>
+struct SplitCopyN {
+  static constexpr int kPer = (NU + NT - 1) / NT;
+  u32x4 v[kPer];
+};
+
+template <int NU, int NT>
+__device__ __forceinline__ void split_copy_load_n(SplitCopyN<NU, NT>& C, const u32x4* __restrict__ src, int tid) {
+#pragma unroll
+  for (int it = 0; it < SplitCopyN<NU, NT>::kPer; ++it)
+    if (NU % NT == 0 || tid + NT * it < NU) C.v[it] = src[tid + NT * it];
+}
+
+template <int NU, int NT>
+__device__ __forceinline__ void split_copy_store_n(const SplitCopyN<NU, NT>& C, bf16x8* dst, int tid) {
+  u32x4* d = reinterpret_cast<u32x4*>(dst);
+#pragma unroll
+  for (int it = 0; it < SplitCopyN<NU, NT>::kPer; ++it)
+    if (NU % NT == 0 || tid + NT * it < NU) d[tid + NT * it] = C.v[it];
+}
+
 __device__ __forceinline__ f32x4 mfma6_16(const Split3& A, const Split3& B, f32x4 acc) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A.mid, B.mid, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A.lo, B.hi, acc, 0, 0, 0);
@@ -2176,7 +2262,7 @@ __device__ __forceinline__ void rpe_load(RowStepE<GDT>& S, const float* __restri
   for (int rb = 0; rb < kRBE; ++rb)
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      S.x[rb][c] = ld_part(reinterpret_cast<const f32x4*>(M + rb * 16 * ld_m + j + 16 * c));
+      if (M != nullptr) S.x[rb][c] = ld_part(reinterpret_cast<const f32x4*>(M + rb * 16 * ld_m + j + 16 * c));
       if constexpr (GDT == DION_DTYPE_BF16)
         S.gb[rb][c] = ld_part(reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(G) + rb * 16 * ld_g + j + 16 * c));
       else if constexpr (GDT == DION_DTYPE_F32)
@@ -2242,30 +2328,38 @@ __device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRBE]
   }
 }
 
-template <int RB, int GDT>
-__global__ void __launch_bounds__(256, 2) rowproj_ef_kernel(const EfProjArgs e) {
+template <int RB, int GDT, int PD, bool TJ>
+__global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_ef_kernel(const EfProjArgs e) {
   constexpr int R = 16 * RB;
   constexpr int KK = RB / 2;
   __shared__ bf16x8 tq[2][RB * 3 * 64];
   __shared__ bf16x8 rs[2][2 * KK * 3 * 64];
+  // TJ: M arrives in whole 128-B lines (lane l: row 8 i + l / 8, 16-B chunk l % 8 of the
+  // step's 32 columns) and is turned into the MFMA layout through a wave-private LDS
+  // tile (chunk k of row r stored at k ^ ((r >> 1) & 7): conflict-free both ways)
+  __shared__ f32x4 xt[TJ ? kPaNW : 1][TJ ? 32 * 8 : 1];
   const ProjArgs& a = e.p;
-  const int b = blockIdx.z;
-  const int kc = blockIdx.y;
+  const BlockXYZ blk = xcd_block();
+  const int b = blk.z;
+  const int kc = blk.y;
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
-  const int row_base = blockIdx.x * (64 * kRBE) + wave * (16 * kRBE);
+  const int row_base = blk.x * (16 * kRBE * kPaNW) + wave * (16 * kRBE);
   const int j_begin = kc * a.kchunk;
   const int j_end = min(a.cols, j_begin + a.kchunk);
+  const int j_len = j_end - j_begin;
+  const int j_rot = walk_rotation(blk, j_len);
+  auto cj = [&](int j) { const int x = j - j_begin + j_rot; return j_begin + (x >= j_len ? x - j_len : x); };
   float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 4 * g;
   const void* G = nullptr;
   if constexpr (GDT == DION_DTYPE_BF16)
     G = static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 4 * g;
   else if constexpr (GDT == DION_DTYPE_F32)
     G = static_cast<const float*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 4 * g;
-  const float* __restrict__ Tp = a.thin[b];
+  const float* __restrict__ Mw = a.m[b] + static_cast<long>(row_base + (lane >> 3)) * a.ld_m + 4 * (lane & 7);
   const float* __restrict__ Rp = e.efr[b];
   const bool has_ef = Rp != nullptr;
 
@@ -2297,43 +2391,65 @@ __global__ void __launch_bounds__(256, 2) rowproj_ef_kernel(const EfProjArgs e) 
   constexpr int NQ = RB * 3 * 64, NR = 2 * KK * 3 * 64;
   const u32x4* qs = e.qsplit + b * e.split_stride;
   const u32x4* rsp = e.rsplit + b * e.split_stride;
-  RowStepE<GDT> SA, SB;
-  SplitCopy<NQ> TA;
-  SplitCopy<NR> EA;
-  rpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j_begin);
-  split_copy_load<NQ>(TA, qs + static_cast<long>(j_begin / 32) * NQ, tid);
-  split_copy_store<NQ>(TA, tq[0], tid);
+  // X (M, G) arrives PD - 1 steps ahead in a register ring; the split operands one step ahead
+  RowStepE<GDT> S[PD];
+  auto xload = [&](RowStepE<GDT>& T, int j) {
+    if constexpr (TJ) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        T.x[q >> 1][q & 1] = *reinterpret_cast<const f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j);
+      rpe_load<GDT>(T, nullptr, G, 0, a.ld_g, j);
+    } else {
+      rpe_load<GDT>(T, M, G, a.ld_m, a.ld_g, j);
+    }
+  };
+  auto xpose = [&](RowStepE<GDT>& T) {
+    f32x4* xw = xt[TJ ? wave : 0];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 8 * q + (lane >> 3), k = lane & 7;
+      xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[q >> 1][q & 1];
+    }
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int r = 16 * rb + t, k = 4 * c + g;
+        T.x[rb][c] = xw[r * 8 + (k ^ ((r >> 1) & 7))];
+      }
+  };
+  SplitCopyN<NQ, 64 * kPaNW> TA;
+  SplitCopyN<NR, 64 * kPaNW> EA;
+#pragma unroll
+  for (int k = 0; k < PD - 1; ++k)
+    if (j_begin + 32 * k < j_end) xload(S[k], cj(j_begin + 32 * k));
+  split_copy_load_n(TA, qs + static_cast<long>(cj(j_begin) / 32) * NQ, tid);
+  split_copy_store_n(TA, tq[0], tid);
   if (has_ef) {
-    split_copy_load<NR>(EA, rsp + static_cast<long>(j_begin / 32) * NR, tid);
-    split_copy_store<NR>(EA, rs[0], tid);
+    split_copy_load_n(EA, rsp + static_cast<long>(cj(j_begin) / 32) * NR, tid);
+    split_copy_store_n(EA, rs[0], tid);
   }
   __syncthreads();
   int cur = 0;
-  for (int j0 = j_begin; j0 < j_end; j0 += 64) {
-    const bool more = j0 + 32 < j_end;
-    if (more) {
-      rpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, j0 + 32);
-      split_copy_load<NQ>(TA, qs + static_cast<long>(j0 / 32 + 1) * NQ, tid);
-      if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(j0 / 32 + 1) * NR, tid);
+  for (int j0 = j_begin; j0 < j_end; j0 += 32 * PD) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      const int j = j0 + 32 * k;
+      if (j >= j_end) break;
+      const bool more = j + 32 < j_end;
+      if (j + 32 * (PD - 1) < j_end) xload(S[(k + PD - 1) % PD], cj(j + 32 * (PD - 1)));
+      if (more) {
+        split_copy_load_n(TA, qs + static_cast<long>(cj(j + 32) / 32) * NQ, tid);
+        if (has_ef) split_copy_load_n(EA, rsp + static_cast<long>(cj(j + 32) / 32) * NR, tid);
+      }
+      if constexpr (TJ) xpose(S[k]);
+      rpe_compute<RB, GDT>(S[k], acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, cj(j), lane, nzb);
+      if (!more) break;
+      split_copy_store_n(TA, tq[cur ^ 1], tid);
+      if (has_ef) split_copy_store_n(EA, rs[cur ^ 1], tid);
+      __syncthreads();
+      cur ^= 1;
     }
-    rpe_compute<RB, GDT>(SA, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, j0, lane, nzb);
-    if (!more) break;
-    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
-    if (has_ef) split_copy_store<NR>(EA, rs[cur ^ 1], tid);
-    __syncthreads();
-    cur ^= 1;
-    const bool more2 = j0 + 64 < j_end;
-    if (more2) {
-      rpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, j0 + 64);
-      split_copy_load<NQ>(TA, qs + static_cast<long>(j0 / 32 + 2) * NQ, tid);
-      if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(j0 / 32 + 2) * NR, tid);
-    }
-    rpe_compute<RB, GDT>(SB, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, j0 + 32, lane, nzb);
-    if (!more2) break;
-    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
-    if (has_ef) split_copy_store<NR>(EA, rs[cur ^ 1], tid);
-    __syncthreads();
-    cur ^= 1;
   }
 
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
@@ -2436,14 +2552,15 @@ __global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) 
   __shared__ bf16x8 tq[2][RB * 3 * 64];
   __shared__ bf16x8 rs[2][2 * KK * 3 * 64];
   const ProjArgs& a = e.p;
-  const int b = blockIdx.z;
-  const int kc = blockIdx.y;
+  const BlockXYZ blk = xcd_block_col();
+  const int b = blk.z;
+  const int kc = blk.y;
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
-  const int col_base = blockIdx.x * 128 + wave * 32;
+  const int col_base = blk.x * 128 + wave * 32;
   const int i_begin = kc * a.kchunk;
   const int i_end = min(a.rows, i_begin + a.kchunk);
   float* __restrict__ M = a.m[b] + static_cast<long>(4 * g) * a.ld_m + col_base + 2 * t;
@@ -2557,16 +2674,20 @@ template <int RB>
 __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   __shared__ bf16x8 tq[2][RB * 3 * 64];
-  const int b = blockIdx.z;
-  const int kc = blockIdx.y;
+  const BlockXYZ blk = xcd_block();
+  const int b = blk.z;
+  const int kc = blk.y;
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
-  const int row_base = blockIdx.x * (64 * kRBE) + wave * (16 * kRBE);
+  const int row_base = blk.x * (64 * kRBE) + wave * (16 * kRBE);
   const int j_begin = kc * a.kchunk;
   const int j_end = min(a.cols, j_begin + a.kchunk);
+  const int j_len = j_end - j_begin;
+  const int j_rot = walk_rotation(blk, j_len);
+  auto cj = [&](int j) { const int x = j - j_begin + j_rot; return j_begin + (x >= j_len ? x - j_len : x); };
   const float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 4 * g;
 
   f32x4 acc[kRBE][RB];
@@ -2579,16 +2700,16 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
   constexpr int NQ = RB * 3 * 64;
   const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
   SplitCopy<NQ> TA;
-  rpe_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, j_begin);
-  split_copy_load<NQ>(TA, qs + static_cast<long>(j_begin / 32) * NQ, tid);
+  rpe_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, cj(j_begin));
+  split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j_begin) / 32) * NQ, tid);
   split_copy_store<NQ>(TA, tq[0], tid);
   __syncthreads();
   int cur = 0;
   for (int j0 = j_begin; j0 < j_end; j0 += 64) {
     const bool more = j0 + 32 < j_end;
     if (more) {
-      rpe_load<DION_DTYPE_NONE>(SB, M, nullptr, a.ld_m, 0, j0 + 32);
-      split_copy_load<NQ>(TA, qs + static_cast<long>(j0 / 32 + 1) * NQ, tid);
+      rpe_load<DION_DTYPE_NONE>(SB, M, nullptr, a.ld_m, 0, cj(j0 + 32));
+      split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j0 + 32) / 32) * NQ, tid);
     }
     rpx_compute<RB>(SA, acc, tq[cur], lane);
     if (!more) break;
@@ -2597,8 +2718,8 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
     cur ^= 1;
     const bool more2 = j0 + 64 < j_end;
     if (more2) {
-      rpe_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, j0 + 64);
-      split_copy_load<NQ>(TA, qs + static_cast<long>(j0 / 32 + 2) * NQ, tid);
+      rpe_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, cj(j0 + 64));
+      split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j0 + 64) / 32) * NQ, tid);
     }
     rpx_compute<RB>(SB, acc, tq[cur], lane);
     if (!more2) break;
@@ -2655,19 +2776,20 @@ __device__ __forceinline__ void cpx_compute(const ColStepX6<CT>& S, f32x4 (&acc)
 template <int RB>
 constexpr int colx6_ct() { return RB >= 4 ? 2 : 4; }
 
-template <int RB>
-__global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_x6_kernel(const ProjArgs a) {
+template <int RB, int NW>
+__global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : (NW >= 8 ? DION_COLX6_MINB : 2)) colproj_x6_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int CT = colx6_ct<RB>();
   __shared__ bf16x8 tq[2][RB * 3 * 64];
-  const int b = blockIdx.z;
-  const int kc = blockIdx.y;
+  const BlockXYZ blk = xcd_block_col();
+  const int b = blk.z;
+  const int kc = blk.y;
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
-  const int col_base = blockIdx.x * (64 * CT) + wave * (16 * CT);
+  const int col_base = blk.x * (16 * CT * NW) + wave * (16 * CT);
   const int i_begin = kc * a.kchunk;
   const int i_end = min(a.rows, i_begin + a.kchunk);
   const float* __restrict__ M = a.m[b] + static_cast<long>(8 * g) * a.ld_m + col_base + CT * t;
@@ -2682,31 +2804,31 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_x6_kernel(const 
   ColStepX6<CT> SA, SB;
   constexpr int NQ = RB * 3 * 64;
   const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
-  SplitCopy<NQ> TA;
+  SplitCopyN<NQ, 64 * NW> TA;
   cpx_load<CT>(SA, M, a.ld_m, i_begin);
-  split_copy_load<NQ>(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
-  split_copy_store<NQ>(TA, tq[0], tid);
+  split_copy_load_n(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
+  split_copy_store_n(TA, tq[0], tid);
   __syncthreads();
   int cur = 0;
   for (int i0 = i_begin; i0 < i_end; i0 += 64) {
     const bool more = i0 + 32 < i_end;
     if (more) {
       cpx_load<CT>(SB, M, a.ld_m, i0 + 32);
-      split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 1) * NQ, tid);
+      split_copy_load_n(TA, qs + static_cast<long>(i0 / 32 + 1) * NQ, tid);
     }
     cpx_compute<RB, CT>(SA, acc, tq[cur], lane);
     if (!more) break;
-    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
+    split_copy_store_n(TA, tq[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
     const bool more2 = i0 + 64 < i_end;
     if (more2) {
       cpx_load<CT>(SA, M, a.ld_m, i0 + 64);
-      split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 2) * NQ, tid);
+      split_copy_load_n(TA, qs + static_cast<long>(i0 / 32 + 2) * NQ, tid);
     }
     cpx_compute<RB, CT>(SB, acc, tq[cur], lane);
     if (!more2) break;
-    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
+    split_copy_store_n(TA, tq[cur ^ 1], tid);
     __syncthreads();
     cur ^= 1;
   }
@@ -2785,10 +2907,11 @@ Geo colproj_geo(int rows, int cols, int batch, bool panel, int kalign = 16) {
   return g;
 }
 
-// colproj_x6_kernel: 64 * CT columns per block (CT = 2 for r >= 64, else 4), 32-row K-steps
+// colproj_x6_kernel: NW waves of 16 CT columns per block (CT = 2 for r >= 64, else 4), 32-row K-steps
+constexpr int kColX6NW = DION_COLX6_NW;
 Geo colx6_geo(int rows, int cols, int batch, int r) {
   Geo g;
-  g.gx = static_cast<int>(ceil_div(cols, r >= 64 ? 128 : 256));
+  g.gx = static_cast<int>(ceil_div(cols, (r >= 64 ? 32 : 64) * kColX6NW));
   long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
   long maxc = ceil_div(rows, 256);
   long nc = want < maxc ? want : maxc;
@@ -2836,11 +2959,21 @@ size_t presplit_bytes(int nq, int r, int batch) { return 2 * 16 * presplit_strid
 // deferred-EF pass A (rowproj_ef_kernel / colproj_ef_kernel)
 bool proj_ef_ok(int m, int n, int r, bool transposed) {
   if (r != 32 && r != 64) return false;
-  return transposed ? (n % 128 == 0 && m % 32 == 0) : (m % (64 * kRBE) == 0 && n % 32 == 0);
+  return transposed ? (n % 128 == 0 && m % 32 == 0) : (m % (16 * kRBE * kPaNW) == 0 && n % 32 == 0);
+}
+
+// rowproj_ef_kernel loads M in whole lines (TJ, default) or in the MFMA layout directly
+// (DION_PA_LINES=0); measured 1 % apart on the Llama fc1 batch
+bool pa_lines() {
+  static const bool v = [] {
+    const char* e = getenv("DION_PA_LINES");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return v;
 }
 
 Geo proj_ef_geo(int m, int n, int batch, bool transposed) {
-  if (!transposed) return rowproj_geo(m, n, batch, 64 * kRBE);
+  if (!transposed) return rowproj_geo(m, n, batch, 16 * kRBE * kPaNW);
   Geo g;
   g.gx = static_cast<int>(ceil_div(n, 128));
   long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
@@ -2936,7 +3069,9 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
   for (int b = 0; b < batch && fast; ++b)
     fast = aligned16(M[b]) && aligned16(thin[b]) && (gdt == DION_DTYPE_NONE || aligned16(G[b]));
   // no gradient (pass B): split-bf16 MFMA kernels (the column one steps 32 rows)
-  const bool x6 = fast && gdt == DION_DTYPE_NONE && (row_mode ? rows % (64 * kRBE) == 0 : rows % 32 == 0);
+  const bool x6 = fast && gdt == DION_DTYPE_NONE &&
+                  (row_mode ? rows % (64 * kRBE) == 0
+                            : (rows % 32 == 0 && cols % ((r >= 64 ? 32 : 64) * kColX6NW) == 0));
   const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, x6 ? 64 * kRBE : (fast ? 64 * kRB : 128))
                  : x6      ? colx6_geo(rows, cols, batch, r)
                            : colproj_geo(rows, cols, batch, false);
@@ -2993,7 +3128,7 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
       if (x6 && row_mode)
         hipLaunchKernelGGL((rowproj_x6_kernel<RB>), grid, dim3(256), 0, st, a);
       else if (x6)
-        hipLaunchKernelGGL((colproj_x6_kernel<RB>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((colproj_x6_kernel<RB, kColX6NW>), grid, dim3(64 * kColX6NW), 0, st, a);
       else if (fast && row_mode)
         hipLaunchKernelGGL((rowproj_fast_kernel<RB, GD>), grid, dim3(256), 0, st, a);
       else if (fast)
@@ -3330,8 +3465,10 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
         constexpr int GD = decltype(Gc)::value;
         if (tr)
           hipLaunchKernelGGL((colproj_ef_kernel<RB, GD>), grid, dim3(256), 0, st, e);
+        else if (pa_lines())
+          hipLaunchKernelGGL((rowproj_ef_kernel<RB, GD, 2, true>), grid, dim3(64 * kPaNW), 0, st, e);
         else
-          hipLaunchKernelGGL((rowproj_ef_kernel<RB, GD>), grid, dim3(256), 0, st, e);
+          hipLaunchKernelGGL((rowproj_ef_kernel<RB, GD, 2, false>), grid, dim3(64 * kPaNW), 0, st, e);
         return check_launch(tr ? "colproj_ef" : "rowproj_ef");
       });
     };
