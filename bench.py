@@ -165,6 +165,56 @@ def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps, deferred):
     return roofline
 
 
+class LoopbackGroup:
+    """--simulate-world W: a replicate group of W ranks whose collectives are local copies.
+
+    Runs the W > 1 batch schedule (batches of W same-shape matrices, the owner rank's
+    single-matrix orthonormalisation, the AsyncRuntime interleave) on one GPU with the
+    exchange itself removed, to time the compute side of the N = W step."""
+
+    def __init__(self, world):
+        self.ranks = tuple(range(world))
+
+
+class _DoneWork:
+    def wait(self):
+        return True
+
+
+def install_loopback(world):
+    group = LoopbackGroup(world)
+    real = {k: getattr(dist, k) for k in ("get_world_size", "get_rank", "reduce_scatter_tensor",
+                                          "all_gather_into_tensor", "all_reduce")}
+
+    def get_world_size(g=None):
+        return world if isinstance(g, LoopbackGroup) else real["get_world_size"](g)
+
+    def get_rank(g=None):
+        return 0 if isinstance(g, LoopbackGroup) else real["get_rank"](g)
+
+    def reduce_scatter_tensor(out, inp, op=None, group=None, async_op=False):
+        if not isinstance(group, LoopbackGroup):
+            return real["reduce_scatter_tensor"](out, inp, op=op, group=group, async_op=async_op)
+        out.copy_(inp[: out.shape[0]])
+        return _DoneWork() if async_op else None
+
+    def all_gather_into_tensor(out, inp, group=None, async_op=False):
+        if not isinstance(group, LoopbackGroup):
+            return real["all_gather_into_tensor"](out, inp, group=group, async_op=async_op)
+        out[: inp.shape[0]].copy_(inp)
+        return _DoneWork() if async_op else None
+
+    def all_reduce(t, op=None, group=None, async_op=False):
+        if not isinstance(group, LoopbackGroup):
+            return real["all_reduce"](t, op=op, group=group, async_op=async_op)
+        return _DoneWork() if async_op else None
+
+    dist.get_world_size, dist.get_rank = get_world_size, get_rank
+    dist.reduce_scatter_tensor, dist.all_gather_into_tensor, dist.all_reduce = (
+        reduce_scatter_tensor, all_gather_into_tensor, all_reduce)
+    return group
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -179,6 +229,8 @@ def main():
                     help="collective backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     ap.add_argument("--eager-ef", action="store_true",
                     help="apply each step's error feedback in its own pass (default: deferred into the next pass A)")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="time the W-rank batch schedule on one GPU with loopback collectives (not a bench line)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -212,6 +264,8 @@ def main():
     opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=1 / 64,
                            codec=codec, local_streams=args.streams, defer_error_feedback=not args.eager_ef,
                            coalesce_max_entries=args.coalesce)
+    if args.simulate_world > 1:
+        group = install_loopback(args.simulate_world)
     attach_dp_routing(opt, named, replicate_group=group)
     elems = sum(m * n for _, m, n in shapes)
 
@@ -269,6 +323,9 @@ def main():
                       "error_feedback": "eager" if args.eager_ef else "deferred (applied in the next step's pass A)",
                       "parallelism": f"dp{world} (replicate, low-rank P/R exchange)" if world > 1 else "dp1"},
            "roofline": roofline}
+    if args.simulate_world > 1:
+        out["simulated_world"] = args.simulate_world
+        out["metric"] = "SIMULATED (loopback collectives, not a bench line): " + METRIC
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -24,8 +24,8 @@ import torch.distributed as dist
 from torch.optim.optimizer import Optimizer
 
 from .batches import build_dion_batches
-from .runtime import (AsyncRuntime, coalesce_local_batches, flush_pending_error_feedback, is_replicated,
-                      run_dion_batch_async)
+from .runtime import (AsyncRuntime, coalesce_local_batches, coalesce_replicated_batches,
+                      flush_pending_error_feedback, is_replicated, run_dion_batch_async)
 from .state import init_dion_state
 from .types import DionDistMeta, DionMixedPrecisionConfig, DionStepParam
 
@@ -121,6 +121,7 @@ class MegatronDion(Optimizer):
         self._dion_update_count += sum(int(b.real_batch_size) for b in batches)
         if self._coalesce_local:
             batches = coalesce_local_batches(batches, max_entries=self._coalesce_max)
+            batches = coalesce_replicated_batches(batches, max_entries=self._coalesce_max)
         return batches
 
     def _run_local_overlapped(self, batches, sketches) -> bool:

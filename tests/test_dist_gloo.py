@@ -116,3 +116,71 @@ def test_gloo_w2_padding_and_per_batch_p():
         for k in ("W", "M", "Q"):
             err = _maxrel(res[rank][f"s{step}_{n}_{k}"], st[k])
             assert err <= 1e-6, (rank, n, k, err)
+
+
+def _coalesce_worker(rank, world, port, out_dir, deferred):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    import megatron_dion_amd as mda
+    from megatron_dion_amd.optimizer import attach_dp_routing
+    from tests._cpu_codec import OracleCodec
+
+    shapes = [(f"a{i}", 64, 48) for i in range(6)] + [(f"t{i}", 48, 96) for i in range(4)] + [("odd", 64, 48)]
+    sketch_gen = {}
+
+    def fixed_sketch(P):  # one sketch per shape, identical in both schedules
+        mp_ = int(P.shape[-2])
+        if mp_ not in sketch_gen:
+            g = torch.Generator().manual_seed(7 + mp_)
+            sketch_gen[mp_] = torch.randn(1, 128, mp_, generator=g) * (1.0 / 128) ** 0.5
+        return sketch_gen[mp_]
+
+    runs = {}
+    for coalesce in (False, True):
+        torch.manual_seed(0)
+        params = [(n, torch.nn.Parameter(torch.randn(m, k) * 0.02)) for n, m, k in shapes]
+        codec = OracleCodec(sketch_lookup=fixed_sketch, deferred=deferred)
+        opt = mda.MegatronDion([p for _, p in params], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=0.125,
+                               codec=codec, coalesce_local=coalesce, coalesce_max_entries=4,
+                               defer_error_feedback=deferred)
+        attach_dp_routing(opt, params, replicate_group=dist.group.WORLD)
+        chunks = []
+        for step in range(3):
+            gen = torch.Generator().manual_seed(100 * step + 10 * rank + 1)
+            for _, p in params:
+                p.grad = (torch.randn(p.shape, generator=gen) * 1e-3).to(torch.bfloat16).float()
+            chunks.append([int(getattr(b, "_chunks", 0) or 0) for b in opt._batches()])
+            opt.step()
+        opt.flush_error_feedback()
+        runs[coalesce] = {"chunks": chunks,
+                          **{f"{n}_{k}": v.detach().clone() for n, p in params
+                             for k, v in (("W", p), ("M", opt.state[p]["momentum"]), ("Q", opt.state[p]["Q"]))}}
+    torch.save(runs, os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("deferred", [False, True], ids=["eager_ef", "deferred_ef"])
+def test_gloo_w2_coalesced_groups_match_per_batch(deferred):
+    """coalesce_replicated_batches: one RS / batched ortho / AG / AR per group of full
+    batches, rank-major layout -- same entries on the same ranks, same results."""
+    world = 2
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_coalesce_worker, args=(world, _free_port(), tmp, deferred), nprocs=world, join=True,
+                           start_method="spawn")
+        res = [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+    for rank in range(world):
+        plain, merged = res[rank][False], res[rank][True]
+        assert all(c == 0 for step in plain["chunks"] for c in step)
+        # 7 (64x48) -> groups of 2 full batches + 1 full + a padded one; 4 (48x96) -> 1 group of 2
+        assert max(max(step) for step in merged["chunks"]) == 2
+        for key, ref in plain.items():
+            if key == "chunks":
+                continue
+            err = _maxrel(merged[key], ref)
+            assert err <= 1e-6, (rank, key, err)
+    for key in res[0][True]:
+        if key.endswith("_W") or key.endswith("_Q"):
+            assert torch.equal(res[0][True][key], res[1][True][key]), key
