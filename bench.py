@@ -225,6 +225,9 @@ def main():
     ap.add_argument("--streams", type=int, default=2, help="HIP streams for independent batches (N=1 path)")
     ap.add_argument("--probe-steps", type=int, default=2, help="single-stream steps timed per kernel for `roofline`")
     ap.add_argument("--coalesce", type=int, default=16, help="matrices per launch group at N = 1")
+    ap.add_argument("--lookahead", type=int, default=0,
+                    help="N = 1 software pipeline depth (groups whose pass A runs before a pass B); 0 = two "
+                         "alternating streams")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="collective backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     ap.add_argument("--eager-ef", action="store_true",
@@ -263,7 +266,7 @@ def main():
     codec = TimedCodec(HipDionCodec(dev))
     opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=1 / 64,
                            codec=codec, local_streams=args.streams, defer_error_feedback=not args.eager_ef,
-                           coalesce_max_entries=args.coalesce)
+                           coalesce_max_entries=args.coalesce, pipeline_lookahead=args.lookahead)
     if args.simulate_world > 1:
         group = install_loopback(args.simulate_world)
     attach_dp_routing(opt, named, replicate_group=group)

@@ -41,7 +41,7 @@ class MegatronDion(Optimizer):
                  extra_scale_factor: float = 0.2, split_qkv: bool = False, split_linear: bool = False,
                  max_concurrent_tasks: Optional[int] = None, *, codec=None, sketch_seed: int = 0,
                  coalesce_local: bool = True, local_streams: int = 2, coalesce_max_entries: int = 16,
-                 defer_error_feedback: bool = False):
+                 defer_error_feedback: bool = False, pipeline_lookahead: int = 0):
         if isinstance(params, (list, tuple)):
             for pg in params:
                 if isinstance(pg, dict) and "wd_mult" in pg:
@@ -76,6 +76,8 @@ class MegatronDion(Optimizer):
         self._coalesce_max = max(1, int(coalesce_max_entries))
         self._streams = None
         self._rstreams = None
+        self._pstreams = None
+        self._pipeline_lookahead = max(0, int(pipeline_lookahead))
         self._codec = codec
         self._defer_ef = bool(defer_error_feedback)
         self._profile_records: List[Tuple[str, float]] = []
@@ -147,6 +149,65 @@ class MegatronDion(Optimizer):
             main.wait_stream(s)
         return True
 
+    def _run_local_pipelined(self, batches, sketches) -> bool:
+        """World-size-1 schedule, software-pipelined over two HIP streams.
+
+        Stream S runs every streaming pass (pass A, pass B, fix-up, the updates) one
+        launch group after another; stream L runs each group's latency-bound
+        orthonormalisation as soon as its pass A is done.  S enqueues group k's pass B
+        only after the pass A of groups k+1 .. k+lookahead, so L's work always has
+        streaming work beside it and the streaming kernels never share the memory
+        system with each other.  Events carry the two hand-offs (A_k -> ortho_k on L,
+        ortho_k -> B_k on S); per-group buffers live until the group's last kernel
+        on S."""
+        if self._local_streams <= 1 or self._pipeline_lookahead <= 0 or not torch.cuda.is_available() \
+                or not batches:
+            return False
+        if any(is_replicated(b) for b in batches):
+            return False
+        if not all(getattr(b.params[0], "is_cuda", False) for b in batches):
+            return False
+        dev = batches[0].params[0].device
+        if self._pstreams is None or self._pstreams[0].device != dev:
+            self._pstreams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+        S, L = self._pstreams
+        main = torch.cuda.current_stream(dev)
+        S.wait_stream(main)
+        L.wait_stream(main)
+
+        def advance(gen, stream):
+            with torch.cuda.stream(stream):
+                try:
+                    return next(gen)
+                except StopIteration:
+                    return None
+
+        pending = []
+        for b in batches:
+            gen = run_dion_batch_async(self, b, sketches=sketches(b) if sketches else None, phase_marks=True)
+            if advance(gen, S) != "ortho":
+                continue
+            ev = torch.cuda.Event()
+            ev.record(S)
+            L.wait_event(ev)
+            if advance(gen, L) != "stream":
+                raise RuntimeError("[DION_INTERNAL] pipelined batch lost its phase marks")
+            done = torch.cuda.Event()
+            done.record(L)
+            pending.append((gen, done))
+            while len(pending) > self._pipeline_lookahead:
+                g0, e0 = pending.pop(0)
+                S.wait_event(e0)
+                if advance(g0, S) is not None:
+                    raise RuntimeError("[DION_INTERNAL] pipelined batch yielded after its phases")
+        for g0, e0 in pending:
+            S.wait_event(e0)
+            if advance(g0, S) is not None:
+                raise RuntimeError("[DION_INTERNAL] pipelined batch yielded after its phases")
+        main.wait_stream(S)
+        main.wait_stream(L)
+        return True
+
     def _replica_streams(self, batches, width):
         """One HIP stream per AsyncRuntime slot for replicated (W > 1) batches on the GPU."""
         if self._local_streams <= 1 or not torch.cuda.is_available() or not batches:
@@ -176,7 +237,7 @@ class MegatronDion(Optimizer):
         width = 3 if self.max_concurrent_tasks is None else int(self.max_concurrent_tasks)
         sketches = getattr(self, "_sketch_override", None)
         batches = self._batches()
-        if not self._run_local_overlapped(batches, sketches):
+        if not (self._run_local_pipelined(batches, sketches) or self._run_local_overlapped(batches, sketches)):
             streams = self._replica_streams(batches, width)
             main = torch.cuda.current_stream(streams[0].device) if streams else None
             for s in streams or ():

@@ -117,12 +117,16 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
                             optimizer_states=None, param_shapes=None, real_batch_size=None,
                             batch_cache_key: int = 0, batch_group=None, batch_collectives=None,
                             commit_updates: Optional[List[Optional[Callable]]] = None,
-                            sketches: Optional[dict] = None, chunks: int = 0) -> Generator[None, None, None]:
+                            sketches: Optional[dict] = None, chunks: int = 0,
+                            phase_marks: bool = False) -> Generator[None, None, None]:
     """One batch of same-shape matrices: project, exchange, orthonormalise, update.
 
     `sketches` (tests only) maps an entry index to an explicit (k, m_P) sketch so
     parity runs can reuse the sketch the reference drew.  `chunks` > 1 marks a
     coalesced group of full W-entry batches (coalesce_replicated_batches).
+    `phase_marks` (world size 1 only): yield "ortho" after pass A and "stream" after
+    the orthonormalisation, so a scheduler can run the latency-bound phase on another
+    HIP stream (MegatronDion._run_local_pipelined).
     """
     codec = optimizer.codec
     B = len(params)
@@ -259,12 +263,16 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
             yield
             work.wait()
     else:
+        if phase_marks:
+            yield "ortho"
         if sketches is None:
             codec.orthonormalize(P[:real], m, n, transposed, _sketch_seed(optimizer, batch_cache_key, 0),
                                  oversample)
         else:
             for i in range(real):
                 ortho(P[i:i + 1], i)
+        if phase_marks:
+            yield "stream"
         R = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
         codec.project_r(list(momentums[:real]), P, R, transposed)
 
@@ -332,7 +340,7 @@ def flush_pending_error_feedback(optimizer, get_codec) -> int:
     return count
 
 
-def run_dion_batch_async(optimizer, batch, sketches=None) -> Generator[None, None, None]:
+def run_dion_batch_async(optimizer, batch, sketches=None, phase_marks=False) -> Generator[None, None, None]:
     """Unpack a DionBatch (ours or the reference's) into batch_dion_update_async."""
     if batch is None or not batch.params:
         return
@@ -343,7 +351,7 @@ def run_dion_batch_async(optimizer, batch, sketches=None) -> Generator[None, Non
         list(batch.dist_metas), list(batch.optim_groups), list(batch.grads), list(batch.optimizer_states),
         list(batch.param_shapes), int(batch.real_batch_size), int(batch.batch_cache_key), batch.batch_group,
         batch.batch_collectives, commit_updates=commit, sketches=sketches,
-        chunks=int(getattr(batch, "_chunks", 0) or 0))
+        chunks=int(getattr(batch, "_chunks", 0) or 0), phase_marks=phase_marks)
 
 
 def coalesce_replicated_batches(batches, max_entries: int = 16):
