@@ -18,6 +18,12 @@
  *    the reference's P_batch / R_batch;
  *  - M, W are fp32 row-major m x n (row stride ld_m / ld_w elements); G is
  *    bf16 or fp32 row-major (ld_g); Q is fp32 n_Q x r contiguous per matrix;
+ *  - bf16 state mode (m_dtype == DION_DTYPE_BF16: the speedrun's
+ *    --dion-momentum-dtype/--dion-q-dtype bfloat16, speedrun_nanogpt_mcore.py:422-431):
+ *    every M and Q pointer then addresses bf16 (uint16) data, W stays fp32, and the
+ *    fp32 P / R buffers hold bf16-representable values, rounded (nearest even)
+ *    wherever the reference's bf16 tensors round (runtime.py:1560-1616, ortho.py:123,
+ *    kernels.py:54-83, 229-290).  dion_project_p_ef is DION_E_UNSUPPORTED in this mode;
  *  - orientation follows the reference's DionParamConfig.is_transposed
  *    (dion/state.py:304-310): transposed == 0 => P has m rows (P = M Q),
  *    transposed == 1 => P has n rows (P = M^T Q).  m_P = transposed ? n : m,
@@ -35,7 +41,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 4
+#define DION_ABI_VERSION 5
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -61,7 +67,7 @@ typedef struct DionBatchDesc {
   int32_t r;          /* rank = columns of P, Q, R  (1..128)                   */
   int32_t transposed; /* reference DionParamConfig.is_transposed               */
   int32_t g_dtype;    /* DION_DTYPE_NONE (no accumulate), _F32 or _BF16        */
-  int32_t m_dtype;    /* DION_DTYPE_F32                                        */
+  int32_t m_dtype;    /* DION_DTYPE_F32, or _BF16 (bf16 momentum and Q)         */
   int32_t w_dtype;    /* DION_DTYPE_F32                                        */
   int64_t ld_g;       /* row strides in elements; 0 means n                    */
   int64_t ld_m;
@@ -158,6 +164,14 @@ int dion_ef_apply(const DionBatchDesc* desc, float* const* M, float* const* W,
                   const float* P, const float* R, const float* const* Qn,
                   const uint32_t* nonzero, float mu, float lr, float wd, float scaled_lr,
                   void* ws, size_t ws_bytes, dion_stream_t stream);
+
+/*
+ * x[i] <- bf16(x[i]) (round to nearest even, kept in fp32 storage), i < n.
+ * The bf16 state mode's rounding after a collective that averages an fp32
+ * buffer of bf16 values (the reference reduces bf16 P / R tensors:
+ * runtime.py:1428-1434 reduce-scatter, :1485-1491 all-reduce).
+ */
+int dion_round_bf16(float* x, int64_t n, dion_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -41,6 +41,22 @@ def _dtype_code(t: Optional[torch.Tensor]) -> int:
     raise RuntimeError(f"[DION_UNSUPPORTED_DTYPE] {t.dtype}")
 
 
+def _dtype_code_state(dtype) -> int:
+    if dtype == torch.float32:
+        return _lib.DTYPE_F32
+    if dtype == torch.bfloat16:
+        return _lib.DTYPE_BF16
+    raise RuntimeError(f"[DION_UNSUPPORTED_STATE_DTYPE] momentum/Q dtype {dtype}")
+
+
+def _state_dtype(momentums, qs) -> torch.dtype:
+    """Momentum and Q share one dtype (fp32, or bf16 for both: speedrun_nanogpt_mcore.py:422-431)."""
+    dts = {t.dtype for t in list(momentums or []) + list(qs or [])}
+    if len(dts) != 1:
+        raise RuntimeError(f"[DION_UNSUPPORTED_MIXED_STATE_DTYPES] momentum/Q dtypes {sorted(map(str, dts))}")
+    return dts.pop()
+
+
 def _row_stride(t: torch.Tensor) -> int:
     if t.dim() != 2 or t.stride(1) != 1:
         raise RuntimeError(f"[DION_NON_ROW_MAJOR] shape={tuple(t.shape)} stride={t.stride()}")
@@ -63,13 +79,15 @@ class HipDionCodec:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def _desc(self, batch, m, n, r, transposed, g=None, M=None, W=None) -> _lib.DionBatchDesc:
+    def _desc(self, batch, m, n, r, transposed, g=None, M=None, W=None, state_dtype=None) -> _lib.DionBatchDesc:
         d = _lib.DionBatchDesc()
         d.batch = int(batch)
         d.m, d.n, d.r = int(m), int(n), int(r)
         d.transposed = 1 if transposed else 0
         d.g_dtype = _dtype_code(g)
-        d.m_dtype = _lib.DTYPE_F32
+        # momentum / Q dtype: fp32, or the speedrun's bf16 state (DionMixedPrecisionConfig)
+        sdt = state_dtype if state_dtype is not None else (M.dtype if M is not None else torch.float32)
+        d.m_dtype = _dtype_code_state(sdt)
         d.w_dtype = _lib.DTYPE_F32
         d.ld_g = _row_stride(g) if g is not None else 0
         d.ld_m = _row_stride(M) if M is not None else 0
@@ -87,10 +105,10 @@ class HipDionCodec:
             self._ws[key] = ws
         return ws
 
-    def _check_batch(self, mats: Sequence[torch.Tensor]):
+    def _check_batch(self, mats: Sequence[torch.Tensor], dtype=torch.float32):
         m, n = mats[0].shape
         for t in mats:
-            if tuple(t.shape) != (m, n) or t.dtype != torch.float32 or t.device != self.device:
+            if tuple(t.shape) != (m, n) or t.dtype != dtype or t.device != self.device:
                 raise RuntimeError(f"[DION_INCONSISTENT_BATCH] {tuple(t.shape)} {t.dtype} {t.device}")
         return int(m), int(n)
 
@@ -101,7 +119,7 @@ class HipDionCodec:
         B = len(momentums)
         if B == 0:
             return
-        m, n = self._check_batch(momentums)
+        m, n = self._check_batch(momentums, _state_dtype(momentums, qs))
         r = int(qs[0].shape[1])
         g0 = grads[0] if grads else None
         if grads:
@@ -115,12 +133,12 @@ class HipDionCodec:
                                      ws.numel(), self._stream())
         _lib.check(rc, "dion_project_p")
 
-    def supports_deferred_ef(self, m: int, n: int, r: int, transposed: bool) -> bool:
+    def supports_deferred_ef(self, m: int, n: int, r: int, transposed: bool, state_dtype=torch.float32) -> bool:
         """True when the fused deferred-EF pass A exists for this shape (dion_project_p_ef)."""
-        key = (int(m), int(n), int(r), bool(transposed))
+        key = (int(m), int(n), int(r), bool(transposed), state_dtype)
         ok = self._ef_ok.get(key)
         if ok is None:
-            d = self._desc(1, m, n, r, transposed)
+            d = self._desc(1, m, n, r, transposed, state_dtype=state_dtype)
             nbytes = ctypes.c_size_t(0)
             ok = self.lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P_EF, ctypes.byref(nbytes)) == 0
             self._ef_ok[key] = ok
@@ -155,12 +173,15 @@ class HipDionCodec:
         _lib.check(rc, "dion_project_p_ef")
 
     def orthonormalize(self, P: torch.Tensor, m: int, n: int, transposed: bool, seed: int,
-                       oversample: float = 1.25, sketch: Optional[torch.Tensor] = None) -> None:
-        """Randomised Cholesky QR of every P_b in place.  ortho.py:71-123."""
+                       oversample: float = 1.25, sketch: Optional[torch.Tensor] = None,
+                       state_dtype=torch.float32) -> None:
+        """Randomised Cholesky QR of every P_b in place.  ortho.py:71-123.
+
+        With a bf16 state the fp32 result is rounded back to bf16 values (ortho.py:123)."""
         B, _, r = P.shape
         if B == 0:
             return
-        d = self._desc(B, m, n, r, transposed)
+        d = self._desc(B, m, n, r, transposed, state_dtype=state_dtype)
         ws = self.workspace(d, _lib.OP_ORTHONORMALIZE)
         rc = self.lib.dion_orthonormalize(ctypes.byref(d), P.data_ptr(),
                                           None if sketch is None else sketch.data_ptr(),
@@ -174,7 +195,7 @@ class HipDionCodec:
         B = len(momentums)
         if B == 0:
             return
-        m, n = self._check_batch(momentums)
+        m, n = self._check_batch(momentums, momentums[0].dtype)
         r = int(P.shape[2])
         d = self._desc(B, m, n, r, transposed, M=momentums[0])
         ws = self.workspace(d, _lib.OP_PROJECT_R)
@@ -189,7 +210,7 @@ class HipDionCodec:
         if B == 0:
             return
         r = int(P.shape[2])
-        d = self._desc(B, m, n, r, transposed)
+        d = self._desc(B, m, n, r, transposed, state_dtype=_state_dtype(None, qs))
         ws = self.workspace(d, _lib.OP_FIXUP_COLNORM)
         rc = self.lib.dion_fixup_colnorm(ctypes.byref(d), P.data_ptr(), R.data_ptr(), _ptrs(qs),
                                          nonzero.data_ptr(), float(eps), ws.data_ptr(), ws.numel(),
@@ -208,14 +229,16 @@ class HipDionCodec:
             return
         if momentums is None and params is None:
             raise RuntimeError("[DION_INTERNAL] ef_apply needs momentums or params")
-        m, n = self._check_batch(momentums if momentums is not None else params)
+        sdt = _state_dtype(momentums, qs)
+        if momentums is not None:
+            m, n = self._check_batch(momentums, sdt)
         if params is not None:
-            self._check_batch(params)
+            m, n = self._check_batch(params)
         r = int(P.shape[2])
         if not (P.is_contiguous() and R.is_contiguous()):
             raise RuntimeError("[DION_BAD_FACTOR] P and R must be contiguous (batch, rows, r)")
         d = self._desc(B, m, n, r, transposed, M=momentums[0] if momentums else None,
-                       W=params[0] if params else None)
+                       W=params[0] if params else None, state_dtype=sdt)
         ws = self.workspace(d, _lib.OP_EF_APPLY) if self.ef_presplit else None
         rc = self.lib.dion_ef_apply(ctypes.byref(d), _ptrs(momentums) if momentums else None,
                                     _ptrs(params) if params else None,
@@ -223,3 +246,10 @@ class HipDionCodec:
                                     float(lr), float(wd), float(scaled_lr), None if ws is None else ws.data_ptr(),
                                     0 if ws is None else ws.numel(), self._stream())
         _lib.check(rc, "dion_ef_apply")
+
+    def round_bf16(self, X: torch.Tensor) -> None:
+        """X <- bf16(X) in place (fp32 storage): the bf16 state's rounding after an averaging
+        collective on P or R (the reference reduces bf16 tensors, runtime.py:1428-1434, 1485-1491)."""
+        if X.dtype != torch.float32 or not X.is_contiguous():
+            raise RuntimeError(f"[DION_BAD_FACTOR] round_bf16 needs a contiguous fp32 buffer, got {X.dtype}")
+        _lib.check(self.lib.dion_round_bf16(X.data_ptr(), X.numel(), self._stream()), "dion_round_bf16")

@@ -1,0 +1,459 @@
+// dion_bf16.hpp -- the Dion step with bf16 momentum and bf16 Q (the speedrun's
+// mixed precision: examples/dion/speedrun_nanogpt_mcore.py:422-431,
+// --dion-momentum-dtype / --dion-q-dtype bfloat16).  Included by dion_codec.hip
+// just before the C ABI; the entry points dispatch here when desc->m_dtype is
+// DION_DTYPE_BF16.
+//
+// Reference semantics (all under /root/reference/megatron/core/optimizer/):
+//   dion/runtime.py:1560-1566   M += G.to(bf16)                -> rne(M + rne(G))
+//   dion/runtime.py:1602-1616   P = M_batch @ Q_batch (bf16)    -> rne(sum_k fp32)
+//   dion/ortho.py:90-123        orthogonalize in fp32, cast back -> rne(P)
+//   dion/runtime.py:1476-1477   R = M^T @ P (bf16)              -> rne(sum_k fp32)
+//   dion/kernels.py:54-83       update = rne(P R^T); update = rne(alpha update); M = rne(M + update)
+//   dion/kernels.py:279-290     Qn = rne(R.float() / (sqrt(colsum) + eps))
+//   dion/kernels.py:229-276     delta = rne(P Qn^T)  (bf16 bmm)
+//   dion/runtime.py:1111-1113   W = W (1 - lr wd);  W += -s delta.float()
+// Every bf16 product runs on v_mfma_f32_16x16x32_bf16: exact bf16 x bf16 products
+// accumulated in fp32, rounded once to bf16 (round-to-nearest-even) where torch
+// rounds its bf16 matmul output.  P and R keep the ABI's fp32 buffers; in this
+// mode every value they hold is bf16-representable.
+//
+// Data layout: M (m x n bf16 row-major, ld_m), Q (n_Q x r bf16 per matrix),
+// G bf16 or fp32 (ld_g), W fp32 (ld_w).  The thin operand of a projection (Q or P)
+// is first transposed into a (batch, rpad, K) bf16 panel in the workspace so every
+// MFMA operand is one 16-byte load.
+
+typedef short bf16x8s __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float x) {
+  const uint32_t u = __float_as_uint(x);
+  if ((u & 0x7FFFFFFFu) > 0x7F800000u) return static_cast<uint16_t>((u >> 16) | 0x0040u);  // quiet NaN
+  return static_cast<uint16_t>((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+__device__ __forceinline__ float bf16_round(float x) { return bf16_to_f32(f32_to_bf16_rne(x)); }
+
+// ----------------------------------------------------------------------------- args
+struct B16ProjArgs {
+  uint16_t* x[MAXB];     // M (bf16), accumulated in place when g != null
+  const void* g[MAXB];   // gradient (bf16 or fp32) or null
+  const uint16_t* tt;    // thin operand, transposed: (batch, rpad, K) bf16
+  float* slab;           // (batch, nchunk, out_rows, r) fp32 partial sums
+  uint32_t* nonzero;     // pass A: nonzero flags (may be null)
+  int rows, cols, r, rpad, kchunk, nchunk, out_rows;
+  int K, Kp;             // contraction length; row stride of the tt panel (multiple of 32)
+  long ld_x, ld_g;
+};
+
+// one 8-wide bf16 run of X at (row, col..col+7), optionally accumulated with G
+// (rne(x + rne(g)), written back), bounds-checked per element at the edges
+template <int GDT>
+__device__ __forceinline__ bf16x8s b16_xload(const B16ProjArgs& a, int b, int row, int col, uint32_t& nz) {
+  bf16x8s v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (row >= a.rows || col >= a.cols) return v;
+  uint16_t* px = a.x[b] + static_cast<long>(row) * a.ld_x + col;
+  const bool full = (col + 8 <= a.cols) && ((reinterpret_cast<uintptr_t>(px) & 15u) == 0);
+  uint16_t e[8];
+  if (full) {
+    const uint4 w = *reinterpret_cast<const uint4*>(px);
+    e[0] = w.x & 0xFFFF; e[1] = w.x >> 16; e[2] = w.y & 0xFFFF; e[3] = w.y >> 16;
+    e[4] = w.z & 0xFFFF; e[5] = w.z >> 16; e[6] = w.w & 0xFFFF; e[7] = w.w >> 16;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = (col + i < a.cols) ? px[i] : 0;
+  }
+  if constexpr (GDT != DION_DTYPE_NONE) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (col + i >= a.cols) break;
+      float gv;
+      if constexpr (GDT == DION_DTYPE_BF16)
+        gv = bf16_to_f32(static_cast<const uint16_t*>(a.g[b])[static_cast<long>(row) * a.ld_g + col + i]);
+      else
+        gv = bf16_round(static_cast<const float*>(a.g[b])[static_cast<long>(row) * a.ld_g + col + i]);
+      e[i] = f32_to_bf16_rne(bf16_to_f32(e[i]) + gv);
+    }
+    if (full) {
+      uint4 w;
+      w.x = e[0] | (static_cast<uint32_t>(e[1]) << 16); w.y = e[2] | (static_cast<uint32_t>(e[3]) << 16);
+      w.z = e[4] | (static_cast<uint32_t>(e[5]) << 16); w.w = e[6] | (static_cast<uint32_t>(e[7]) << 16);
+      *reinterpret_cast<uint4*>(px) = w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (col + i < a.cols) px[i] = e[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    nz |= e[i] & 0x7FFFu;
+    v[i] = static_cast<short>(e[i]);
+  }
+  return v;
+}
+
+__device__ __forceinline__ bf16x8s b16_tload(const uint16_t* tt, int Kp, int c, int k) {
+  // panel rows are Kp (a multiple of 32) long and zero past K: 16-byte aligned runs
+  return *reinterpret_cast<const bf16x8s*>(tt + static_cast<long>(c) * Kp + k);
+}
+
+// out = X T (row mode: out_rows = rows, K = cols) or X^T T (column mode:
+// out_rows = cols, K = rows).  Block = 4 waves = 64 output rows, blockIdx.y =
+// K-chunk, blockIdx.z = matrix.  Row mode reads its MFMA A operand straight
+// from X (8 consecutive columns per lane); column mode stages a 32 x 64 tile of
+// X through LDS (128-byte row segments in, one column per lane out).
+template <bool COL, int RB, int GDT>
+__global__ void __launch_bounds__(256) b16_proj_kernel(const B16ProjArgs a) {
+  __shared__ uint16_t tile[COL ? 32 : 1][COL ? 72 : 1];
+  const int b = blockIdx.z, kc = blockIdx.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int t = lane & 15, g = lane >> 4;
+  const int o0 = blockIdx.x * 64 + wave * 16;  // first output row of this wave
+  const int k_begin = kc * a.kchunk;
+  const int k_end = min(a.K, k_begin + a.kchunk);
+  const uint16_t* tt = a.tt + static_cast<long>(b) * a.rpad * a.Kp;
+  f32x4 acc[RB];
+#pragma unroll
+  for (int cb = 0; cb < RB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t nz = 0;
+  for (int k0 = k_begin; k0 < k_end; k0 += 32) {
+    bf16x8s A;
+    if constexpr (!COL) {
+      // chunk bounds are multiples of 32, so an 8-run never straddles two chunks
+      // (each element is accumulated by exactly one block)
+      A = bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+      if (k0 + 8 * g < k_end) A = b16_xload<GDT>(a, b, o0 + t, k0 + 8 * g, nz);
+    } else {
+      // tile rows = X rows k0 .. k0+31, tile columns = X columns blockIdx.x*64 .. +63
+      const int tr = tid >> 3, tc = (tid & 7) * 8;
+      uint32_t nzt = 0;
+      bf16x8s v = bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+      if (k0 + tr < k_end) v = b16_xload<GDT>(a, b, k0 + tr, blockIdx.x * 64 + tc, nzt);
+      nz |= nzt;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) tile[tr][tc + i] = static_cast<uint16_t>(v[i]);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 8; ++i) A[i] = static_cast<short>(tile[8 * g + i][wave * 16 + t]);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      const bf16x8s B = (k0 + 8 * g < k_end) ? b16_tload(tt, a.Kp, 16 * cb + t, k0 + 8 * g)
+                                             : bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+      acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B, acc[cb], 0, 0, 0);
+    }
+  }
+  float* out = a.slab + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * a.r;
+#pragma unroll
+  for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int orow = o0 + 4 * g + q, c = 16 * cb + t;
+      if (orow < a.out_rows && c < a.r) out[static_cast<long>(orow) * a.r + c] = acc[cb][q];
+    }
+  if (a.nonzero != nullptr && __any(nz != 0u) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+}
+
+// tt[b][c][k] = c < r ? bf16(T_b[k][c]) : 0  for k < K (zero up to the stride Kp)
+struct B16ThinArgs {
+  const void* src[MAXB];  // per matrix: K x r, bf16 (src_bf16) or fp32
+  uint16_t* tt;
+  int K, Kp, r, rpad, src_bf16;
+};
+
+__global__ void __launch_bounds__(256) b16_thin_kernel(const B16ThinArgs a) {
+  const int b = blockIdx.y;
+  const long total = static_cast<long>(a.rpad) * a.Kp;
+  for (long i = static_cast<long>(blockIdx.x) * 256 + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
+    const int c = static_cast<int>(i / a.Kp), k = static_cast<int>(i - static_cast<long>(c) * a.Kp);
+    uint16_t v = 0;
+    if (c < a.r && k < a.K) {
+      const long s = static_cast<long>(k) * a.r + c;
+      v = a.src_bf16 ? static_cast<const uint16_t*>(a.src[b])[s] : f32_to_bf16_rne(static_cast<const float*>(a.src[b])[s]);
+    }
+    a.tt[static_cast<long>(b) * total + i] = v;
+  }
+}
+
+// out[b][e] = rne_bf16(sum_k slab[b][k][e]) in fixed k order
+__global__ void __launch_bounds__(256) b16_reduce_round_kernel(float* __restrict__ out, const float* __restrict__ slab,
+                                                               int nchunk, long per_entry, int batch) {
+  const long total = per_entry * batch;
+  for (long idx = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
+       idx += static_cast<long>(gridDim.x) * blockDim.x) {
+    const long b = idx / per_entry, e = idx - b * per_entry;
+    const float* s = slab + b * nchunk * per_entry + e;
+    float v = 0.f;
+    for (int k = 0; k < nchunk; ++k) v += s[k * per_entry];
+    out[idx] = bf16_round(v);
+  }
+}
+
+__global__ void __launch_bounds__(256) b16_round_kernel(float* __restrict__ x, long n) {
+  for (long i = static_cast<long>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<long>(gridDim.x) * 256)
+    x[i] = bf16_round(x[i]);
+}
+
+// ----------------------------------------------------------------------------- updates
+// For every element (i, j) of the m x n storage:
+//   u = sum_c RF_u[i][c] CF_u[j][c];   M = rne(M + rne(alpha rne(u)))      (error feedback)
+//   d = sum_c RF_w[i][c] CF_w[j][c];   W = fma(beta, rne(d), W decay)      (weight update)
+// not transposed: RF_u = RF_w = P (m x r), CF_u = R (n x r), CF_w = Qn (n x r)
+// transposed:     RF_u = R, RF_w = Qn (m x r),  CF_u = CF_w = P (n x r)
+// The MFMA computes the transposed tile (rows j, columns i) so a lane's four
+// accumulator values are four adjacent columns of one storage row.  A wave owns
+// 64 columns and walks 16-row steps down its block's row range.
+struct B16UpdArgs {
+  uint16_t* m[MAXB];         // bf16 momentum or null (weight update only)
+  float* w[MAXB];            // fp32 weights or null (error feedback only)
+  const void* rf_u[MAXB];    // fp32 (P/R buffers)
+  const void* cf_u[MAXB];
+  const void* rf_w[MAXB];    // fp32 (P) or bf16 (Qn)
+  const void* cf_w[MAXB];
+  int rfw_bf16, cfw_bf16;
+  int rows, cols, r, rows_per_block;
+  long ld_m, ld_w;
+  float alpha, beta, decay;
+};
+
+template <int KS>
+__device__ __forceinline__ void b16_factor(bf16x8s (&o)[KS], const void* base, bool is_bf16, int row, int nrows, int r,
+                                           int g) {
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    bf16x8s v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (row < nrows) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = 32 * s + 8 * g + e;
+        if (c < r) {
+          const long idx = static_cast<long>(row) * r + c;
+          v[e] = static_cast<short>(is_bf16 ? static_cast<const uint16_t*>(base)[idx]
+                                            : f32_to_bf16_rne(static_cast<const float*>(base)[idx]));
+        }
+      }
+    }
+    o[s] = v;
+  }
+}
+
+template <int KS>
+__global__ void __launch_bounds__(256) b16_update_kernel(const B16UpdArgs a) {
+  const int b = blockIdx.z;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int t = lane & 15, g = lane >> 4;
+  const int j0 = blockIdx.x * 256 + wave * 64;
+  const int i_begin = blockIdx.y * a.rows_per_block;
+  const int i_end = min(a.rows, i_begin + a.rows_per_block);
+  uint16_t* M = a.m[b];
+  float* W = a.w[b];
+  // column factors of this wave's 64 columns: 4 blocks of 16 columns, operand rows j = j0 + 16 jb + t
+  bf16x8s cu[4][KS], cw[4][KS];
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) {
+    if (M) b16_factor<KS>(cu[jb], a.cf_u[b], false, j0 + 16 * jb + t, a.cols, a.r, g);
+    if (W) b16_factor<KS>(cw[jb], a.cf_w[b], a.cfw_bf16 != 0, j0 + 16 * jb + t, a.cols, a.r, g);
+  }
+  for (int i0 = i_begin; i0 < i_end; i0 += 16) {
+    const int i = i0 + t;  // the storage row of this lane's accumulator column
+    bf16x8s ru[KS], rw[KS];
+    if (M) b16_factor<KS>(ru, a.rf_u[b], false, i, a.rows, a.r, g);
+    if (W) b16_factor<KS>(rw, a.rf_w[b], a.rfw_bf16 != 0, i, a.rows, a.r, g);
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      const int j = j0 + 16 * jb + 4 * g;  // first of this lane's four columns
+      if (M) {
+        f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cu[jb][s], ru[s], u, 0, 0, 0);
+        if (i < i_end) {
+          uint16_t* pm = M + static_cast<long>(i) * a.ld_m + j;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (j + q < a.cols) {
+              const float upd = bf16_round(a.alpha * bf16_round(u[q]));
+              pm[q] = f32_to_bf16_rne(bf16_to_f32(pm[q]) + upd);
+            }
+        }
+      }
+      if (W) {
+        f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[jb][s], rw[s], d, 0, 0, 0);
+        if (i < i_end) {
+          float* pw = W + static_cast<long>(i) * a.ld_w + j;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (j + q < a.cols) pw[q] = fmaf(a.beta, bf16_round(d[q]), pw[q] * a.decay);
+        }
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- host side
+namespace b16 {
+
+constexpr int kBlockRows = 64;
+
+int rpad_of(int r) { return (r + 15) / 16 * 16; }
+long kpad_of(int K) { return (K + 31) / 32 * 32; }
+
+Geo geo(int out_rows, int K, int batch) {
+  Geo g;
+  g.gx = static_cast<int>(ceil_div(out_rows, kBlockRows));
+  long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
+  long maxc = ceil_div(K, 256);
+  long nc = want < maxc ? want : maxc;
+  if (nc < 1) nc = 1;
+  g.kchunk = round_up(ceil_div(K, nc), 32);
+  g.nchunk = static_cast<int>(ceil_div(K, g.kchunk));
+  g.out_rows = out_rows;
+  return g;
+}
+
+size_t proj_ws(int m, int n, int r, int batch, bool row_mode) {
+  const int out_rows = row_mode ? m : n, K = row_mode ? n : m;
+  const Geo g = geo(out_rows, K, batch);
+  const size_t slab = (sizeof(float) * static_cast<size_t>(batch) * g.nchunk * out_rows * r + 255) / 256 * 256;
+  return slab + sizeof(uint16_t) * static_cast<size_t>(batch) * rpad_of(r) * kpad_of(K);
+}
+
+// one projection of up to MAXB matrices: out (batch, out_rows, r) = rne(X T) or rne(X^T T)
+int project(bool row_mode, int m, int n, int r, int nb, const void* const* G, int gdt, uint16_t* const* X, long ld_x,
+            long ld_g, const void* const* thin, bool thin_bf16, float* out, uint32_t* nonzero, void* ws,
+            size_t ws_bytes, hipStream_t st) {
+  if (r > 128) return fail(DION_E_UNSUPPORTED, "bf16 path: r=%d > 128", r);
+  const int out_rows = row_mode ? m : n, K = row_mode ? n : m;
+  const Geo g = geo(out_rows, K, nb);
+  const size_t need = proj_ws(m, n, r, nb, row_mode);
+  if (ws == nullptr || ws_bytes < need) return fail(DION_E_WORKSPACE, "bf16 projection needs %zu workspace bytes, got %zu", need, ws_bytes);
+  const size_t slab_b = (sizeof(float) * static_cast<size_t>(nb) * g.nchunk * out_rows * r + 255) / 256 * 256;
+  float* slab = static_cast<float*>(ws);
+  uint16_t* tt = reinterpret_cast<uint16_t*>(static_cast<char*>(ws) + slab_b);
+  const int rp = rpad_of(r);
+  const long Kp = kpad_of(K);
+  {
+    B16ThinArgs ta;
+    memset(&ta, 0, sizeof(ta));
+    for (int b = 0; b < nb; ++b) ta.src[b] = thin[b];
+    ta.tt = tt;
+    ta.K = K;
+    ta.Kp = static_cast<int>(Kp);
+    ta.r = r;
+    ta.rpad = rp;
+    ta.src_bf16 = thin_bf16 ? 1 : 0;
+    long blocks = ceil_div(static_cast<long>(rp) * Kp, 256);
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(b16_thin_kernel, dim3(static_cast<unsigned>(blocks), nb), dim3(256), 0, st, ta);
+    int rc = check_launch("b16_thin");
+    if (rc != DION_OK) return rc;
+  }
+  B16ProjArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int b = 0; b < nb; ++b) {
+    a.x[b] = X[b];
+    a.g[b] = G ? G[b] : nullptr;
+    if (X[b] == nullptr || (gdt != DION_DTYPE_NONE && a.g[b] == nullptr)) return fail(DION_E_INVALID, "null matrix at %d", b);
+  }
+  a.tt = tt;
+  a.slab = slab;
+  a.nonzero = nonzero;
+  a.rows = m;
+  a.cols = n;
+  a.r = r;
+  a.rpad = rp;
+  a.kchunk = g.kchunk;
+  a.nchunk = g.nchunk;
+  a.out_rows = out_rows;
+  a.K = K;
+  a.Kp = static_cast<int>(Kp);
+  a.ld_x = ld_x;
+  a.ld_g = ld_g;
+  const dim3 grid(g.gx, g.nchunk, nb);
+  auto launch = [&](auto RBc) {
+    constexpr int RB = decltype(RBc)::value;
+    return dispatch_gdt(gdt, [&](auto Gc) {
+      constexpr int GD = decltype(Gc)::value;
+      if (row_mode)
+        hipLaunchKernelGGL((b16_proj_kernel<false, RB, GD>), grid, dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((b16_proj_kernel<true, RB, GD>), grid, dim3(256), 0, st, a);
+      return check_launch("b16_proj");
+    });
+  };
+  int rc;
+  switch (rp / 16) {
+    case 1: rc = launch(std::integral_constant<int, 1>{}); break;
+    case 2: rc = launch(std::integral_constant<int, 2>{}); break;
+    case 3: rc = launch(std::integral_constant<int, 3>{}); break;
+    case 4: rc = launch(std::integral_constant<int, 4>{}); break;
+    case 5: rc = launch(std::integral_constant<int, 5>{}); break;
+    case 6: rc = launch(std::integral_constant<int, 6>{}); break;
+    case 7: rc = launch(std::integral_constant<int, 7>{}); break;
+    default: rc = launch(std::integral_constant<int, 8>{}); break;
+  }
+  if (rc != DION_OK) return rc;
+  const long per = static_cast<long>(out_rows) * r;
+  long blocks = ceil_div(per * nb, 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(b16_reduce_round_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, out, slab, g.nchunk,
+                     per, nb);
+  return check_launch("b16_reduce_round");
+}
+
+int round_buffer(float* x, long n, hipStream_t st) {
+  if (n <= 0) return DION_OK;
+  long blocks = ceil_div(n, 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(b16_round_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, x, n);
+  return check_launch("b16_round");
+}
+
+int update(const DionBatchDesc* d, uint16_t* const* M, float* const* W, const float* P, const float* R,
+           const uint16_t* const* Qn, float alpha, float beta, float decay, hipStream_t st) {
+  const int mp = d->transposed ? d->n : d->m;
+  const int nq = d->transposed ? d->m : d->n;
+  const int r = d->r;
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    B16UpdArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int b = 0; b < nb; ++b) {
+      const float* Pb = P + static_cast<long>(b0 + b) * mp * r;
+      const float* Rb = R + static_cast<long>(b0 + b) * nq * r;
+      a.m[b] = M ? M[b0 + b] : nullptr;
+      a.w[b] = W ? W[b0 + b] : nullptr;
+      if ((M && a.m[b] == nullptr) || (W && a.w[b] == nullptr) || Qn[b0 + b] == nullptr)
+        return fail(DION_E_INVALID, "null pointer at entry %d", b0 + b);
+      if (!d->transposed) {
+        a.rf_u[b] = Pb; a.cf_u[b] = Rb; a.rf_w[b] = Pb; a.cf_w[b] = Qn[b0 + b];
+      } else {
+        a.rf_u[b] = Rb; a.cf_u[b] = Pb; a.rf_w[b] = Qn[b0 + b]; a.cf_w[b] = Pb;
+      }
+    }
+    a.rfw_bf16 = d->transposed ? 1 : 0;
+    a.cfw_bf16 = d->transposed ? 0 : 1;
+    a.rows = d->m;
+    a.cols = d->n;
+    a.r = r;
+    a.rows_per_block = 256;
+    a.ld_m = ldv(d->ld_m, d->n);
+    a.ld_w = ldv(d->ld_w, d->n);
+    a.alpha = alpha;
+    a.beta = beta;
+    a.decay = decay;
+    const dim3 grid(static_cast<unsigned>(ceil_div(d->n, 256)), static_cast<unsigned>(ceil_div(d->m, a.rows_per_block)), nb);
+    const int ks = (r + 31) / 32;
+    if (ks == 1) hipLaunchKernelGGL(b16_update_kernel<1>, grid, dim3(256), 0, st, a);
+    else if (ks == 2) hipLaunchKernelGGL(b16_update_kernel<2>, grid, dim3(256), 0, st, a);
+    else if (ks == 3) hipLaunchKernelGGL(b16_update_kernel<3>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(b16_update_kernel<4>, grid, dim3(256), 0, st, a);
+    int rc = check_launch("b16_update");
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+}  // namespace b16

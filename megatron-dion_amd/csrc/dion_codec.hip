@@ -1265,7 +1265,8 @@ __global__ void __launch_bounds__(256) chol_inv_kernel(const float* __restrict__
 // reduction), so the column sums are deterministic.
 // ============================================================================
 struct FixArgs {
-  float* q[MAXB];
+  float* q[MAXB];     // fp32, or bf16 (uint16_t) when q_bf16
+  int q_bf16;
   float* R;           // (batch, nq, r)
   float* part;        // (batch, nchunk, r) partial column sums of squares
   const uint32_t* nonzero;
@@ -1289,7 +1290,8 @@ __global__ void __launch_bounds__(256) fixup_partial_kernel(const FixArgs a) {
   if (p < tpc) {
     for (int row = row0 + p; row < row1; row += tpc) {
       const long idx = static_cast<long>(row) * r + c;
-      const float v = zero ? nan_to_num(Q[idx]) : nan_to_num(R[idx]);
+      const float qv = a.q_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(Q)[idx]) : Q[idx];
+      const float v = zero ? nan_to_num(qv) : nan_to_num(R[idx]);
       R[idx] = v;
       ss += v * v;
     }
@@ -1325,7 +1327,15 @@ __global__ void __launch_bounds__(256) colnorm_apply_kernel(const FixArgs a) {
     const float d = denom[c];
     for (int row = row0 + p; row < row1; row += tpc) {
       const long idx = static_cast<long>(row) * r + c;
-      Q[idx] = R[idx] / d;
+      if (a.q_bf16) {
+        // kernels.py:287-290: the fp32 quotient cast back to R's dtype (bf16, round to nearest even)
+        const uint32_t u = __float_as_uint(R[idx] / d);
+        reinterpret_cast<uint16_t*>(Q)[idx] = ((u & 0x7FFFFFFFu) > 0x7F800000u)
+                                                  ? static_cast<uint16_t>((u >> 16) | 0x40u)
+                                                  : static_cast<uint16_t>((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+      } else {
+        Q[idx] = R[idx] / d;
+      }
     }
   }
 }
@@ -2862,7 +2872,8 @@ int validate(const DionBatchDesc* d) {
     return fail(DION_E_UNSUPPORTED, "rank r=%d outside 1..128", d->r);
   if (d->r > d->m || d->r > d->n)
     return fail(DION_E_INVALID, "rank r=%d exceeds min(m=%d, n=%d)", d->r, d->m, d->n);
-  if (d->m_dtype != DION_DTYPE_F32) return fail(DION_E_UNSUPPORTED, "momentum dtype %d", d->m_dtype);
+  if (d->m_dtype != DION_DTYPE_F32 && d->m_dtype != DION_DTYPE_BF16)
+    return fail(DION_E_UNSUPPORTED, "momentum dtype %d", d->m_dtype);
   if (d->w_dtype != DION_DTYPE_F32) return fail(DION_E_UNSUPPORTED, "weight dtype %d", d->w_dtype);
   if (d->g_dtype != DION_DTYPE_NONE && d->g_dtype != DION_DTYPE_F32 && d->g_dtype != DION_DTYPE_BF16)
     return fail(DION_E_UNSUPPORTED, "grad dtype %d", d->g_dtype);
@@ -3291,6 +3302,8 @@ size_t qr_lds_bytes(int K, int r) { return sizeof(float) * (static_cast<size_t>(
 // ============================================================================
 // C ABI
 // ============================================================================
+#include "dion_bf16.hpp"
+
 extern "C" {
 
 int dion_abi_version(void) { return DION_ABI_VERSION; }
@@ -3305,6 +3318,24 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
   const int nq = d->transposed ? d->m : d->n;
   size_t need = 0;
   const int chunks[2] = {d->batch < MAXB ? d->batch : MAXB, d->batch % MAXB};
+  if (d->m_dtype == DION_DTYPE_BF16) {
+    if (op == DION_OP_PROJECT_P_EF)
+      return fail(DION_E_UNSUPPORTED, "no deferred-EF pass A for bf16 momentum");
+    if (op == DION_OP_PROJECT_P || op == DION_OP_PROJECT_R) {
+      const bool row_mode = (op == DION_OP_PROJECT_P) ? !d->transposed : d->transposed;
+      for (int ci = 0; ci < 2; ++ci)
+        if (chunks[ci] > 0) {
+          const size_t n = b16::proj_ws(d->m, d->n, d->r, chunks[ci], row_mode);
+          if (n > need) need = n;
+        }
+      *bytes = need;
+      return DION_OK;
+    }
+    if (op == DION_OP_EF_APPLY) {
+      *bytes = 0;
+      return DION_OK;
+    }
+  }
   for (int ci = 0; ci < 2; ++ci) {
     const int chunk = chunks[ci];
     if (chunk <= 0) continue;
@@ -3367,6 +3398,18 @@ int dion_project_p(const DionBatchDesc* d, const void* const* G, float* const* M
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int mp = d->transposed ? d->n : d->m;
   const long ld_m = ldv(d->ld_m, d->n), ld_g = ldv(d->ld_g, d->n);
+  if (d->m_dtype == DION_DTYPE_BF16) {
+    // bf16 momentum / Q: M = rne(M + rne(G)), P = rne(X Q)
+    for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+      const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+      rc = b16::project(!d->transposed, d->m, d->n, d->r, nb, G ? G + b0 : nullptr, d->g_dtype,
+                        reinterpret_cast<uint16_t* const*>(M + b0), ld_m, ld_g,
+                        reinterpret_cast<const void* const*>(Q + b0), true, P + static_cast<long>(b0) * mp * d->r,
+                        nonzero ? nonzero + b0 : nullptr, ws, ws_bytes, st);
+      if (rc != DION_OK) return rc;
+    }
+    return DION_OK;
+  }
   for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
     const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
     rc = run_projection(!d->transposed, d->m, d->n, d->r, nb, G ? G + b0 : nullptr, M + b0, Q + b0, ld_m, ld_g,
@@ -3383,6 +3426,7 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
   if (ef == nullptr) return dion_project_p(d, G, M, Q, P, nonzero, ws, ws_bytes, stream);
   int rc = validate(d);
   if (rc != DION_OK) return rc;
+  if (d->m_dtype != DION_DTYPE_F32) return fail(DION_E_UNSUPPORTED, "no deferred-EF pass A for bf16 momentum");
   if (M == nullptr || Q == nullptr || P == nullptr || ef->P == nullptr || ef->R == nullptr)
     return fail(DION_E_INVALID, "null argument");
   if (d->g_dtype != DION_DTYPE_NONE && G == nullptr) return fail(DION_E_INVALID, "G is null");
@@ -3491,6 +3535,19 @@ int dion_project_r(const DionBatchDesc* d, const float* const* M, const float* P
   const int mp = d->transposed ? d->n : d->m;
   const int nq = d->transposed ? d->m : d->n;
   const long ld_m = ldv(d->ld_m, d->n);
+  if (d->m_dtype == DION_DTYPE_BF16) {
+    // R = rne(X^T P), P already bf16-valued
+    for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+      const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+      const void* thin[MAXB];
+      for (int b = 0; b < nb; ++b) thin[b] = P + static_cast<long>(b0 + b) * mp * d->r;
+      rc = b16::project(d->transposed != 0, d->m, d->n, d->r, nb, nullptr, DION_DTYPE_NONE,
+                        reinterpret_cast<uint16_t* const*>(const_cast<float* const*>(M + b0)), ld_m, 0, thin, false,
+                        R + static_cast<long>(b0) * nq * d->r, nullptr, ws, ws_bytes, st);
+      if (rc != DION_OK) return rc;
+    }
+    return DION_OK;
+  }
   for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
     const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
     const float* thin[MAXB];
@@ -3523,6 +3580,10 @@ int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, u
       hipLaunchKernelGGL(householder_qr_kernel, dim3(nb), dim3(256), lds, st, Pb, nullptr, Pb, mp, r, 1);
       rc = check_launch("householder_qr(Q)");
       if (rc != DION_OK) return rc;
+      if (d->m_dtype == DION_DTYPE_BF16) {
+        rc = b16::round_buffer(Pb, static_cast<long>(nb) * mp * r, st);
+        if (rc != DION_OK) return rc;
+      }
       continue;
     }
     if (plan.total > ws_bytes || ws == nullptr)
@@ -3562,6 +3623,8 @@ int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, u
     rc = apply_right(p1, Pb, uinv, mp, r, nb, st);
     if (rc != DION_OK) return rc;
   }
+  // ortho.py:123: the fp32 result is cast back to P's dtype
+  if (d->m_dtype == DION_DTYPE_BF16) return b16::round_buffer(P, static_cast<long>(d->batch) * mp * r, st);
   return DION_OK;
 }
 
@@ -3592,6 +3655,7 @@ int dion_fixup_colnorm(const DionBatchDesc* d, float* P, float* R, float* const*
       if (Q[b0 + b] == nullptr) return fail(DION_E_INVALID, "null Q at %d", b0 + b);
       a.q[b] = Q[b0 + b];
     }
+    a.q_bf16 = d->m_dtype == DION_DTYPE_BF16 ? 1 : 0;
     a.R = R + static_cast<long>(b0) * nq * r;
     a.nonzero = nonzero + b0;
     a.nq = nq;
@@ -3621,6 +3685,13 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
   if (P == nullptr || R == nullptr || Qn == nullptr || nonzero == nullptr || (M == nullptr && W == nullptr))
     return fail(DION_E_INVALID, "null argument");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (d->m_dtype == DION_DTYPE_BF16) {
+    // kernels.py:54-83 (bf16): M = rne(M + rne(alpha rne(P R^T)));  runtime.py:1111-1113: W = W d - s rne(P Qn^T)
+    const float alpha = static_cast<float>(-(1.0 - static_cast<double>(mu)));
+    return b16::update(d, reinterpret_cast<uint16_t* const*>(M), W, P, R,
+                       reinterpret_cast<const uint16_t* const*>(Qn), alpha, -scaled_lr,
+                       (wd > 0.f) ? (1.0f - lr * wd) : 1.0f, st);
+  }
   const int mp = d->transposed ? d->n : d->m;
   const int nq = d->transposed ? d->m : d->n;
   const int r = d->r;
@@ -3796,6 +3867,11 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
     if (rc != DION_OK) return rc;
   }
   return DION_OK;
+}
+
+int dion_round_bf16(float* x, int64_t n, dion_stream_t stream) {
+  if (n < 0 || (n > 0 && x == nullptr)) return fail(DION_E_INVALID, "bad buffer (n=%lld)", static_cast<long long>(n));
+  return b16::round_buffer(x, static_cast<long>(n), reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

@@ -252,6 +252,15 @@ class MegatronDion(Optimizer):
         return loss
 
 
+def _as_dtype(d):
+    """DionMixedPrecisionConfig fields may be torch dtypes or their names (state.py str_to_dtype)."""
+    if d is None or isinstance(d, torch.dtype):
+        return d
+    name = str(d).replace("torch.", "")
+    return {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "float32": torch.float32,
+            "fp32": torch.float32, "float": torch.float32}[name]
+
+
 # ---------------------------------------------------------------------------- standalone routing
 def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str, torch.Tensor]],
                       replicate_group=None, base_seed: int = 0) -> Dict[str, torch.Tensor]:
@@ -269,8 +278,11 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
     mult = int(optimizer.defaults.get("rank_multiple_of", 1))
     metas = {}
     for name, p in named_params:
+        mpc = optimizer._mixed_precision_config
         state, cfg = init_dion_state(p, rank_fraction=rf, rank_multiple_of=mult, base_seed=base_seed,
                                      param_uid=(name,), param_name=name,
+                                     momentum_dtype=_as_dtype(getattr(mpc, "momentum_dtype", None)),
+                                     q_dtype=_as_dtype(getattr(mpc, "q_dtype", None)),
                                      use_low_rank_sync=optimizer.use_low_rank_sync)
         optimizer.state[p].update(state)
         metas[name] = (cfg, DionDistMeta(shape=tuple(p.shape), global_shape=tuple(p.shape), rank_fraction=rf,

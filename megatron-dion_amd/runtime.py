@@ -172,6 +172,11 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     mp, nq = factor_rows(m, n, transposed)
     dev = momentums[0].device
     oversample = float(optimizer.defaults["rcqr_oversample"])
+    # bf16 momentum and Q (the speedrun's DionMixedPrecisionConfig): P and R stay fp32
+    # buffers of bf16 values; the kernels round where the reference's bf16 tensors round,
+    # and an averaging collective is followed by the same rounding (round_bf16)
+    sdt = momentums[0].dtype
+    bf16_state = sdt == torch.bfloat16
 
     # padded entries (and the W > 1 exchange buffers) must read as zero; a full
     # world-size-1 batch is written completely by the kernels
@@ -181,7 +186,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     # deferred error feedback: the previous step's M += -(1-mu) P R^T rides on this pass A
     defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
              and (commit_updates is None or all(c is None for c in commit_updates[:real]))
-             and codec.supports_deferred_ef(m, n, r, transposed))
+             and not bf16_state and codec.supports_deferred_ef(m, n, r, transposed))
     pending = [optimizer_states[i].pop(_PENDING_EF, None) if optimizer_states[i] is not None else None
                for i in range(real)]
     if any(p is not None for p in pending):
@@ -201,7 +206,8 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     def ortho(P_slice, entry):
         S = None if sketches is None else sketches.get(entry)
         codec.orthonormalize(P_slice, m, n, transposed, _sketch_seed(optimizer, batch_cache_key, entry),
-                             oversample, sketch=None if S is None else S.reshape(1, *S.shape[-2:]).contiguous())
+                             oversample, sketch=None if S is None else S.reshape(1, *S.shape[-2:]).contiguous(),
+                             state_dtype=sdt)
 
     if W > 1 and kch:
         rank = dist.get_rank(group)
@@ -211,17 +217,20 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
             work = dist.reduce_scatter_tensor(P_own, P, op=dist.ReduceOp.AVG, group=group, async_op=True)
             yield
             work.wait()
+            if bf16_state:
+                codec.round_bf16(P_own)
         else:
             P_own.copy_(mine)
         if sketches is None:
             codec.orthonormalize(P_own, m, n, transposed,
-                                 _sketch_seed(optimizer, batch_cache_key, rank * kch), oversample)
+                                 _sketch_seed(optimizer, batch_cache_key, rank * kch), oversample, state_dtype=sdt)
         else:
             for c in range(kch):
                 S = sketches.get(rank * kch + c)
                 codec.orthonormalize(P_own[c:c + 1], m, n, transposed,
                                      _sketch_seed(optimizer, batch_cache_key, rank * kch + c), oversample,
-                                     sketch=None if S is None else S.reshape(1, *S.shape[-2:]).contiguous())
+                                     sketch=None if S is None else S.reshape(1, *S.shape[-2:]).contiguous(),
+                                     state_dtype=sdt)
         work = dist.all_gather_into_tensor(P, P_own, group=group, async_op=True)
         yield
         work.wait()
@@ -231,6 +240,8 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
             work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
             yield
             work.wait()
+            if bf16_state:
+                codec.round_bf16(R)
     elif W > 1:
         rank = dist.get_rank(group)
         padded = (B + W - 1) // W * W
@@ -245,6 +256,8 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
                                                   async_op=True)
                 yield
                 work.wait()
+                if bf16_state:
+                    codec.round_bf16(P_single)
             else:
                 P_single.copy_(chunk[rank:rank + 1])
             idx = start + rank
@@ -262,12 +275,14 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
             work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
             yield
             work.wait()
+            if bf16_state:
+                codec.round_bf16(R)
     else:
         if phase_marks:
             yield "ortho"
         if sketches is None:
             codec.orthonormalize(P[:real], m, n, transposed, _sketch_seed(optimizer, batch_cache_key, 0),
-                                 oversample)
+                                 oversample, state_dtype=sdt)
         else:
             for i in range(real):
                 ortho(P[i:i + 1], i)

@@ -61,9 +61,12 @@ def init_q(q_global_shape: Tuple[int, int], seed: int, device, dtype=torch.float
 
 def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_of: int = 1,
                     base_seed: int = 0, param_uid=None, param_name: str = "",
-                    momentum_dtype: Optional[torch.dtype] = None,
+                    momentum_dtype: Optional[torch.dtype] = None, q_dtype: Optional[torch.dtype] = None,
                     use_low_rank_sync: bool = True) -> Tuple[dict, DionParamConfig]:
-    """Fresh optimizer state + config for one 2D parameter (no TP/FS sharding)."""
+    """Fresh optimizer state + config for one 2D parameter (no TP/FS sharding).
+
+    `momentum_dtype` / `q_dtype` follow DionMixedPrecisionConfig (dion/state.py:502-514,
+    544-547): None keeps the parameter's dtype; the speedrun sets both to bf16."""
     if param.dim() != 2:
         raise RuntimeError(f"[DION_NOT_2D] shape={tuple(param.shape)}")
     m, n = (int(d) for d in param.shape)
@@ -74,7 +77,7 @@ def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_
                                  q_global_shape=q_shape, is_transposed=transposed)
     state = {
         "momentum": torch.zeros_like(param, dtype=momentum_dtype or param.dtype),
-        "Q": init_q(q_shape, seed, param.device),
+        "Q": init_q(q_shape, seed, param.device, dtype=q_dtype or param.dtype),
         "r": r,
         "local_shape": (m, n),
         "global_shape": (m, n),

@@ -90,6 +90,24 @@ CASES = [
         world=1,
         steps=1,
     ),
+    # (viii) the speedrun's mixed precision: bf16 momentum and bf16 Q
+    # (examples/dion/speedrun_nanogpt_mcore.py:422-431, --dion-momentum-dtype/--dion-q-dtype bfloat16)
+    dict(
+        name="c11_bf16_two_steps_mixed",
+        mats=[("p", 96, 64), ("q", 64, 160), ("s", 96, 64)],
+        r=16,
+        world=1,
+        steps=2,
+        bf16=True,
+    ),
+    dict(
+        name="c12_bf16_w2_two_steps_T",
+        mats=[("x", 48, 80), ("y", 48, 80)],
+        r=8,
+        world=2,
+        steps=2,
+        bf16=True,
+    ),
 ]
 
 HYPER = dict(lr=0.01, mu=0.95, weight_decay=0.01, epsilon=1e-8, rcqr_oversample=1.25,
@@ -138,6 +156,7 @@ def _worker(rank, world, case, port, out_path):
     from megatron.core.optimizer.dion.algorithm import MegatronDion
     from megatron.core.optimizer.dion.types import (
         DionDistMeta,
+        DionMixedPrecisionConfig,
         DionParamConfig,
         DionStepParam,
     )
@@ -151,6 +170,8 @@ def _worker(rank, world, case, port, out_path):
         params[name] = torch.nn.Parameter(inputs[name]["w0"].clone())
     m0, n0 = inputs[names[0]]["m"], inputs[names[0]]["n"]
     rank_fraction = r / min(m0, n0)
+    state_dtype = torch.bfloat16 if case.get("bf16") else torch.float32
+    mixed = DionMixedPrecisionConfig(momentum_dtype=state_dtype, q_dtype=state_dtype) if case.get("bf16") else None
     opt = MegatronDion(
         [params[n] for n in names],
         lr=HYPER["lr"],
@@ -161,6 +182,7 @@ def _worker(rank, world, case, port, out_path):
         rcqr_oversample=HYPER["rcqr_oversample"],
         scale_mode=HYPER["scale_mode"],
         extra_scale_factor=HYPER["extra_scale_factor"],
+        mixed_precision_config=mixed,
     )
     configs, metas = {}, {}
     for name in names:
@@ -174,8 +196,8 @@ def _worker(rank, world, case, port, out_path):
             param_config=configs[name], is_transposed=d["transposed"],
         )
         opt.state[params[name]] = dict(
-            momentum=torch.zeros(m, n),
-            Q=d["q0"].clone(),
+            momentum=torch.zeros(m, n, dtype=state_dtype),
+            Q=d["q0"].clone().to(state_dtype),
             r=r,
             local_shape=(m, n),
             global_shape=(m, n),
@@ -287,7 +309,9 @@ def _worker(rank, world, case, port, out_path):
             arrays[f"s{step}_norm{i}_rin"] = nrm["r_in"]
             arrays[f"s{step}_norm{i}_qout"] = nrm["q_out"]
         meta["steps"].append(smeta)
-    np.savez_compressed(out_path, **{k: v.detach().numpy() for k, v in arrays.items()})
+    # bf16 tensors are stored as their exact fp32 values (numpy has no bf16)
+    np.savez_compressed(out_path, **{k: (v.detach().float() if v.dtype == torch.bfloat16 else v.detach()).numpy()
+                                     for k, v in arrays.items()})
     with open(out_path + ".json", "w") as fh:
         json.dump(meta, fh)
     dist.barrier()
@@ -295,9 +319,18 @@ def _worker(rank, world, case, port, out_path):
 
 
 def main():
+    """`make_golden.py [name ...]` regenerates only the named cases and keeps the rest of the manifest."""
+    only = set(sys.argv[1:])
     manifest = {"hyper": HYPER, "cases": []}
+    if only and os.path.exists(os.path.join(HERE, "manifest.json")):
+        with open(os.path.join(HERE, "manifest.json")) as fh:
+            manifest = json.load(fh)
+        manifest["cases"] = [c for c in manifest["cases"] if c["name"] not in only]
     port = 29611
     for case in CASES:
+        if only and case["name"] not in only:
+            port += 1
+            continue
         world = case["world"]
         with tempfile.TemporaryDirectory() as tmp:
             paths = [os.path.join(tmp, f"rank{r}.npz") for r in range(world)]
@@ -327,6 +360,8 @@ def main():
         entry["rank_meta"] = metas
         manifest["cases"].append(entry)
         print("wrote", out, os.path.getsize(out), "bytes", flush=True)
+    order = [c["name"] for c in CASES]
+    manifest["cases"].sort(key=lambda c: order.index(c["name"]) if c["name"] in order else len(order))
     with open(os.path.join(HERE, "manifest.json"), "w") as fh:
         json.dump(manifest, fh, indent=1, default=list)
 

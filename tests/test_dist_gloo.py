@@ -42,9 +42,13 @@ def _worker(rank, world, port, name, out_dir, deferred=False):
     params = {n: torch.nn.Parameter(case.t(rank, 0, f"{n}_W0").clone()) for n in names}
     state = {"step": 0}
     codec = OracleCodec(sketch_lookup=lambda P: case.sketch_for(rank, state["step"], P), deferred=deferred)
+    # case (viii): the speedrun's bf16 momentum and Q
+    mpc = mda.DionMixedPrecisionConfig(momentum_dtype=torch.bfloat16, q_dtype=torch.bfloat16) \
+        if case.entry.get("bf16") else None
     opt = mda.MegatronDion([params[n] for n in names], lr=h["lr"], mu=h["mu"], weight_decay=h["weight_decay"],
                            rank_fraction=case.rank_fraction, epsilon=h["epsilon"],
-                           rcqr_oversample=h["rcqr_oversample"], codec=codec, defer_error_feedback=deferred)
+                           rcqr_oversample=h["rcqr_oversample"], codec=codec, defer_error_feedback=deferred,
+                           mixed_precision_config=mpc)
     attach_dp_routing(opt, [(n, params[n]) for n in names], replicate_group=dist.group.WORLD)
     for n in names:
         opt.state[params[n]]["Q"].copy_(case.t(rank, 0, f"{n}_Q0"))
@@ -101,6 +105,30 @@ def test_gloo_w2_matches_reference_single_batch(deferred):
         assert torch.equal(res[0][f"s1_{n}_W"], res[1][f"s1_{n}_W"])
         assert torch.equal(res[0][f"s1_{n}_Q"], res[1][f"s1_{n}_Q"])
         assert not torch.equal(res[0][f"s1_{n}_M"], res[1][f"s1_{n}_M"])
+
+
+def test_gloo_w2_bf16_state_matches_reference():
+    """Case (viii) at world size 2: bf16 momentum and Q through the product runtime
+    (reduce-scatter / all-gather of P, all-reduce of R, each average rounded back to
+    bf16) against the reference's 2-rank bf16 capture c12.  The CPU codec's bf16
+    products accumulate in another order than the reference's bf16 matmul, so single
+    bf16 roundings may differ: bar 1 bf16 ulp of the largest element (2^-8)."""
+    from tests._golden import Case
+
+    case = Case("c12_bf16_w2_two_steps_T")
+    res = _run(case.name)
+    names = [n for n, _, _ in case.mats]
+    for rank in range(2):
+        for step in range(case.steps):
+            for n in names:
+                assert res[rank][f"s{step}_{n}_M"].dtype == torch.bfloat16
+                assert res[rank][f"s{step}_{n}_Q"].dtype == torch.bfloat16
+                for k, ref in (("W", "W1"), ("M", "M1"), ("Q", "Q1")):
+                    err = _maxrel(res[rank][f"s{step}_{n}_{k}"].float(), case.t(rank, step, f"{n}_{ref}"))
+                    assert err <= 2 ** -8, (rank, step, n, k, err)
+    for n in names:
+        assert torch.equal(res[0][f"s1_{n}_W"], res[1][f"s1_{n}_W"])
+        assert torch.equal(res[0][f"s1_{n}_Q"], res[1][f"s1_{n}_Q"])
 
 
 def test_gloo_w2_padding_and_per_batch_p():

@@ -25,7 +25,7 @@ def _header_symbols():
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     syms = _header_symbols()
-    assert len(syms) == 9
+    assert len(syms) == 10
     assert sorted(_lib.EXPORTED) == syms
     for s in syms:
         assert getattr(lib, s) is not None
@@ -45,6 +45,12 @@ def test_deferred_ef_query_names_the_fused_shapes():
         assert (rc == _lib.DION_OK) == ok, (m, n, r, tr, rc)
         if not ok:
             assert rc == _lib.DION_E_UNSUPPORTED
+        # bf16 momentum (case viii) has no fused deferred-EF pass A: the eager schedule runs
+        d.m_dtype = _lib.DTYPE_BF16
+        assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P_EF, ctypes.byref(nbytes)) \
+            == _lib.DION_E_UNSUPPORTED
+        for op in (_lib.OP_PROJECT_P, _lib.OP_PROJECT_R, _lib.OP_ORTHONORMALIZE, _lib.OP_FIXUP_COLNORM):
+            assert lib.dion_workspace_bytes(ctypes.byref(d), op, ctypes.byref(nbytes)) == _lib.DION_OK
 
 
 def test_abi_rejects_bad_descriptors_without_gpu():
@@ -58,7 +64,9 @@ def test_abi_rejects_bad_descriptors_without_gpu():
         _lib.DION_E_UNSUPPORTED
     assert b"rank" in lib.dion_last_error()
     d.r = 8
-    d.m_dtype = _lib.DTYPE_BF16
+    d.m_dtype = _lib.DTYPE_BF16     # the bf16 state mode (case viii) is supported ...
+    assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P, ctypes.byref(nbytes)) == _lib.DION_OK
+    d.m_dtype = 7                   # ... other state dtypes are not
     assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P, ctypes.byref(nbytes)) == \
         _lib.DION_E_UNSUPPORTED
     d.m_dtype = _lib.DTYPE_F32
