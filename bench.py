@@ -54,6 +54,17 @@ KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("ef_apply", True): ("rank_stream_kernel<4, false, 8, 2>", 2)}
 
 
+# --state-dtype bf16 (the speedrun's bf16 momentum and Q, SURVEY 8c case viii): eager EF,
+# bytes per element A: G 2 + M 2 + M 2, B: M 2, EF + weight update in one pass: M 4 + W 8
+BYTES_PER_ELEM_BF16 = {"project_p": 6.0, "project_r": 2.0, "ef_apply": 12.0}
+KERNEL_OF_BF16 = {("project_p", False): ("b16_proj_kernel<false, 4, 2>", 1),
+                  ("project_p", True): ("b16_proj_kernel<true, 4, 2>", 1),
+                  ("project_r", False): ("b16_proj_kernel<true, 4, 0>", 1),
+                  ("project_r", True): ("b16_proj_kernel<false, 4, 0>", 1),
+                  ("ef_apply", False): ("b16_update_kernel<2>", 1),
+                  ("ef_apply", True): ("b16_update_kernel<2>", 1)}
+
+
 class TimedCodec:
     """Wraps the HIP codec; records HIP events around each call on the stream it launches on."""
 
@@ -139,7 +150,7 @@ def cpu_baseline(sample_layers=1, steps=1):
                       f"r=64, best of {steps} step(s), {best:.2f} s, torch CPU fp32 with {cores} threads"}
 
 
-def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps, deferred):
+def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps, deferred, step_bpe=None):
     """`roofline` of the dominant kernel (most probe time) + every kernel's rate + the step-level view."""
     dominant = max(per_kernel, key=lambda k: per_kernel[k]["ms"])
     d = per_kernel[dominant]
@@ -149,7 +160,7 @@ def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps, deferred):
     traffic = load_pmc_traffic(dominant)
     # the schedule's own bytes: 30 B/elem eager, 22 B/elem with the deferred error feedback
     # (the EF's M read + write rides on pass A)
-    step_bytes = (22.0 if deferred else 30.0) * elems
+    step_bytes = (step_bpe if step_bpe is not None else (22.0 if deferred else 30.0)) * elems
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else round(traffic),
@@ -232,6 +243,8 @@ def main():
                     help="collective backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     ap.add_argument("--eager-ef", action="store_true",
                     help="apply each step's error feedback in its own pass (default: deferred into the next pass A)")
+    ap.add_argument("--state-dtype", default="f32", choices=("f32", "bf16"),
+                    help="momentum/Q dtype; bf16 = the speedrun's mixed precision (eager EF, not the bench line)")
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="time the W-rank batch schedule on one GPU with loopback collectives (not a bench line)")
     args = ap.parse_args()
@@ -264,9 +277,16 @@ def main():
         w.main_grad = torch.empty(m, n, device=dev).normal_(0.0, 1e-3).to(torch.bfloat16)
         named.append((name, w))
     codec = TimedCodec(HipDionCodec(dev))
+    bf16_state = args.state_dtype == "bf16"
+    if bf16_state:
+        global BYTES_PER_ELEM, KERNEL_OF
+        BYTES_PER_ELEM, KERNEL_OF = BYTES_PER_ELEM_BF16, KERNEL_OF_BF16
+        args.eager_ef = True  # no deferred-EF pass A for a bf16 momentum
+    mpc = mda.DionMixedPrecisionConfig(momentum_dtype=torch.bfloat16, q_dtype=torch.bfloat16) if bf16_state else None
     opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=1 / 64,
                            codec=codec, local_streams=args.streams, defer_error_feedback=not args.eager_ef,
-                           coalesce_max_entries=args.coalesce, pipeline_lookahead=args.lookahead)
+                           coalesce_max_entries=args.coalesce, pipeline_lookahead=args.lookahead,
+                           mixed_precision_config=mpc)
     if args.simulate_world > 1:
         group = install_loopback(args.simulate_world)
     attach_dp_routing(opt, named, replicate_group=group)
@@ -315,17 +335,20 @@ def main():
         agg["launches"] += v["calls"] * launches_per_call
     roofline = None
     if per_kernel:
-        roofline = kernel_roofline(per_kernel, elems, ms_per_step, args.probe_steps, not args.eager_ef)
+        roofline = kernel_roofline(per_kernel, elems, ms_per_step, args.probe_steps, not args.eager_ef,
+                                   step_bpe=20.0 if bf16_state else None)
 
     out = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
            "data": "synthetic (random-init Llama-3-8B 2D weight shapes, bf16 grads N(0,1e-3^2))",
            "config": {"workload": "llama3-8b-2d-grad-set-r64", "matrices": len(shapes), "grad_elements": elems,
-                      "rank": 64, "grad_dtype": "bf16", "state_dtype": "f32",
+                      "rank": 64, "grad_dtype": "bf16", "state_dtype": args.state_dtype,
                       "error_feedback": "eager" if args.eager_ef else "deferred (applied in the next step's pass A)",
                       "parallelism": f"dp{world} (replicate, low-rank P/R exchange)" if world > 1 else "dp1"},
            "roofline": roofline}
+    if bf16_state:
+        out["dtype"] = "bf16 state (f32 accumulate)"
     if args.simulate_world > 1:
         out["simulated_world"] = args.simulate_world
         out["metric"] = "SIMULATED (loopback collectives, not a bench line): " + METRIC
