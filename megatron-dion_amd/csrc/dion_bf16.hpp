@@ -42,17 +42,19 @@ struct B16ProjArgs {
   uint32_t* nonzero;     // pass A: nonzero flags (may be null)
   int rows, cols, r, rpad, kchunk, nchunk, out_rows;
   int K, Kp;             // contraction length; row stride of the tt panel (multiple of 32)
+  int vec;               // 16-byte X / G accesses allowed (aligned bases, strides multiple of 8)
   long ld_x, ld_g;
 };
 
 // one 8-wide bf16 run of X at (row, col..col+7), optionally accumulated with G
-// (rne(x + rne(g)), written back), bounds-checked per element at the edges
+// (rne(x + rne(g)), written back); 16-byte accesses when `a.vec` (aligned bases,
+// row strides multiple of 8), per-element bounds checks at the ragged edges
 template <int GDT>
 __device__ __forceinline__ bf16x8s b16_xload(const B16ProjArgs& a, int b, int row, int col, uint32_t& nz) {
   bf16x8s v = {0, 0, 0, 0, 0, 0, 0, 0};
   if (row >= a.rows || col >= a.cols) return v;
   uint16_t* px = a.x[b] + static_cast<long>(row) * a.ld_x + col;
-  const bool full = (col + 8 <= a.cols) && ((reinterpret_cast<uintptr_t>(px) & 15u) == 0);
+  const bool full = a.vec && (col + 8 <= a.cols);
   uint16_t e[8];
   if (full) {
     const uint4 w = *reinterpret_cast<const uint4*>(px);
@@ -63,16 +65,38 @@ __device__ __forceinline__ bf16x8s b16_xload(const B16ProjArgs& a, int b, int ro
     for (int i = 0; i < 8; ++i) e[i] = (col + i < a.cols) ? px[i] : 0;
   }
   if constexpr (GDT != DION_DTYPE_NONE) {
+    float gv[8];
+    const long go = static_cast<long>(row) * a.ld_g + col;
+    if (full) {
+      if constexpr (GDT == DION_DTYPE_BF16) {
+        const uint4 q = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.g[b]) + go);
+        const uint32_t qq[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (col + i >= a.cols) break;
-      float gv;
-      if constexpr (GDT == DION_DTYPE_BF16)
-        gv = bf16_to_f32(static_cast<const uint16_t*>(a.g[b])[static_cast<long>(row) * a.ld_g + col + i]);
-      else
-        gv = bf16_round(static_cast<const float*>(a.g[b])[static_cast<long>(row) * a.ld_g + col + i]);
-      e[i] = f32_to_bf16_rne(bf16_to_f32(e[i]) + gv);
+        for (int i = 0; i < 4; ++i) {
+          gv[2 * i] = __uint_as_float(qq[i] << 16);
+          gv[2 * i + 1] = __uint_as_float(qq[i] & 0xFFFF0000u);
+        }
+      } else {
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(static_cast<const float*>(a.g[b]) + go);
+        const f32x4 g1 = *reinterpret_cast<const f32x4*>(static_cast<const float*>(a.g[b]) + go + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          gv[i] = bf16_round(g0[i]);
+          gv[4 + i] = bf16_round(g1[i]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        gv[i] = 0.f;
+        if (col + i < a.cols) {
+          if constexpr (GDT == DION_DTYPE_BF16) gv[i] = bf16_to_f32(static_cast<const uint16_t*>(a.g[b])[go + i]);
+          else gv[i] = bf16_round(static_cast<const float*>(a.g[b])[go + i]);
+        }
+      }
     }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = f32_to_bf16_rne(bf16_to_f32(e[i]) + gv[i]);
     if (full) {
       uint4 w;
       w.x = e[0] | (static_cast<uint32_t>(e[1]) << 16); w.y = e[2] | (static_cast<uint32_t>(e[3]) << 16);
@@ -86,7 +110,7 @@ __device__ __forceinline__ bf16x8s b16_xload(const B16ProjArgs& a, int b, int ro
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    nz |= e[i] & 0x7FFFu;
+    nz |= (col + i < a.cols) ? (e[i] & 0x7FFFu) : 0u;
     v[i] = static_cast<short>(e[i]);
   }
   return v;
@@ -97,61 +121,77 @@ __device__ __forceinline__ bf16x8s b16_tload(const uint16_t* tt, int Kp, int c, 
   return *reinterpret_cast<const bf16x8s*>(tt + static_cast<long>(c) * Kp + k);
 }
 
+constexpr int kB16RW = 4;                // 16-row output blocks per wave
+constexpr int kB16BO = 64 * kB16RW;      // output rows per block (4 waves)
+
 // out = X T (row mode: out_rows = rows, K = cols) or X^T T (column mode:
-// out_rows = cols, K = rows).  Block = 4 waves = 64 output rows, blockIdx.y =
-// K-chunk, blockIdx.z = matrix.  Row mode reads its MFMA A operand straight
-// from X (8 consecutive columns per lane); column mode stages a 32 x 64 tile of
-// X through LDS (128-byte row segments in, one column per lane out).
+// out_rows = cols, K = rows).  Block = 4 waves x 4 x 16 output rows, blockIdx.y =
+// K-chunk, blockIdx.z = matrix; each K-step's thin-operand run is loaded once per
+// wave and reused by its 4 row blocks.  Row mode reads its MFMA A operand straight
+// from X (8 consecutive columns per lane); column mode stages a 32 x 256 tile of X
+// through LDS (512-byte row segments in, one column per lane out).
 template <bool COL, int RB, int GDT>
 __global__ void __launch_bounds__(256) b16_proj_kernel(const B16ProjArgs a) {
-  __shared__ uint16_t tile[COL ? 32 : 1][COL ? 72 : 1];
+  constexpr int RW = kB16RW, BO = kB16BO;
+  __shared__ uint16_t tile[COL ? 32 : 1][COL ? BO + 8 : 1];
   const int b = blockIdx.z, kc = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int t = lane & 15, g = lane >> 4;
-  const int o0 = blockIdx.x * 64 + wave * 16;  // first output row of this wave
+  const int o0 = blockIdx.x * BO + wave * 16 * RW;  // first output row of this wave
   const int k_begin = kc * a.kchunk;
   const int k_end = min(a.K, k_begin + a.kchunk);
   const uint16_t* tt = a.tt + static_cast<long>(b) * a.rpad * a.Kp;
-  f32x4 acc[RB];
+  f32x4 acc[RW][RB];
 #pragma unroll
-  for (int cb = 0; cb < RB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int rw = 0; rw < RW; ++rw)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[rw][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
   uint32_t nz = 0;
   for (int k0 = k_begin; k0 < k_end; k0 += 32) {
-    bf16x8s A;
+    bf16x8s A[RW];
     if constexpr (!COL) {
       // chunk bounds are multiples of 32, so an 8-run never straddles two chunks
       // (each element is accumulated by exactly one block)
-      A = bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
-      if (k0 + 8 * g < k_end) A = b16_xload<GDT>(a, b, o0 + t, k0 + 8 * g, nz);
-    } else {
-      // tile rows = X rows k0 .. k0+31, tile columns = X columns blockIdx.x*64 .. +63
-      const int tr = tid >> 3, tc = (tid & 7) * 8;
-      uint32_t nzt = 0;
-      bf16x8s v = bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
-      if (k0 + tr < k_end) v = b16_xload<GDT>(a, b, k0 + tr, blockIdx.x * 64 + tc, nzt);
-      nz |= nzt;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) tile[tr][tc + i] = static_cast<uint16_t>(v[i]);
+      for (int rw = 0; rw < RW; ++rw) {
+        A[rw] = bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+        if (k0 + 8 * g < k_end) A[rw] = b16_xload<GDT>(a, b, o0 + 16 * rw + t, k0 + 8 * g, nz);
+      }
+    } else {
+      // tile rows = X rows k0 .. k0+31, tile columns = X columns blockIdx.x*BO .. +BO-1
+#pragma unroll
+      for (int it = 0; it < (32 * BO / 8) / 256; ++it) {
+        const int chunk = tid + 256 * it;
+        const int tr = chunk / (BO / 8), tc = (chunk % (BO / 8)) * 8;
+        bf16x8s v = bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+        if (k0 + tr < k_end) v = b16_xload<GDT>(a, b, k0 + tr, blockIdx.x * BO + tc, nz);
+        *reinterpret_cast<bf16x8s*>(&tile[tr][tc]) = v;
+      }
       __syncthreads();
 #pragma unroll
-      for (int i = 0; i < 8; ++i) A[i] = static_cast<short>(tile[8 * g + i][wave * 16 + t]);
+      for (int rw = 0; rw < RW; ++rw)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) A[rw][i] = static_cast<short>(tile[8 * g + i][wave * 16 * RW + 16 * rw + t]);
       __syncthreads();
     }
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb) {
       const bf16x8s B = (k0 + 8 * g < k_end) ? b16_tload(tt, a.Kp, 16 * cb + t, k0 + 8 * g)
                                              : bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
-      acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B, acc[cb], 0, 0, 0);
+#pragma unroll
+      for (int rw = 0; rw < RW; ++rw) acc[rw][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[rw], B, acc[rw][cb], 0, 0, 0);
     }
   }
   float* out = a.slab + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * a.r;
 #pragma unroll
-  for (int cb = 0; cb < RB; ++cb)
+  for (int rw = 0; rw < RW; ++rw)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int orow = o0 + 4 * g + q, c = 16 * cb + t;
-      if (orow < a.out_rows && c < a.r) out[static_cast<long>(orow) * a.r + c] = acc[cb][q];
-    }
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int orow = o0 + 16 * rw + 4 * g + q, c = 16 * cb + t;
+        if (orow < a.out_rows && c < a.r) out[static_cast<long>(orow) * a.r + c] = acc[rw][cb][q];
+      }
   if (a.nonzero != nullptr && __any(nz != 0u) && lane == 0) atomicOr(&a.nonzero[b], 1u);
 }
 
@@ -212,30 +252,48 @@ struct B16UpdArgs {
   const void* rf_w[MAXB];    // fp32 (P) or bf16 (Qn)
   const void* cf_w[MAXB];
   int rfw_bf16, cfw_bf16;
+  int vec;                   // 8-byte M / 16-byte W runs (cols, strides multiple of 4, aligned bases)
+  int fvec;                  // 16-byte factor loads (r % 8 == 0, aligned factors)
   int rows, cols, r, rows_per_block;
   long ld_m, ld_w;
   float alpha, beta, decay;
 };
 
 template <int KS>
-__device__ __forceinline__ void b16_factor(bf16x8s (&o)[KS], const void* base, bool is_bf16, int row, int nrows, int r,
-                                           int g) {
+__device__ __forceinline__ void b16_factor(bf16x8s (&o)[KS], const void* base, bool is_bf16, bool vec, int row,
+                                           int nrows, int r, int g) {
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     bf16x8s v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (row < nrows) {
+    const int c0 = 32 * s + 8 * g;
+    if (row < nrows && c0 < r) {
+      const long idx = static_cast<long>(row) * r + c0;
+      if (vec) {  // r % 8 == 0 and 16-byte aligned factors: one or two 16-byte loads
+        if (is_bf16) {
+          v = *reinterpret_cast<const bf16x8s*>(static_cast<const uint16_t*>(base) + idx);
+        } else {
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(static_cast<const float*>(base) + idx);
+          const f32x4 x1 = *reinterpret_cast<const f32x4*>(static_cast<const float*>(base) + idx + 4);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = 32 * s + 8 * g + e;
-        if (c < r) {
-          const long idx = static_cast<long>(row) * r + c;
-          v[e] = static_cast<short>(is_bf16 ? static_cast<const uint16_t*>(base)[idx]
-                                            : f32_to_bf16_rne(static_cast<const float*>(base)[idx]));
+          for (int e = 0; e < 4; ++e) {
+            v[e] = static_cast<short>(f32_to_bf16_rne(x0[e]));
+            v[4 + e] = static_cast<short>(f32_to_bf16_rne(x1[e]));
+          }
         }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (c0 + e < r)
+            v[e] = static_cast<short>(is_bf16 ? static_cast<const uint16_t*>(base)[idx + e]
+                                              : f32_to_bf16_rne(static_cast<const float*>(base)[idx + e]));
       }
     }
     o[s] = v;
   }
+}
+
+__device__ __forceinline__ uint16_t b16_ef(uint16_t m, float u, float alpha) {
+  return f32_to_bf16_rne(bf16_to_f32(m) + bf16_round(alpha * bf16_round(u)));
 }
 
 template <int KS>
@@ -248,18 +306,63 @@ __global__ void __launch_bounds__(256) b16_update_kernel(const B16UpdArgs a) {
   const int i_end = min(a.rows, i_begin + a.rows_per_block);
   uint16_t* M = a.m[b];
   float* W = a.w[b];
+  const bool fvec = a.fvec != 0;
   // column factors of this wave's 64 columns: 4 blocks of 16 columns, operand rows j = j0 + 16 jb + t
   bf16x8s cu[4][KS], cw[4][KS];
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb) {
-    if (M) b16_factor<KS>(cu[jb], a.cf_u[b], false, j0 + 16 * jb + t, a.cols, a.r, g);
-    if (W) b16_factor<KS>(cw[jb], a.cf_w[b], a.cfw_bf16 != 0, j0 + 16 * jb + t, a.cols, a.r, g);
+    if (M) b16_factor<KS>(cu[jb], a.cf_u[b], false, fvec, j0 + 16 * jb + t, a.cols, a.r, g);
+    if (W) b16_factor<KS>(cw[jb], a.cf_w[b], a.cfw_bf16 != 0, fvec, j0 + 16 * jb + t, a.cols, a.r, g);
   }
   for (int i0 = i_begin; i0 < i_end; i0 += 16) {
     const int i = i0 + t;  // the storage row of this lane's accumulator column
+    const bool row_ok = i < i_end;
     bf16x8s ru[KS], rw[KS];
-    if (M) b16_factor<KS>(ru, a.rf_u[b], false, i, a.rows, a.r, g);
-    if (W) b16_factor<KS>(rw, a.rf_w[b], a.rfw_bf16 != 0, i, a.rows, a.r, g);
+    if (M) b16_factor<KS>(ru, a.rf_u[b], false, fvec, i, a.rows, a.r, g);
+    if (W) b16_factor<KS>(rw, a.rf_w[b], a.rfw_bf16 != 0, fvec, i, a.rows, a.r, g);
+    if (a.vec) {
+      // cols % 4 == 0: a lane's four columns are one 8-byte M run and one 16-byte W run;
+      // all loads of the step are issued before the products
+      uint2 mv[4];
+      f32x4 wv[4];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const int j = j0 + 16 * jb + 4 * g;
+        const bool ok = row_ok && j < a.cols;
+        if (M) mv[jb] = ok ? *reinterpret_cast<const uint2*>(M + static_cast<long>(i) * a.ld_m + j) : uint2{0u, 0u};
+        if (W) wv[jb] = ok ? *reinterpret_cast<const f32x4*>(W + static_cast<long>(i) * a.ld_w + j)
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const int j = j0 + 16 * jb + 4 * g;
+        const bool ok = row_ok && j < a.cols;
+        if (M) {
+          f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < KS; ++s) u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cu[jb][s], ru[s], u, 0, 0, 0);
+          if (ok) {
+            const uint32_t lo = b16_ef(mv[jb].x & 0xFFFFu, u[0], a.alpha) |
+                                (static_cast<uint32_t>(b16_ef(mv[jb].x >> 16, u[1], a.alpha)) << 16);
+            const uint32_t hi = b16_ef(mv[jb].y & 0xFFFFu, u[2], a.alpha) |
+                                (static_cast<uint32_t>(b16_ef(mv[jb].y >> 16, u[3], a.alpha)) << 16);
+            *reinterpret_cast<uint2*>(M + static_cast<long>(i) * a.ld_m + j) = uint2{lo, hi};
+          }
+        }
+        if (W) {
+          f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < KS; ++s) d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[jb][s], rw[s], d, 0, 0, 0);
+          if (ok) {
+            f32x4 w = wv[jb];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[q] = fmaf(a.beta, bf16_round(d[q]), w[q] * a.decay);
+            *reinterpret_cast<f32x4*>(W + static_cast<long>(i) * a.ld_w + j) = w;
+          }
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb) {
       const int j = j0 + 16 * jb + 4 * g;  // first of this lane's four columns
@@ -267,21 +370,18 @@ __global__ void __launch_bounds__(256) b16_update_kernel(const B16UpdArgs a) {
         f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KS; ++s) u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cu[jb][s], ru[s], u, 0, 0, 0);
-        if (i < i_end) {
+        if (row_ok) {
           uint16_t* pm = M + static_cast<long>(i) * a.ld_m + j;
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            if (j + q < a.cols) {
-              const float upd = bf16_round(a.alpha * bf16_round(u[q]));
-              pm[q] = f32_to_bf16_rne(bf16_to_f32(pm[q]) + upd);
-            }
+            if (j + q < a.cols) pm[q] = b16_ef(pm[q], u[q], a.alpha);
         }
       }
       if (W) {
         f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KS; ++s) d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[jb][s], rw[s], d, 0, 0, 0);
-        if (i < i_end) {
+        if (row_ok) {
           float* pw = W + static_cast<long>(i) * a.ld_w + j;
 #pragma unroll
           for (int q = 0; q < 4; ++q)
@@ -295,14 +395,13 @@ __global__ void __launch_bounds__(256) b16_update_kernel(const B16UpdArgs a) {
 // ----------------------------------------------------------------------------- host side
 namespace b16 {
 
-constexpr int kBlockRows = 64;
 
 int rpad_of(int r) { return (r + 15) / 16 * 16; }
 long kpad_of(int K) { return (K + 31) / 32 * 32; }
 
 Geo geo(int out_rows, int K, int batch) {
   Geo g;
-  g.gx = static_cast<int>(ceil_div(out_rows, kBlockRows));
+  g.gx = static_cast<int>(ceil_div(out_rows, kB16BO));
   long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
   long maxc = ceil_div(K, 256);
   long nc = want < maxc ? want : maxc;
@@ -371,6 +470,13 @@ int project(bool row_mode, int m, int n, int r, int nb, const void* const* G, in
   a.Kp = static_cast<int>(Kp);
   a.ld_x = ld_x;
   a.ld_g = ld_g;
+  {
+    bool vec = ld_x % 8 == 0 && (gdt == DION_DTYPE_NONE || ld_g % 8 == 0);
+    for (int b = 0; b < nb && vec; ++b)
+      vec = (reinterpret_cast<uintptr_t>(X[b]) & 15u) == 0 &&
+            (gdt == DION_DTYPE_NONE || (reinterpret_cast<uintptr_t>(G[b]) & 15u) == 0);
+    a.vec = vec ? 1 : 0;
+  }
   const dim3 grid(g.gx, g.nchunk, nb);
   auto launch = [&](auto RBc) {
     constexpr int RB = decltype(RBc)::value;
@@ -433,14 +539,26 @@ int update(const DionBatchDesc* d, uint16_t* const* M, float* const* W, const fl
         a.rf_u[b] = Rb; a.cf_u[b] = Pb; a.rf_w[b] = Qn[b0 + b]; a.cf_w[b] = Pb;
       }
     }
+    a.ld_m = ldv(d->ld_m, d->n);
+    a.ld_w = ldv(d->ld_w, d->n);
+    {
+      bool vec = d->n % 4 == 0 && a.ld_m % 4 == 0 && a.ld_w % 4 == 0;
+      bool fvec = r % 8 == 0;
+      for (int b = 0; b < nb; ++b) {
+        if (a.m[b]) vec = vec && (reinterpret_cast<uintptr_t>(a.m[b]) & 7u) == 0;
+        if (a.w[b]) vec = vec && (reinterpret_cast<uintptr_t>(a.w[b]) & 15u) == 0;
+        for (const void* f : {a.rf_u[b], a.cf_u[b], a.rf_w[b], a.cf_w[b]})
+          fvec = fvec && (reinterpret_cast<uintptr_t>(f) & 15u) == 0;
+      }
+      a.vec = vec ? 1 : 0;
+      a.fvec = fvec ? 1 : 0;
+    }
     a.rfw_bf16 = d->transposed ? 1 : 0;
     a.cfw_bf16 = d->transposed ? 0 : 1;
     a.rows = d->m;
     a.cols = d->n;
     a.r = r;
     a.rows_per_block = 256;
-    a.ld_m = ldv(d->ld_m, d->n);
-    a.ld_w = ldv(d->ld_w, d->n);
     a.alpha = alpha;
     a.beta = beta;
     a.decay = decay;
