@@ -2786,6 +2786,11 @@ __device__ __forceinline__ void cpx_compute(const ColStepX6<CT>& S, f32x4 (&acc)
 template <int RB>
 constexpr int colx6_ct() { return RB >= 4 ? 2 : 4; }
 
+#ifndef DION_COLX6_PD
+#define DION_COLX6_PD 2
+#endif
+constexpr int kColX6PD = DION_COLX6_PD;  // register-ring depth of the pass-B column kernel (tuning knob)
+
 template <int RB, int NW>
 __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : (NW >= 8 ? DION_COLX6_MINB : 2)) colproj_x6_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
@@ -2811,36 +2816,34 @@ __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : (NW >= 8 ? DION_COLX6_M
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  ColStepX6<CT> SA, SB;
   constexpr int NQ = RB * 3 * 64;
   const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
   SplitCopyN<NQ, 64 * NW> TA;
-  cpx_load<CT>(SA, M, a.ld_m, i_begin);
+  // M arrives PD - 1 K-steps ahead in a register ring (bytes in flight per wave =
+  // (PD - 1) x 32 rows x 16 CT columns x 4 B); the split thin operand one step ahead
+  constexpr int PD = kColX6PD;
+  ColStepX6<CT> S[PD];
+#pragma unroll
+  for (int k = 0; k < PD - 1; ++k)
+    if (i_begin + 32 * k < i_end) cpx_load<CT>(S[k], M, a.ld_m, i_begin + 32 * k);
   split_copy_load_n(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
   split_copy_store_n(TA, tq[0], tid);
   __syncthreads();
   int cur = 0;
-  for (int i0 = i_begin; i0 < i_end; i0 += 64) {
-    const bool more = i0 + 32 < i_end;
-    if (more) {
-      cpx_load<CT>(SB, M, a.ld_m, i0 + 32);
-      split_copy_load_n(TA, qs + static_cast<long>(i0 / 32 + 1) * NQ, tid);
+  for (int i0 = i_begin; i0 < i_end; i0 += 32 * PD) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      const int i = i0 + 32 * k;
+      if (i >= i_end) break;
+      const bool more = i + 32 < i_end;
+      if (i + 32 * (PD - 1) < i_end) cpx_load<CT>(S[(k + PD - 1) % PD], M, a.ld_m, i + 32 * (PD - 1));
+      if (more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
+      cpx_compute<RB, CT>(S[k], acc, tq[cur], lane);
+      if (!more) break;
+      split_copy_store_n(TA, tq[cur ^ 1], tid);
+      __syncthreads();
+      cur ^= 1;
     }
-    cpx_compute<RB, CT>(SA, acc, tq[cur], lane);
-    if (!more) break;
-    split_copy_store_n(TA, tq[cur ^ 1], tid);
-    __syncthreads();
-    cur ^= 1;
-    const bool more2 = i0 + 64 < i_end;
-    if (more2) {
-      cpx_load<CT>(SA, M, a.ld_m, i0 + 64);
-      split_copy_load_n(TA, qs + static_cast<long>(i0 / 32 + 2) * NQ, tid);
-    }
-    cpx_compute<RB, CT>(SB, acc, tq[cur], lane);
-    if (!more2) break;
-    split_copy_store_n(TA, tq[cur ^ 1], tid);
-    __syncthreads();
-    cur ^= 1;
   }
 
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
