@@ -41,7 +41,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 5
+#define DION_ABI_VERSION 6
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -60,6 +60,7 @@ typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 #define DION_OP_FIXUP_COLNORM 4
 #define DION_OP_PROJECT_P_EF 5 /* DION_E_UNSUPPORTED: no fused kernel for this shape */
 #define DION_OP_EF_APPLY 6     /* optional: pre-split P for the rank-update kernels   */
+#define DION_OP_GRAD_SUM_SQ 7  /* dion_grad_sum_sq (only batch, m, n, g_dtype, ld_g used) */
 
 typedef struct DionBatchDesc {
   int32_t batch;      /* matrices in this call (all the same shape)            */
@@ -172,6 +173,17 @@ int dion_ef_apply(const DionBatchDesc* desc, float* const* M, float* const* W,
  * runtime.py:1428-1434 reduce-scatter, :1485-1491 all-reduce).
  */
 int dion_round_bf16(float* x, int64_t n, dion_stream_t stream);
+
+/*
+ * *out += sum_b sum_ij G_b[i][j]^2, in fp64 (every square exact, fixed summation
+ * order: bitwise reproducible).  The Dion term of the gradient norm that gradient
+ * clipping needs before the step: replaces distrib_dion/grad_norm.py:54-68
+ * (_grad_sum_sq_fp64) as used by _dion_grad_norm_sq (:144-258).  `out` is one
+ * device double the caller zeroes; only batch, m, n, g_dtype (_F32 / _BF16) and
+ * ld_g of `desc` are read.  Scratch: dion_workspace_bytes(desc, DION_OP_GRAD_SUM_SQ).
+ */
+int dion_grad_sum_sq(const DionBatchDesc* desc, const void* const* G, double* out, void* ws,
+                     size_t ws_bytes, dion_stream_t stream);
 
 #ifdef __cplusplus
 }

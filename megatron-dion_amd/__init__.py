@@ -28,6 +28,7 @@ from .kernels import scaled_lr_for_shape  # noqa: F401
 from .batches import build_dion_batches  # noqa: F401
 from .runtime import AsyncRuntime, batch_dion_update_async  # noqa: F401
 from .optimizer import MegatronDion  # noqa: F401
+from .grad_norm import dion_grad_norm, dion_grad_norm_sq  # noqa: F401
 
 __all__ = [
     "MegatronDion",
@@ -49,4 +50,6 @@ __all__ = [
     "is_transposed_shape",
     "q_seed_from_param_key",
     "init_dion_state",
+    "dion_grad_norm_sq",
+    "dion_grad_norm",
 ]

@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # DION_LIB_PATH: load another build of the same ABI (kernel-variant A/B runs during tuning)
 LIB_PATH = os.environ.get("DION_LIB_PATH") or os.path.join(HERE, "csrc", "libdion_codec.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -30,6 +30,7 @@ OP_PROJECT_R = 3
 OP_FIXUP_COLNORM = 4
 OP_PROJECT_P_EF = 5
 OP_EF_APPLY = 6
+OP_GRAD_SUM_SQ = 7
 
 # every symbol include/dion_codec.h declares
 EXPORTED = (
@@ -43,6 +44,7 @@ EXPORTED = (
     "dion_fixup_colnorm",
     "dion_ef_apply",
     "dion_round_bf16",
+    "dion_grad_sum_sq",
 )
 
 
@@ -89,6 +91,7 @@ _SIGNATURES = {
     "dion_ef_apply": ([_DESC, _PP, _PP, _P, _P, _PP, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                        ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_round_bf16": ([_P, ctypes.c_int64, _P], ctypes.c_int),
+    "dion_grad_sum_sq": ([_DESC, _PP, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
 }
 
 _lib = None

@@ -253,3 +253,25 @@ class HipDionCodec:
         if X.dtype != torch.float32 or not X.is_contiguous():
             raise RuntimeError(f"[DION_BAD_FACTOR] round_bf16 needs a contiguous fp32 buffer, got {X.dtype}")
         _lib.check(self.lib.dion_round_bf16(X.data_ptr(), X.numel(), self._stream()), "dion_round_bf16")
+
+    def grad_sum_sq(self, grads: Sequence[torch.Tensor], out: torch.Tensor) -> None:
+        """out (fp64, (1,)) += sum of squares of every gradient (grad_norm.py:54-68, :144-258)."""
+        if out.dtype != torch.float64 or out.numel() != 1 or out.device != self.device:
+            raise RuntimeError("[DION_BAD_NORM_OUT] out must be one float64 on the codec's device")
+        groups = {}
+        for g in grads:
+            if g.dim() != 2 or g.stride(1) != 1:
+                raise RuntimeError(f"[DION_NON_ROW_MAJOR] grad shape={tuple(g.shape)} stride={g.stride()}")
+            groups.setdefault((tuple(g.shape), g.dtype, g.stride(0)), []).append(g)
+        for (shape, _, _), members in groups.items():
+            d = _lib.DionBatchDesc()
+            d.batch = len(members)
+            d.m, d.n, d.r = int(shape[0]), int(shape[1]), 1
+            d.g_dtype = _dtype_code(members[0])
+            d.m_dtype = d.w_dtype = _lib.DTYPE_F32
+            d.ld_g = _row_stride(members[0])
+            ws = self.workspace(d, _lib.OP_GRAD_SUM_SQ)
+            rc = self.lib.dion_grad_sum_sq(ctypes.byref(d), _ptrs(members), out.data_ptr(), ws.data_ptr(),
+                                           ws.numel(), self._stream())
+            _lib.check(rc, "dion_grad_sum_sq")
+

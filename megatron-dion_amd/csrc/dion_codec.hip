@@ -3306,6 +3306,19 @@ size_t qr_lds_bytes(int K, int r) { return sizeof(float) * (static_cast<size_t>(
 // C ABI
 // ============================================================================
 #include "dion_bf16.hpp"
+#include "dion_gradnorm.hpp"
+
+namespace {
+int validate_grads(const DionBatchDesc* d) {
+  if (d == nullptr) return fail(DION_E_INVALID, "desc is null");
+  if (d->batch < 0) return fail(DION_E_INVALID, "batch=%d", d->batch);
+  if (d->m <= 0 || d->n <= 0) return fail(DION_E_INVALID, "bad shape m=%d n=%d", d->m, d->n);
+  if (d->g_dtype != DION_DTYPE_F32 && d->g_dtype != DION_DTYPE_BF16)
+    return fail(DION_E_UNSUPPORTED, "grad dtype %d", d->g_dtype);
+  if (d->ld_g != 0 && d->ld_g < d->n) return fail(DION_E_INVALID, "ld_g=%lld < n=%d", static_cast<long long>(d->ld_g), d->n);
+  return DION_OK;
+}
+}  // namespace
 
 extern "C" {
 
@@ -3314,6 +3327,13 @@ int dion_abi_version(void) { return DION_ABI_VERSION; }
 const char* dion_last_error(void) { return g_err; }
 
 int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
+  if (op == DION_OP_GRAD_SUM_SQ) {
+    const int rcg = validate_grads(d);
+    if (rcg != DION_OK) return rcg;
+    if (bytes == nullptr) return fail(DION_E_INVALID, "bytes is null");
+    *bytes = gnorm::ws_bytes(d->m, d->batch);
+    return DION_OK;
+  }
   int rc = validate(d);
   if (rc != DION_OK) return rc;
   if (bytes == nullptr) return fail(DION_E_INVALID, "bytes is null");
@@ -3875,6 +3895,14 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
 int dion_round_bf16(float* x, int64_t n, dion_stream_t stream) {
   if (n < 0 || (n > 0 && x == nullptr)) return fail(DION_E_INVALID, "bad buffer (n=%lld)", static_cast<long long>(n));
   return b16::round_buffer(x, static_cast<long>(n), reinterpret_cast<hipStream_t>(stream));
+}
+
+int dion_grad_sum_sq(const DionBatchDesc* d, const void* const* G, double* out, void* ws, size_t ws_bytes,
+                     dion_stream_t stream) {
+  int rc = validate_grads(d);
+  if (rc != DION_OK) return rc;
+  if (out == nullptr || (d->batch > 0 && G == nullptr)) return fail(DION_E_INVALID, "null argument");
+  return gnorm::run(d, G, out, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

@@ -46,6 +46,7 @@ __all__ = [
     "DionHyper",
     "dion_batch_step_local",
     "dion_batch_step_replicated",
+    "grad_sum_sq_fp64",
 ]
 
 
@@ -339,6 +340,20 @@ def dion_step_replicated(batches, hyper: DionHyper, sketch_fn=None,
     gens = (_replicated_batch_gen(per_rank, real, hyper, sketch_fn, buffers)
             for per_rank, real in batches)
     run_async_runtime(gens, max_concurrent=max_concurrent)
+
+
+def grad_sum_sq_fp64(tensors, chunk_bytes: int = 128 * 1024 * 1024) -> torch.Tensor:
+    """distrib_dion/grad_norm.py:54-68 (_grad_sum_sq_fp64), summed over `tensors`
+    like _dion_grad_norm_sq (:166-172): chunked cast to fp64, square, sum."""
+    total = torch.zeros(1, dtype=torch.float64)
+    for t in tensors:
+        flat = t.detach().reshape(-1)
+        step = max(1, int(chunk_bytes) // 8)
+        for start in range(0, flat.numel(), step):
+            chunk = flat[start:start + step].to(torch.float64)
+            chunk.mul_(chunk)
+            total += chunk.sum()
+    return total
 
 
 def dion_batch_step_replicated(per_rank, real, hyper, sketch_fn=None) -> None:

@@ -75,3 +75,7 @@ class OracleCodec:
                     W.mul_(1 - lr * wd)
                 delta = (qs[b] @ Pb.mT) if transposed else (Pb @ qs[b].mT)
                 W.add_(delta.to(W.dtype), alpha=-scaled_lr)
+
+    def grad_sum_sq(self, grads, out):
+        out += O.grad_sum_sq_fp64(grads).to(out.device)
+
