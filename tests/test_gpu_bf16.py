@@ -23,6 +23,8 @@ max |a - b| / max |b|:
   W                   <= 1e-3
   Q (bf16, unit columns) <= 2e-2
 """
+import math
+
 import pytest
 import torch
 
@@ -183,3 +185,57 @@ def test_bf16_round_kernel_is_rne():
     opt.codec.round_bf16(y)
     torch.cuda.synchronize()
     assert torch.equal(y.cpu().view(torch.int32), ref.view(torch.int32))
+
+
+@pytest.mark.parametrize("m,n", [(28672, 4096), (4096, 14336)])
+def test_bf16_llama_shape_properties(m, n):
+    """Full Llama-3-8B fc1 / fc2 matrices at r = 64 in the bf16 state mode, through the C ABI:
+    exact rounding identities where the kernel's output is determined elementwise
+    (M += G, bf16-valued factors), Freivalds probes for the products, orthonormal P."""
+    from megatron_dion_amd.codec import HipDionCodec
+
+    dev = _dev()
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.manual_seed(12)
+    r = 64
+    transposed = m < n
+    mp, nq = (n, m) if transposed else (m, n)
+    codec = HipDionCodec(dev)
+    M = (torch.randn(m, n, device=dev) * 1e-3).to(torch.bfloat16)
+    G = (torch.randn(m, n, device=dev) * 1e-3).to(torch.bfloat16)
+    W = torch.randn(m, n, device=dev) * 0.02
+    Q = torch.randn(nq, r, device=dev).to(torch.bfloat16)
+    X0 = (M.float() + G.float()).to(torch.bfloat16)            # runtime.py:1560-1566 in bf16
+    W0 = W.clone()
+    P = torch.zeros(1, mp, r, device=dev)
+    nz = torch.zeros(1, dtype=torch.int32, device=dev)
+    codec.project_p([G], [M], [Q], P, nz, transposed)
+    torch.cuda.synchronize()
+    assert torch.equal(M, X0) and int(nz[0]) == 1
+    assert torch.equal(P, P.to(torch.bfloat16).float())
+    Xo = (X0.t() if transposed else X0).double()
+    v = torch.randn(r, 1, device=dev, dtype=torch.float64)
+    assert maxrel(P[0].double() @ v, Xo @ (Q.double() @ v)) <= 1e-2
+    codec.orthonormalize(P, m, n, transposed, seed=99, state_dtype=torch.bfloat16)
+    assert torch.equal(P, P.to(torch.bfloat16).float())
+    I = P[0].double().t() @ P[0].double()
+    assert (I - torch.eye(r, device=dev, dtype=torch.float64)).abs().max().item() <= 2e-2
+    R = torch.zeros(1, nq, r, device=dev)
+    codec.project_r([M], P, R, transposed)
+    assert torch.equal(R, R.to(torch.bfloat16).float())
+    assert maxrel(R[0].double() @ v, Xo.t() @ (P[0].double() @ v)) <= 1e-2
+    Qs = [Q]
+    codec.fixup_colnorm(P, R, Qs, nz, 1e-8, m, n, transposed)
+    qn_ref = (R[0] / (R[0].square().sum(dim=0, keepdim=True).sqrt() + 1e-8)).to(torch.bfloat16)
+    assert maxrel(Q.float(), qn_ref.float()) <= 2 ** -7
+    Pb, Rb = P[0].to(torch.bfloat16).float(), R[0]
+    s = 0.01 * 0.2 * math.sqrt(max(m, n))
+    codec.ef_apply([M], [W], P, R, Qs, nz, 0.95, 0.01, 0.01, s, transposed)
+    torch.cuda.synchronize()
+    upd = (Rb @ Pb.t()) if transposed else (Pb @ Rb.t())        # kernels.py:54-83 in bf16
+    upd = (upd.to(torch.bfloat16).float() * -(1.0 - 0.95)).to(torch.bfloat16)
+    m_ref = (X0.float() + upd.float()).to(torch.bfloat16)
+    assert maxrel(M.float(), m_ref.float()) <= 2 ** -7
+    delta = (Q.float() @ Pb.t()) if transposed else (Pb @ Q.float().t())
+    w_ref = W0 * (1 - 0.01 * 0.01) - s * delta.to(torch.bfloat16).float()
+    assert maxrel(W, w_ref) <= 5e-3
