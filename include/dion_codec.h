@@ -41,7 +41,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 6
+#define DION_ABI_VERSION 7
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -184,6 +184,27 @@ int dion_round_bf16(float* x, int64_t n, dion_stream_t stream);
  */
 int dion_grad_sum_sq(const DionBatchDesc* desc, const void* const* G, double* out, void* ws,
                      size_t ws_bytes, dion_stream_t stream);
+
+/*
+ * The elementwise branch of MegatronDion.step (algorithm.py:247-429) for one bucket of
+ * n_tensors same-hyper-parameter tensors: W, exp_avg (first_moment), exp_avg_sq
+ * (second_moment) fp32, G fp32 or bf16 (g_dtype), numels[i] elements each, contiguous.
+ * One read and one write of every tensor replaces the reference's chain of
+ * torch._foreach_* passes:
+ *   AdamW  elementwise_opts.py:45-80:  m = lerp(m, g, 1-b1); v = lerp(v, g*g, 1-b2);
+ *          W = W (1 - lr wd) - (m / (sqrt(v) / sqrt(1-b2^t) + eps)) (lr / (1-b1^t))
+ *   Lion   elementwise_opts.py:83-105: u = sign(lerp(m, g, 1-b1)); m = lerp(m, g, 1-b2);
+ *          W = W (1 - lr wd) - lr u
+ * (the decay multiply only when weight_decay != 0).  Scalars are the reference's
+ * Python doubles; step > 0 for AdamW ([DION_INVALID_ELEMENTWISE_ADAMW_STEP]).
+ */
+int dion_elementwise_adamw(int32_t n_tensors, const int64_t* numels, float* const* W, const void* const* G,
+                           int32_t g_dtype, float* const* exp_avg, float* const* exp_avg_sq, double lr,
+                           double beta1, double beta2, double weight_decay, double eps, int32_t step,
+                           dion_stream_t stream);
+int dion_elementwise_lion(int32_t n_tensors, const int64_t* numels, float* const* W, const void* const* G,
+                          int32_t g_dtype, float* const* exp_avg, double lr, double beta1, double beta2,
+                          double weight_decay, dion_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # DION_LIB_PATH: load another build of the same ABI (kernel-variant A/B runs during tuning)
 LIB_PATH = os.environ.get("DION_LIB_PATH") or os.path.join(HERE, "csrc", "libdion_codec.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -45,6 +45,8 @@ EXPORTED = (
     "dion_ef_apply",
     "dion_round_bf16",
     "dion_grad_sum_sq",
+    "dion_elementwise_adamw",
+    "dion_elementwise_lion",
 )
 
 
@@ -92,6 +94,11 @@ _SIGNATURES = {
                        ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_round_bf16": ([_P, ctypes.c_int64, _P], ctypes.c_int),
     "dion_grad_sum_sq": ([_DESC, _PP, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "dion_elementwise_adamw": ([ctypes.c_int32, _P, _PP, _PP, ctypes.c_int32, _PP, _PP, ctypes.c_double,
+                                ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int32,
+                                _P], ctypes.c_int),
+    "dion_elementwise_lion": ([ctypes.c_int32, _P, _PP, _PP, ctypes.c_int32, _PP, ctypes.c_double, ctypes.c_double,
+                               ctypes.c_double, ctypes.c_double, _P], ctypes.c_int),
 }
 
 _lib = None

@@ -275,3 +275,37 @@ class HipDionCodec:
                                            ws.numel(), self._stream())
             _lib.check(rc, "dion_grad_sum_sq")
 
+    # ------------------------------------------------------------------ elementwise branch
+    def _ew_lists(self, params, grads, moments):
+        for t in list(params) + [m for ms in moments for m in ms]:
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != self.device:
+                raise RuntimeError(f"[DION_ELEMENTWISE_STATE_DTYPE_UNSUPPORTED] {t.dtype} {tuple(t.shape)} {t.device}; "
+                                   "the elementwise kernel takes contiguous fp32 params and moments")
+        by_gdt = {}
+        for i, g in enumerate(grads):
+            if not g.is_contiguous() or g.numel() != params[i].numel():
+                raise RuntimeError(f"[DION_ELEMENTWISE_BAD_GRAD] {tuple(g.shape)} for param {tuple(params[i].shape)}")
+            by_gdt.setdefault(_dtype_code(g), []).append(i)
+        return by_gdt
+
+    def elementwise_adamw(self, params, grads, first_moments, second_moments, *, lr, beta1, beta2, weight_decay,
+                          step, epsilon) -> None:
+        """elementwise_opts.py:45-80 in one multi-tensor pass (dion_elementwise_adamw)."""
+        for gdt, idx in self._ew_lists(params, grads, (first_moments, second_moments)).items():
+            numels = (ctypes.c_int64 * len(idx))(*[int(params[i].numel()) for i in idx])
+            rc = self.lib.dion_elementwise_adamw(
+                len(idx), numels, _ptrs([params[i] for i in idx]), _ptrs([grads[i] for i in idx]), gdt,
+                _ptrs([first_moments[i] for i in idx]), _ptrs([second_moments[i] for i in idx]), float(lr),
+                float(beta1), float(beta2), float(weight_decay), float(epsilon), int(step), self._stream())
+            _lib.check(rc, "dion_elementwise_adamw")
+
+    def elementwise_lion(self, params, grads, first_moments, *, lr, beta1, beta2, weight_decay) -> None:
+        """elementwise_opts.py:83-105 in one multi-tensor pass (dion_elementwise_lion)."""
+        for gdt, idx in self._ew_lists(params, grads, (first_moments,)).items():
+            numels = (ctypes.c_int64 * len(idx))(*[int(params[i].numel()) for i in idx])
+            rc = self.lib.dion_elementwise_lion(
+                len(idx), numels, _ptrs([params[i] for i in idx]), _ptrs([grads[i] for i in idx]), gdt,
+                _ptrs([first_moments[i] for i in idx]), float(lr), float(beta1), float(beta2), float(weight_decay),
+                self._stream())
+            _lib.check(rc, "dion_elementwise_lion")
+

@@ -9,8 +9,10 @@ run the batches through a width-limited AsyncRuntime.  The per-batch work runs
 in HIP kernels (`codec=` backend, default `HipDionCodec`); there is no CPU
 fallback.
 
-Out of scope on this path: the elementwise AdamW/Lion branch for
-non-2D parameters, TP/FS-sharded Dion and split-qkv children.
+The elementwise branch (AdamW / Lion for the ElementwiseStepParam items,
+algorithm.py:247-429) runs after the Dion batches in one multi-tensor HIP launch per
+update contract.  Out of scope on this path: TP/FS-sharded Dion and
+split-qkv children.
 """
 from __future__ import annotations
 
@@ -116,15 +118,68 @@ class MegatronDion(Optimizer):
 
     def _batches(self):
         batches, elementwise = self._route_step_params()
-        if elementwise:
-            raise RuntimeError(
-                "[DION_ELEMENTWISE_UNSUPPORTED] the MI355X codec covers the 2D Dion path only; route "
-                "non-2D parameters to a separate optimizer")
         self._dion_update_count += sum(int(b.real_batch_size) for b in batches)
+        self._elementwise_update_count += len(elementwise)
         if self._coalesce_local:
             batches = coalesce_local_batches(batches, max_entries=self._coalesce_max)
             batches = coalesce_replicated_batches(batches, max_entries=self._coalesce_max)
-        return batches
+        return batches, list(elementwise)
+
+    # ------------------------------------------------------------------ elementwise branch
+    def _apply_elementwise_batches(self, elementwise_params) -> None:
+        """algorithm.py:247-429: group the elementwise items by their update contract
+        (algorithm, group, device, dtypes, lr, wd, eps, betas, step) in first-seen order and
+        run one multi-tensor AdamW / Lion launch per group (elementwise_opts.py)."""
+        default_opt = self.defaults.get("elementwise_optimizer", "adam")
+        default_scale = float(self.defaults.get("elementwise_lr_scale", 1.0))
+        default_betas = self.defaults.get("betas", (0.9, 0.95))
+        default_eps = self.defaults.get("elementwise_eps", 1e-8)
+        mpc = self._mixed_precision_config
+        groups: "OrderedDict[tuple, dict]" = OrderedDict()
+        for item in elementwise_params:
+            p, grad, state, grp = item.param, item.grad, item.optimizer_state, item.optim_group
+            algo = grp.get("algorithm", None)
+            opt_name = grp.get("elementwise_optimizer", default_opt) if algo in (None, "dion") else algo
+            if opt_name == "adam":
+                opt_name = "adamw"
+            if opt_name not in ("adamw", "lion"):
+                raise RuntimeError(f"[DION_INVALID_ELEMENTWISE_OPT] elementwise_optimizer={opt_name}")
+            lr_scale = float(grp.get("elementwise_lr_scale", default_scale))
+            if lr_scale < 0.0:
+                raise RuntimeError(f"[DION_INVALID_ELEMENTWISE_LR_SCALE] elementwise_lr_scale={lr_scale}")
+            lr = float(grp.get("lr", self.defaults["lr"])) * lr_scale
+            wd = float(grp.get("weight_decay", self.defaults["weight_decay"] * grp.get("wd_mult", 1.0)))
+            step = int(grp.get("step", 0))
+            eps = float(grp.get("elementwise_eps", grp.get("eps", grp.get("epsilon", default_eps))))
+            if "betas" in grp:
+                b1, b2 = (float(x) for x in grp["betas"])
+            else:
+                b1 = float(grp.get("beta1", default_betas[0]))
+                b2 = float(grp.get("beta2", default_betas[1]))
+            if step <= 0:
+                raise RuntimeError(f"[DION_INVALID_ELEMENTWISE_STEP] step={step}")
+            m1 = _elementwise_moment(state, p, "first_moment", ("exp_avg", "momentum"), mpc.momentum_dtype)
+            state["step"] = step
+            m2 = None
+            if opt_name == "adamw":
+                m2 = _elementwise_moment(state, p, "second_moment", ("exp_avg_sq", "variance"), mpc.variance_dtype)
+            key = (opt_name, id(grp), str(p.device), str(p.dtype), str(m1.dtype),
+                   str(m2.dtype if m2 is not None else torch.float32), lr, wd, eps, b1, b2, step)
+            g = groups.setdefault(key, dict(opt=opt_name, params=[], grads=[], m1=[], m2=[], lr=lr, wd=wd,
+                                            eps=eps, step=step, b1=b1, b2=b2))
+            g["params"].append(p.data if isinstance(p, torch.nn.Parameter) else p)
+            g["grads"].append(grad)
+            g["m1"].append(m1)
+            if m2 is not None:
+                g["m2"].append(m2)
+        codec = self.codec
+        for g in groups.values():
+            if g["opt"] == "lion":
+                codec.elementwise_lion(g["params"], g["grads"], g["m1"], lr=g["lr"], beta1=g["b1"], beta2=g["b2"],
+                                       weight_decay=g["wd"])
+            else:
+                codec.elementwise_adamw(g["params"], g["grads"], g["m1"], g["m2"], lr=g["lr"], beta1=g["b1"],
+                                        beta2=g["b2"], weight_decay=g["wd"], step=g["step"], epsilon=g["eps"])
 
     def _run_local_overlapped(self, batches, sketches) -> bool:
         """World-size-1 schedule: independent batches alternate over HIP streams, so one
@@ -236,7 +291,7 @@ class MegatronDion(Optimizer):
         t0 = time.perf_counter() if profile else None
         width = 3 if self.max_concurrent_tasks is None else int(self.max_concurrent_tasks)
         sketches = getattr(self, "_sketch_override", None)
-        batches = self._batches()
+        batches, elementwise = self._batches()
         if not (self._run_local_pipelined(batches, sketches) or self._run_local_overlapped(batches, sketches)):
             streams = self._replica_streams(batches, width)
             main = torch.cuda.current_stream(streams[0].device) if streams else None
@@ -246,10 +301,27 @@ class MegatronDion(Optimizer):
                           for b in batches), width, streams=streams).run()
             for s in streams or ():
                 main.wait_stream(s)
+        if elementwise:
+            # runtime.py:314-315: the elementwise task runs after the Dion batches
+            self._apply_elementwise_batches(elementwise)
         if profile:
             torch.cuda.synchronize()
             self._profile_records.append(("step", time.perf_counter() - t0))
         return loss
+
+
+def _elementwise_moment(state, param, key, legacy, dtype):
+    """algorithm.py:295-331: the moment under `key`, migrated from a legacy key or zero-initialised."""
+    if key in state and legacy[0] in state:
+        raise RuntimeError(f"[DION_SCALAR_STATE_LAYOUT_CONFLICT] found both {key} and {legacy[0]}")
+    if key not in state:
+        for old in legacy:
+            if old in state:
+                state[key] = state.pop(old)
+                break
+        else:
+            state[key] = torch.zeros_like(param, dtype=_as_dtype(dtype) or param.dtype)
+    return state[key]
 
 
 def _as_dtype(d):

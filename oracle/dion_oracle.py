@@ -47,6 +47,8 @@ __all__ = [
     "dion_batch_step_local",
     "dion_batch_step_replicated",
     "grad_sum_sq_fp64",
+    "elementwise_adamw",
+    "elementwise_lion",
 ]
 
 
@@ -340,6 +342,39 @@ def dion_step_replicated(batches, hyper: DionHyper, sketch_fn=None,
     gens = (_replicated_batch_gen(per_rank, real, hyper, sketch_fn, buffers)
             for per_rank, real in batches)
     run_async_runtime(gens, max_concurrent=max_concurrent)
+
+
+def elementwise_adamw(params, grads, first_moments, second_moments, *, lr, beta1, beta2, weight_decay,
+                      step, epsilon) -> None:
+    """dion/elementwise_opts.py:45-80 (_adamw_update_foreach_chunk), same foreach chain."""
+    n = len(params)
+    g1 = [g.to(dtype=first_moments[0].dtype) for g in grads]
+    torch._foreach_lerp_(first_moments, g1, [1.0 - beta1] * n)
+    gsq = [g.to(dtype=second_moments[0].dtype) for g in torch._foreach_mul(g1, g1)]
+    torch._foreach_lerp_(second_moments, gsq, [1.0 - beta2] * n)
+    bc1 = 1.0 - beta1 ** step
+    bc2_sqrt = (1.0 - beta2 ** step) ** 0.5
+    denom = torch._foreach_sqrt(second_moments)
+    torch._foreach_div_(denom, bc2_sqrt)
+    torch._foreach_add_(denom, [epsilon] * n)
+    upd = torch._foreach_div(first_moments, denom)
+    torch._foreach_mul_(upd, lr / bc1)
+    if weight_decay != 0.0:
+        torch._foreach_mul_(params, 1.0 - lr * weight_decay)
+    torch._foreach_sub_(params, upd)
+
+
+def elementwise_lion(params, grads, first_moments, *, lr, beta1, beta2, weight_decay) -> None:
+    """dion/elementwise_opts.py:83-105 (_lion_update_foreach_chunk), same foreach chain."""
+    n = len(params)
+    g1 = [g.to(dtype=first_moments[0].dtype) for g in grads]
+    upd = torch._foreach_lerp(first_moments, g1, [1.0 - beta1] * n)
+    torch._foreach_sign_(upd)
+    torch._foreach_lerp_(first_moments, g1, [1.0 - beta2] * n)
+    torch._foreach_mul_(upd, lr)
+    if weight_decay != 0.0:
+        torch._foreach_mul_(params, 1.0 - lr * weight_decay)
+    torch._foreach_sub_(params, upd)
 
 
 def grad_sum_sq_fp64(tensors, chunk_bytes: int = 128 * 1024 * 1024) -> torch.Tensor:

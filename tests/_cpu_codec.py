@@ -79,3 +79,9 @@ class OracleCodec:
     def grad_sum_sq(self, grads, out):
         out += O.grad_sum_sq_fp64(grads).to(out.device)
 
+    def elementwise_adamw(self, params, grads, first_moments, second_moments, **kw):
+        O.elementwise_adamw(params, grads, first_moments, second_moments, **kw)
+
+    def elementwise_lion(self, params, grads, first_moments, **kw):
+        O.elementwise_lion(params, grads, first_moments, **kw)
+

@@ -179,7 +179,7 @@ def _coalesce_worker(rank, world, port, out_dir, deferred):
             gen = torch.Generator().manual_seed(100 * step + 10 * rank + 1)
             for _, p in params:
                 p.grad = (torch.randn(p.shape, generator=gen) * 1e-3).to(torch.bfloat16).float()
-            chunks.append([int(getattr(b, "_chunks", 0) or 0) for b in opt._batches()])
+            chunks.append([int(getattr(b, "_chunks", 0) or 0) for b in opt._batches()[0]])
             opt.step()
         opt.flush_error_feedback()
         runs[coalesce] = {"chunks": chunks,

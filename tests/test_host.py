@@ -25,7 +25,7 @@ def _header_symbols():
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     syms = _header_symbols()
-    assert len(syms) == 11
+    assert len(syms) == 13
     assert sorted(_lib.EXPORTED) == syms
     for s in syms:
         assert getattr(lib, s) is not None
@@ -155,15 +155,23 @@ def test_async_runtime_interleave_matches_reference_emulation():
     assert trace_a == trace_b
 
 
-def test_step_requires_distributed_mode_and_rejects_elementwise():
+def test_step_requires_distributed_mode_and_checks_elementwise_items():
+    from megatron_dion_amd.types import ElementwiseStepParam
     p = torch.nn.Parameter(torch.zeros(8, 8))
-    opt = mda.MegatronDion([p], codec=object())
+    opt = mda.MegatronDion([p], codec=object(), elementwise_optimizer="sgd")
     with pytest.raises(RuntimeError, match="DION_STEP_REQUIRES_DISTRIBUTED_MODE"):
         opt.step()
-    opt.enable_distributed_mode(route_step_params=lambda: ([], [object()]))
-    with pytest.raises(RuntimeError, match="DION_ELEMENTWISE_UNSUPPORTED"):
+    item = ElementwiseStepParam(param=p, grad=torch.zeros(8, 8), optimizer_state=opt.state[p],
+                                optim_group=opt.param_groups[0])
+    opt.enable_distributed_mode(route_step_params=lambda: ([], [item]))
+    with pytest.raises(RuntimeError, match="DION_INVALID_ELEMENTWISE_OPT"):  # algorithm.py:276-280
         opt.step()
     assert opt.param_groups[0]["step"] == 2 and opt._step_count == 2
+    opt.state[p]["first_moment"] = torch.zeros(8, 8)
+    opt.state[p]["exp_avg"] = torch.zeros(8, 8)
+    opt.param_groups[0]["elementwise_optimizer"] = "adamw"
+    with pytest.raises(RuntimeError, match="DION_SCALAR_STATE_LAYOUT_CONFLICT"):  # algorithm.py:296-299
+        opt.step()
 
 
 def test_optimizer_defaults_match_reference_keys():
