@@ -187,8 +187,10 @@ int dion_grad_sum_sq(const DionBatchDesc* desc, const void* const* G, double* ou
 
 /*
  * The elementwise branch of MegatronDion.step (algorithm.py:247-429) for one bucket of
- * n_tensors same-hyper-parameter tensors: W, exp_avg (first_moment), exp_avg_sq
- * (second_moment) fp32, G fp32 or bf16 (g_dtype), numels[i] elements each, contiguous.
+ * n_tensors same-hyper-parameter tensors: W fp32; exp_avg (first_moment) and exp_avg_sq
+ * (second_moment) in m_dtype (DION_DTYPE_F32, or _BF16 for the speedrun's bf16 moments,
+ * every foreach result then rounded to bf16 as torch does); G fp32 or bf16 (g_dtype);
+ * numels[i] elements each, contiguous.
  * One read and one write of every tensor replaces the reference's chain of
  * torch._foreach_* passes:
  *   AdamW  elementwise_opts.py:45-80:  m = lerp(m, g, 1-b1); v = lerp(v, g*g, 1-b2);
@@ -199,12 +201,12 @@ int dion_grad_sum_sq(const DionBatchDesc* desc, const void* const* G, double* ou
  * Python doubles; step > 0 for AdamW ([DION_INVALID_ELEMENTWISE_ADAMW_STEP]).
  */
 int dion_elementwise_adamw(int32_t n_tensors, const int64_t* numels, float* const* W, const void* const* G,
-                           int32_t g_dtype, float* const* exp_avg, float* const* exp_avg_sq, double lr,
-                           double beta1, double beta2, double weight_decay, double eps, int32_t step,
+                           int32_t g_dtype, int32_t m_dtype, void* const* exp_avg, void* const* exp_avg_sq,
+                           double lr, double beta1, double beta2, double weight_decay, double eps, int32_t step,
                            dion_stream_t stream);
 int dion_elementwise_lion(int32_t n_tensors, const int64_t* numels, float* const* W, const void* const* G,
-                          int32_t g_dtype, float* const* exp_avg, double lr, double beta1, double beta2,
-                          double weight_decay, dion_stream_t stream);
+                          int32_t g_dtype, int32_t m_dtype, void* const* exp_avg, double lr, double beta1,
+                          double beta2, double weight_decay, dion_stream_t stream);
 
 #ifdef __cplusplus
 }

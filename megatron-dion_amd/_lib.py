@@ -94,10 +94,10 @@ _SIGNATURES = {
                        ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_round_bf16": ([_P, ctypes.c_int64, _P], ctypes.c_int),
     "dion_grad_sum_sq": ([_DESC, _PP, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
-    "dion_elementwise_adamw": ([ctypes.c_int32, _P, _PP, _PP, ctypes.c_int32, _PP, _PP, ctypes.c_double,
+    "dion_elementwise_adamw": ([ctypes.c_int32, _P, _PP, _PP, ctypes.c_int32, ctypes.c_int32, _PP, _PP, ctypes.c_double,
                                 ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int32,
                                 _P], ctypes.c_int),
-    "dion_elementwise_lion": ([ctypes.c_int32, _P, _PP, _PP, ctypes.c_int32, _PP, ctypes.c_double, ctypes.c_double,
+    "dion_elementwise_lion": ([ctypes.c_int32, _P, _PP, _PP, ctypes.c_int32, ctypes.c_int32, _PP, ctypes.c_double, ctypes.c_double,
                                ctypes.c_double, ctypes.c_double, _P], ctypes.c_int),
 }
 

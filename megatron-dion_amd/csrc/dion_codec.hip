@@ -3909,22 +3909,22 @@ int dion_grad_sum_sq(const DionBatchDesc* d, const void* const* G, double* out, 
 // the host-side scalars follow the reference's Python doubles (elementwise_opts.py:64-78,
 // 98-104): bias corrections and 1 - lr wd in double, cast to fp32 once
 int dion_elementwise_adamw(int32_t n_tensors, const int64_t* numels, float* const* W, const void* const* G,
-                           int32_t g_dtype, float* const* exp_avg, float* const* exp_avg_sq, double lr,
+                           int32_t g_dtype, int32_t m_dtype, void* const* exp_avg, void* const* exp_avg_sq, double lr,
                            double beta1, double beta2, double weight_decay, double eps, int32_t step,
                            dion_stream_t stream) {
   if (step <= 0) return fail(DION_E_INVALID, "[DION_INVALID_ELEMENTWISE_ADAMW_STEP] step=%d", step);
   const double bc1 = 1.0 - pow(beta1, step);
   const double bc2 = 1.0 - pow(beta2, step);
-  return ew::run(n_tensors, numels, W, G, g_dtype, exp_avg, exp_avg_sq, false, static_cast<float>(1.0 - beta1),
+  return ew::run(n_tensors, numels, W, G, g_dtype, m_dtype, exp_avg, exp_avg_sq, false, static_cast<float>(1.0 - beta1),
                  static_cast<float>(1.0 - beta2), static_cast<float>(sqrt(bc2)), static_cast<float>(eps),
                  static_cast<float>(lr / bc1), static_cast<float>(1.0 - lr * weight_decay), weight_decay != 0.0,
                  reinterpret_cast<hipStream_t>(stream));
 }
 
 int dion_elementwise_lion(int32_t n_tensors, const int64_t* numels, float* const* W, const void* const* G,
-                          int32_t g_dtype, float* const* exp_avg, double lr, double beta1, double beta2,
+                          int32_t g_dtype, int32_t m_dtype, void* const* exp_avg, double lr, double beta1, double beta2,
                           double weight_decay, dion_stream_t stream) {
-  return ew::run(n_tensors, numels, W, G, g_dtype, exp_avg, nullptr, true, static_cast<float>(1.0 - beta1),
+  return ew::run(n_tensors, numels, W, G, g_dtype, m_dtype, exp_avg, nullptr, true, static_cast<float>(1.0 - beta1),
                  static_cast<float>(1.0 - beta2), 1.0f, 0.0f, static_cast<float>(lr),
                  static_cast<float>(1.0 - lr * weight_decay), weight_decay != 0.0, reinterpret_cast<hipStream_t>(stream));
 }

@@ -15,8 +15,8 @@
 struct EwArgs {
   float* w[MAXB];
   const void* g[MAXB];
-  float* m1[MAXB];   // first moment
-  float* m2[MAXB];   // second moment (AdamW) or null
+  void* m1[MAXB];    // first moment (fp32, or bf16 in the mixed-precision mode)
+  void* m2[MAXB];    // second moment (AdamW) or null
   long numel[MAXB];
   float lerp1, lerp2;    // 1 - beta1, 1 - beta2
   float bc2_sqrt;        // sqrt(1 - beta2^step)
@@ -36,38 +36,57 @@ __device__ __forceinline__ float torch_sign(float x) {
   return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f);
 }
 
-template <int GDT, bool LION>
+// every foreach result lands in the moment dtype: rounded to bf16 in the
+// mixed-precision mode (torch computes bf16 elementwise ops in fp32 and rounds once)
+template <int MDT>
+__device__ __forceinline__ float rnd(float x) {
+  if constexpr (MDT == DION_DTYPE_BF16) return bf16_round(x);
+  else return x;
+}
+
+template <int MDT>
+__device__ __forceinline__ float ld_moment(const void* p, long i) {
+  if constexpr (MDT == DION_DTYPE_BF16) return bf16_to_f32(static_cast<const uint16_t*>(p)[i]);
+  else return static_cast<const float*>(p)[i];
+}
+
+template <int MDT>
+__device__ __forceinline__ void st_moment(void* p, long i, float v) {
+  if constexpr (MDT == DION_DTYPE_BF16) static_cast<uint16_t*>(p)[i] = f32_to_bf16_rne(v);
+  else static_cast<float*>(p)[i] = v;
+}
+
+template <int GDT, int MDT, bool LION>
 __global__ void __launch_bounds__(256) elementwise_kernel(const EwArgs a) {
   const int b = blockIdx.y;
   const long n = a.numel[b];
   float* __restrict__ W = a.w[b];
-  float* __restrict__ M1 = a.m1[b];
-  float* __restrict__ M2 = a.m2[b];
   for (long i = static_cast<long>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<long>(gridDim.x) * 256) {
     float g;
     if constexpr (GDT == DION_DTYPE_BF16) g = bf16_to_f32(static_cast<const uint16_t*>(a.g[b])[i]);
     else g = static_cast<const float*>(a.g[b])[i];
+    g = rnd<MDT>(g);  // grad.to(first_moment.dtype)
     float w = W[i];
-    const float m = M1[i];
+    const float m = ld_moment<MDT>(a.m1[b], i);
     if constexpr (LION) {
       // elementwise_opts.py:88-105
-      float u = torch_sign(torch_lerp(m, g, a.lerp1));
-      M1[i] = torch_lerp(m, g, a.lerp2);
-      u = u * a.step_size;
+      float u = torch_sign(rnd<MDT>(torch_lerp(m, g, a.lerp1)));
+      st_moment<MDT>(a.m1[b], i, torch_lerp(m, g, a.lerp2));
+      u = rnd<MDT>(u * a.step_size);
       if (a.has_decay) w = w * a.decay;
       W[i] = w - u;
     } else {
       // elementwise_opts.py:45-80
-      const float m_new = torch_lerp(m, g, a.lerp1);
-      const float gsq = g * g;
-      const float v_new = torch_lerp(M2[i], gsq, a.lerp2);
-      M1[i] = m_new;
-      M2[i] = v_new;
-      float denom = sqrtf(v_new);
-      denom = denom / a.bc2_sqrt;
-      denom = denom + a.eps;
-      float u = m_new / denom;
-      u = u * a.step_size;
+      const float m_new = rnd<MDT>(torch_lerp(m, g, a.lerp1));
+      const float gsq = rnd<MDT>(g * g);
+      const float v_new = rnd<MDT>(torch_lerp(ld_moment<MDT>(a.m2[b], i), gsq, a.lerp2));
+      st_moment<MDT>(a.m1[b], i, m_new);
+      st_moment<MDT>(a.m2[b], i, v_new);
+      float denom = rnd<MDT>(sqrtf(v_new));
+      denom = rnd<MDT>(denom / a.bc2_sqrt);
+      denom = rnd<MDT>(denom + a.eps);
+      float u = rnd<MDT>(m_new / denom);
+      u = rnd<MDT>(u * a.step_size);
       if (a.has_decay) w = w * a.decay;
       W[i] = w - u;
     }
@@ -78,13 +97,14 @@ __global__ void __launch_bounds__(256) elementwise_kernel(const EwArgs a) {
 
 namespace ew {
 
-int run(int n_tensors, const int64_t* numels, float* const* W, const void* const* G, int g_dtype, float* const* m1,
-        float* const* m2, bool lion, float lerp1, float lerp2, float bc2_sqrt, float eps, float step_size,
+int run(int n_tensors, const int64_t* numels, float* const* W, const void* const* G, int g_dtype, int m_dtype,
+        void* const* m1, void* const* m2, bool lion, float lerp1, float lerp2, float bc2_sqrt, float eps, float step_size,
         float decay, int has_decay, hipStream_t st) {
   if (n_tensors < 0) return fail(DION_E_INVALID, "n_tensors=%d", n_tensors);
   if (n_tensors > 0 && (numels == nullptr || W == nullptr || G == nullptr || m1 == nullptr || (!lion && m2 == nullptr)))
     return fail(DION_E_INVALID, "null argument");
   if (g_dtype != DION_DTYPE_F32 && g_dtype != DION_DTYPE_BF16) return fail(DION_E_UNSUPPORTED, "grad dtype %d", g_dtype);
+  if (m_dtype != DION_DTYPE_F32 && m_dtype != DION_DTYPE_BF16) return fail(DION_E_UNSUPPORTED, "moment dtype %d", m_dtype);
   for (int t0 = 0; t0 < n_tensors; t0 += MAXB) {
     const int nt = n_tensors - t0 < MAXB ? n_tensors - t0 : MAXB;
     EwArgs a;
@@ -111,12 +131,17 @@ int run(int n_tensors, const int64_t* numels, float* const* W, const void* const
     long gx = ceil_div(maxn, 256 * 4);
     if (gx > 2048) gx = 2048;
     const dim3 grid(static_cast<unsigned>(gx), nt);
-    if (lion) {
-      if (g_dtype == DION_DTYPE_BF16) hipLaunchKernelGGL((elementwise_kernel<DION_DTYPE_BF16, true>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((elementwise_kernel<DION_DTYPE_F32, true>), grid, dim3(256), 0, st, a);
+    auto launch = [&](auto Gc, auto Mc) {
+      constexpr int GD = decltype(Gc)::value, MD = decltype(Mc)::value;
+      if (lion) hipLaunchKernelGGL((elementwise_kernel<GD, MD, true>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((elementwise_kernel<GD, MD, false>), grid, dim3(256), 0, st, a);
+    };
+    using F32 = std::integral_constant<int, DION_DTYPE_F32>;
+    using B16 = std::integral_constant<int, DION_DTYPE_BF16>;
+    if (g_dtype == DION_DTYPE_BF16) {
+      if (m_dtype == DION_DTYPE_BF16) launch(B16{}, B16{}); else launch(B16{}, F32{});
     } else {
-      if (g_dtype == DION_DTYPE_BF16) hipLaunchKernelGGL((elementwise_kernel<DION_DTYPE_BF16, false>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((elementwise_kernel<DION_DTYPE_F32, false>), grid, dim3(256), 0, st, a);
+      if (m_dtype == DION_DTYPE_BF16) launch(F32{}, B16{}); else launch(F32{}, F32{});
     }
     const int rc = check_launch(lion ? "elementwise(lion)" : "elementwise(adamw)");
     if (rc != DION_OK) return rc;

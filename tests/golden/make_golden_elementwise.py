@@ -24,6 +24,11 @@ CASES = [
     dict(name="e2_lion", opt="lion", betas=(0.9, 0.99), wd=0.1, lr=0.003, eps=1e-8, gdtype="float32"),
     dict(name="e3_adamw_bf16grad_nowd", opt="adamw", betas=(0.8, 0.999), wd=0.0, lr=0.02, eps=1e-6,
          gdtype="bfloat16"),
+    # the speedrun's mixed precision (speedrun_nanogpt_mcore.py:422-431): bf16 moments
+    dict(name="e4_adamw_bf16_moments", opt="adam", betas=(0.9, 0.95), wd=0.01, lr=0.01, eps=1e-8,
+         gdtype="float32", state_dtype="bfloat16"),
+    dict(name="e5_lion_bf16_moments", opt="lion", betas=(0.9, 0.99), wd=0.1, lr=0.003, eps=1e-8,
+         gdtype="bfloat16", state_dtype="bfloat16"),
 ]
 TENSORS = [("ln", (64,)), ("emb", (40, 24)), ("bias", (33,)), ("head", (17, 96))]
 STEPS = 3
@@ -31,12 +36,15 @@ STEPS = 3
 
 def run_case(case):
     from megatron.core.optimizer.dion.algorithm import MegatronDion
-    from megatron.core.optimizer.dion.types import ElementwiseStepParam
+    from megatron.core.optimizer.dion.types import DionMixedPrecisionConfig, ElementwiseStepParam
 
     gen = torch.Generator().manual_seed(7)
     params = {n: torch.nn.Parameter(torch.randn(*s, generator=gen) * 0.02) for n, s in TENSORS}
+    sdt = getattr(torch, case.get("state_dtype", "float32"))
+    mpc = DionMixedPrecisionConfig(momentum_dtype=sdt, q_dtype=sdt, variance_dtype=sdt) \
+        if case.get("state_dtype") else None
     opt = MegatronDion(list(params.values()), lr=case["lr"], weight_decay=case["wd"], betas=case["betas"],
-                       elementwise_eps=case["eps"], elementwise_optimizer=case["opt"])
+                       elementwise_eps=case["eps"], elementwise_optimizer=case["opt"], mixed_precision_config=mpc)
     grads = {}
 
     def route():
@@ -67,8 +75,10 @@ def run_case(case):
 
 def main():
     os.environ["DION_DISABLE_TORCH_COMPILE"] = "1"
+    only = set(sys.argv[1:])
     for case in CASES:
-        run_case(case)
+        if not only or case["name"] in only:
+            run_case(case)
     man = {"tensors": [[n, list(s)] for n, s in TENSORS], "steps": STEPS,
            "cases": [dict(c, betas=list(c["betas"])) for c in CASES]}
     with open(os.path.join(HERE, "manifest_elementwise.json"), "w") as fh:

@@ -50,8 +50,9 @@ def test_oracle_matches_reference_elementwise(name):
     man, case, arr = _load(name)
     names = [n for n, _ in man["tensors"]]
     W = [arr[f"s0_{n}_W0"].clone() for n in names]
-    m1 = [torch.zeros_like(w) for w in W]
-    m2 = [torch.zeros_like(w) for w in W]
+    sdt = getattr(torch, case.get("state_dtype", "float32"))
+    m1 = [torch.zeros_like(w, dtype=sdt) for w in W]
+    m2 = [torch.zeros_like(w, dtype=sdt) for w in W]
     b1, b2 = case["betas"]
     for step in range(man["steps"]):
         G = [arr[f"s{step}_{n}_G"].to(getattr(torch, case["gdtype"])) for n in names]
@@ -62,9 +63,9 @@ def test_oracle_matches_reference_elementwise(name):
                                 step=step + 1, epsilon=case["eps"])
         for i, n in enumerate(names):
             assert torch.equal(W[i], arr[f"s{step}_{n}_W1"])
-            assert torch.equal(m1[i], arr[f"s{step}_{n}_m1"])
+            assert torch.equal(m1[i].float(), arr[f"s{step}_{n}_m1"])
             if case["opt"] != "lion":
-                assert torch.equal(m2[i], arr[f"s{step}_{n}_m2"])
+                assert torch.equal(m2[i].float(), arr[f"s{step}_{n}_m2"])
 
 
 def run_through_optimizer(name, dev, codec=None):
@@ -72,8 +73,12 @@ def run_through_optimizer(name, dev, codec=None):
     man, case, arr = _load(name)
     names = [n for n, _ in man["tensors"]]
     params = {n: torch.nn.Parameter(arr[f"s0_{n}_W0"].clone().to(dev)) for n in names}
+    sdt = getattr(torch, case.get("state_dtype", "float32"))
+    mpc = mda.DionMixedPrecisionConfig(momentum_dtype=sdt, q_dtype=sdt, variance_dtype=sdt) \
+        if case.get("state_dtype") else None
     opt = mda.MegatronDion(list(params.values()), lr=case["lr"], weight_decay=case["wd"], betas=tuple(case["betas"]),
-                           elementwise_eps=case["eps"], elementwise_optimizer=case["opt"], codec=codec)
+                           elementwise_eps=case["eps"], elementwise_optimizer=case["opt"], codec=codec,
+                           mixed_precision_config=mpc)
     grads = {}
     opt.enable_distributed_mode(route_step_params=lambda: ([], [
         ElementwiseStepParam(param=params[n], grad=grads[n], optimizer_state=opt.state[params[n]],
@@ -88,10 +93,11 @@ def run_through_optimizer(name, dev, codec=None):
         for n in names:
             st = opt.state[params[n]]
             assert st["step"] == step + 1
+            assert st["first_moment"].dtype == sdt
             yield step, n, "W", params[n], arr[f"s{step}_{n}_W1"]
-            yield step, n, "m1", st["first_moment"], arr[f"s{step}_{n}_m1"]
+            yield step, n, "m1", st["first_moment"].float(), arr[f"s{step}_{n}_m1"]
             if case["opt"] != "lion":
-                yield step, n, "m2", st["second_moment"], arr[f"s{step}_{n}_m2"]
+                yield step, n, "m2", st["second_moment"].float(), arr[f"s{step}_{n}_m2"]
 
 
 @pytest.mark.parametrize("name", _cases())

@@ -5,7 +5,9 @@ The kernel performs the reference's foreach chain per element in fp32, in the sa
 order and with torch's lerp formula; it differs from the captured CPU results only
 where a CPU library routine (sqrt, division) rounds differently from the GPU's
 correctly rounded ones.  Bar: max |a - b| / max |b| <= 1e-6 for W and the moments
-(observed: printed).
+(observed: printed).  With bf16 moments (the speedrun's mixed precision) such a
+difference can flip one bf16 rounding: moments <= 2^-7 (one ulp of the largest
+element), W <= 2e-3 (one flipped bf16 update is about 1e-3 of max |W| here).
 """
 import pytest
 import torch
@@ -19,11 +21,14 @@ pytestmark = pytest.mark.gpu
 def test_hip_elementwise_matches_reference(name):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    from tests.test_elementwise import _load
+    bf16 = _load(name)[1].get("state_dtype") == "bfloat16"
     worst = 0.0
     for step, n, k, ours, ref in run_through_optimizer(name, torch.device("cuda", 0)):
         err = _maxrel(ours, ref)
         worst = max(worst, err)
-        assert err <= 1e-6, (name, step, n, k, err)
+        tol = (2e-3 if k == "W" else 2 ** -7) if bf16 else 1e-6
+        assert err <= tol, (name, step, n, k, err)
     print(name, "worst maxrel", worst)
 
 
