@@ -2,20 +2,30 @@
 
 Contract (see the task's bench section and BASELINE.json):
   python bench.py [--gpus N --steps K --warmup W]
-  N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL); every rank
-  compresses its own full gradient set (weak scaling) and exchanges P (reduce-
-  scatter + all-gather) and R (all-reduce) over the replicate group, exactly the
-  reference's RP = N low-rank path.  One JSON line on rank 0.
+  N > 1: one rank per GPU over RCCL.  The driver launches the N ranks with
+  torch.distributed.run; run directly with --gpus N (WORLD_SIZE unset), bench.py starts
+  that launcher itself as a child process (nothing GPU-side runs in the parent) and
+  exits with its status.  Every rank compresses its own full gradient set (weak
+  scaling) and exchanges P (reduce-scatter + all-gather) and R (all-reduce) over the
+  replicate group, exactly the reference's RP = N low-rank path.  One JSON line on
+  rank 0: `value` is the whole-job aggregate (all ranks' gradient bytes / the slowest
+  rank's time); `value_per_gpu` is the metric's per-GPU figure (value / N).
 
-A step = MegatronDion.step() over all 128 matrices (32 x {qkv 6144x4096,
-proj 4096x4096, fc1 28672x4096, fc2 4096x14336 (transposed)}): M += G,
-P = M Q, RCQR, R = M^T P, fix-up, error feedback, column norm, weight update.
-G is bf16 (synthetic N(0, 1e-3^2)), M / W / Q fp32, all resident in HBM.
+A step = MegatronDion.step() over all matrices of the workload:
+  llama3-8b (default, BASELINE config 3/4): 32 x {qkv 6144x4096, proj 4096x4096,
+      fc1 28672x4096, fc2 4096x14336 (transposed)}, r = 64;
+  mixtral-8x7b-experts (config 5): 8 layers x 8 experts x {fc1 28672x4096,
+      fc2 4096x14336}, r = 128;
+  single-4096 (config 2): one 4096x4096 matrix, r = 64.
+M += G, P = M Q, RCQR, R = M^T P, fix-up, error feedback, column norm, weight update.
+G is bf16 (synthetic N(0, 1e-3^2)), M / W / Q fp32, all resident in HBM.  The
+optimizer is built with MegatronDion's defaults (deferred error feedback), i.e. exactly
+what INTEGRATION.md's Megatron kwargs construct.
 """
 import argparse
 import json
-import math
 import os
+import subprocess
 import sys
 import time
 
@@ -38,6 +48,27 @@ BYTES_PER_ELEM = {"project_p": 10.0, "project_p_ef": 10.0, "project_r": 4.0, "ef
 
 def llama_shapes(layers):
     return [(f"layers.{i}.{n}.weight", m, k) for i in range(layers) for n, m, k in LLAMA3_8B_LAYER]
+
+
+# Mixtral-8x7B experts (examples/mixtral/train_mixtral_8x7b_distributed.sh:32-55): hidden 4096,
+# ffn 14336 (SwiGLU: fc1 fuses gate and up, 28672 rows), 8 experts; 8 of the 32 layers fit
+# one GPU with W, M and G resident
+MIXTRAL_EXPERT = (("linear_fc1", 28672, 4096), ("linear_fc2", 4096, 14336))
+
+
+def mixtral_shapes(layers, experts=8):
+    return [(f"layers.{i}.mlp.experts.local_experts.{e}.{n}.weight", m, k)
+            for i in range(layers) for e in range(experts) for n, m, k in MIXTRAL_EXPERT]
+
+
+WORKLOADS = {
+    # name: (shapes(layers), rank, default layers, BASELINE config)
+    "llama3-8b-2d-grad-set-r64": (llama_shapes, 64, 32, "Llama-3-8B full 2D-weight grad set, rank=64"),
+    "mixtral-8x7b-experts-r128": (mixtral_shapes, 128, 8,
+                                  "Mixtral-8x7B expert-weight grads batched (8 layers x 8 experts), rank=128"),
+    "single-4096x4096-r64": (lambda layers: [("w", 4096, 4096)] * 1, 64, 1,
+                             "single 4096x4096 bf16 grad matrix, rank=64"),
+}
 
 
 # kernel instance behind each (codec call, orientation) on the Llama set (r = 64 -> RB = RU = 4);
@@ -122,32 +153,20 @@ def load_pmc_traffic(kernel):
         return None
 
 
-def cpu_baseline(sample_layers=1, steps=1):
-    """The pinned CPU oracle (`port`) on one Llama-3-8B layer, timed on this host's cores."""
-    from oracle import dion_oracle as O
+def cpu_baseline():
+    """The CPU restatement (`port`) timed on this host's cores per BASELINE.md:49-63: config 1
+    (GPT-125M 2D set, 2 gloo ranks, r = 16) and one Llama-3-8B layer (r = 64); 1 warm-up,
+    median of 5 steps each (oracle/cpu_baseline.py).  `value` is the Llama layer's rate, the
+    bench workload's unit; the full Llama set is 32 layers of the same work."""
+    from oracle import cpu_baseline as CB
 
-    # the GPU box exposes the whole host's CPUs; its share is OMP_NUM_THREADS (16 per GPU)
-    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    torch.set_num_threads(cores)
-    gen = torch.Generator().manual_seed(99)
-    hyper = O.DionHyper(rank_fraction=1 / 64)
-    mats = []
-    for _, m, n in llama_shapes(sample_layers):
-        W = torch.randn(m, n, generator=gen) * 0.02
-        M = torch.zeros(m, n)
-        q = torch.randn(m if m < n else n, 64, generator=gen)
-        G = (torch.randn(m, n, generator=gen) * 1e-3).to(torch.bfloat16).float()
-        mats.append(O.DionMatrix(W=W, M=M, Q=q, G=G, transposed=m < n, rank_fraction=1 / 64))
-    best = float("inf")
-    for _ in range(steps):
-        t0 = time.perf_counter()
-        for mt in mats:
-            O.dion_batch_step_local([mt], hyper)
-        best = min(best, time.perf_counter() - t0)
-    elems = sum(m * n for _, m, n in llama_shapes(sample_layers))
-    return {"value": round(elems * 2 / best / 2 ** 30, 4), "unit": "GiB/s", "cores": cores, "kind": "port",
-            "sample": f"{sample_layers} of 32 Llama-3-8B layers (qkv, proj, fc1, fc2; {elems} grad elements), "
-                      f"r=64, best of {steps} step(s), {best:.2f} s, torch CPU fp32 with {cores} threads"}
+    c1 = CB.gpt125m_gloo(world=2, steps=5, warmup=1)
+    c3 = CB.llama_layer(steps=5, warmup=1)
+    return {"value": c3["GiB_s"], "unit": "GiB/s", "cores": c3["threads"], "kind": "port",
+            "sample": f"one Llama-3-8B layer ({c3['grad_elements']} bf16 grad elements, 1/32 of the set), r=64, "
+                      f"median of 5 steps after 1 warm-up = {c3['step_s_median']} s/step, torch CPU fp32, "
+                      f"{c3['threads']} threads; product host runtime + oracle codec, eager error feedback",
+            "config1_gpt125m_2rank_gloo": c1, "llama_layer": c3}
 
 
 def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps, deferred, step_bpe=None):
@@ -226,12 +245,34 @@ def install_loopback(world):
     return group
 
 
+def kernel_names(r):
+    """KERNEL_OF / KERNEL_OF_BF16 with the rank-block template argument of rank r (dispatch_rb)."""
+    rb = {1: 1, 2: 2, 3: 4, 4: 4}.get((r + 15) // 16, 8)
+    table = KERNEL_OF_BF16 if BYTES_PER_ELEM is BYTES_PER_ELEM_BF16 else KERNEL_OF
+    return {k: (name.replace("<4", f"<{rb}", 1), n) for k, (name, n) in table.items()}
+
+
+def launch_ranks(args) -> int:
+    """--gpus N without a launcher: start torch.distributed.run as a CHILD process (this
+    process never touches the GPU) with the same arguments, and return its exit status."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--layers", type=int, default=32, help="Llama-3-8B has 32; fewer only for debugging")
+    ap.add_argument("--workload", default="llama3-8b-2d-grad-set-r64", choices=sorted(WORKLOADS))
+    ap.add_argument("--layers", type=int, default=0, help="layers of the workload (0 = its default); "
+                                                          "fewer only for debugging")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams for independent batches (N=1 path)")
     ap.add_argument("--probe-steps", type=int, default=2, help="single-stream steps timed per kernel for `roofline`")
@@ -249,9 +290,13 @@ def main():
                     help="time the W-rank batch schedule on one GPU with loopback collectives (not a bench line)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.backend == "gloo":
         # rehearsal of the multi-rank path on fewer GPUs than ranks (gloo exchanges through the host)
         local %= max(1, torch.cuda.device_count())
@@ -269,7 +314,8 @@ def main():
     from megatron_dion_amd.codec import HipDionCodec
     from megatron_dion_amd.optimizer import attach_dp_routing
 
-    shapes = llama_shapes(args.layers)
+    make_shapes, rank_r, default_layers, config_name = WORKLOADS[args.workload]
+    shapes = make_shapes(args.layers or default_layers)
     torch.manual_seed(1234 + rank)
     named = []
     for name, m, n in shapes:
@@ -279,17 +325,21 @@ def main():
     codec = TimedCodec(HipDionCodec(dev))
     bf16_state = args.state_dtype == "bf16"
     if bf16_state:
-        global BYTES_PER_ELEM, KERNEL_OF
-        BYTES_PER_ELEM, KERNEL_OF = BYTES_PER_ELEM_BF16, KERNEL_OF_BF16
+        global BYTES_PER_ELEM
+        BYTES_PER_ELEM = BYTES_PER_ELEM_BF16
         args.eager_ef = True  # no deferred-EF pass A for a bf16 momentum
     mpc = mda.DionMixedPrecisionConfig(momentum_dtype=torch.bfloat16, q_dtype=torch.bfloat16) if bf16_state else None
-    opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=1 / 64,
-                           codec=codec, local_streams=args.streams, defer_error_feedback=not args.eager_ef,
+    kw = {} if not args.eager_ef else {"defer_error_feedback": False}
+    min_side = min(min(m, n) for _, m, n in shapes)
+    opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01,
+                           rank_fraction=rank_r / min_side, codec=codec, local_streams=args.streams,
                            coalesce_max_entries=args.coalesce, pipeline_lookahead=args.lookahead,
-                           mixed_precision_config=mpc)
+                           mixed_precision_config=mpc, **kw)
     if args.simulate_world > 1:
         group = install_loopback(args.simulate_world)
     attach_dp_routing(opt, named, replicate_group=group)
+    assert all(opt.state[p]["r"] == rank_r for _, p in named), "rank rule gave another r"
+    deferred = bool(opt._defer_ef) and codec.supports_deferred_ef(*shapes[0][1:], rank_r, shapes[0][1] < shapes[0][2])
     elems = sum(m * n for _, m, n in shapes)
 
     for _ in range(args.warmup):
@@ -325,27 +375,34 @@ def main():
     opt._local_streams = args.streams
     summ = codec.summary()
     per_kernel = {}
+    knames = kernel_names(rank_r)
     for key, v in summ.items():
-        if key not in KERNEL_OF:
+        if key not in knames:
             continue
-        kname, launches_per_call = KERNEL_OF[key]
+        kname, launches_per_call = knames[key]
         agg = per_kernel.setdefault(kname, {"ms": 0.0, "bytes": 0.0, "launches": 0})
         agg["ms"] += v["total_ms"]
         agg["bytes"] += BYTES_PER_ELEM[key[0]] * v["elems"]
         agg["launches"] += v["calls"] * launches_per_call
     roofline = None
     if per_kernel:
-        roofline = kernel_roofline(per_kernel, elems, ms_per_step, args.probe_steps, not args.eager_ef,
+        roofline = kernel_roofline(per_kernel, elems, ms_per_step, args.probe_steps, deferred,
                                    step_bpe=20.0 if bf16_state else None)
 
+    wl = args.workload if (args.layers or default_layers) == default_layers else \
+        f"{args.workload} ({args.layers} layers, debug)"
     out = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-           "data": "synthetic (random-init Llama-3-8B 2D weight shapes, bf16 grads N(0,1e-3^2))",
-           "config": {"workload": "llama3-8b-2d-grad-set-r64", "matrices": len(shapes), "grad_elements": elems,
-                      "rank": 64, "grad_dtype": "bf16", "state_dtype": args.state_dtype,
-                      "error_feedback": "eager" if args.eager_ef else "deferred (applied in the next step's pass A)",
-                      "parallelism": f"dp{world} (replicate, low-rank P/R exchange)" if world > 1 else "dp1"},
+           "value_per_gpu": round(value / world, 2),
+           "value_definition": "value = aggregate bf16-grad GiB/s of all ranks (bench contract); "
+                               "value_per_gpu = value / n_gpus (the metric's per-GPU figure)",
+           "data": "synthetic (random-init weights of the workload's 2D shapes, bf16 grads N(0,1e-3^2))",
+           "config": {"workload": wl, "baseline_config": config_name, "matrices": len(shapes),
+                      "grad_elements": elems, "rank": rank_r, "grad_dtype": "bf16", "state_dtype": args.state_dtype,
+                      "error_feedback": "deferred (applied in the next step's pass A)" if deferred else "eager",
+                      "parallelism": f"dp{world} (replicate, low-rank P/R exchange, {args.backend})" if world > 1
+                      else "dp1"},
            "roofline": roofline}
     if bf16_state:
         out["dtype"] = "bf16 state (f32 accumulate)"

@@ -27,9 +27,10 @@ from torch.optim.optimizer import Optimizer
 
 from .batches import build_dion_batches
 from .runtime import (AsyncRuntime, coalesce_local_batches, coalesce_replicated_batches,
-                      flush_pending_error_feedback, is_replicated, run_dion_batch_async)
+                      drop_pending_error_feedback, flush_pending_error_feedback, is_replicated,
+                      run_dion_batch_async)
 from .state import init_dion_state
-from .types import DionDistMeta, DionMixedPrecisionConfig, DionStepParam
+from .types import DionDistMeta, DionMixedPrecisionConfig, DionStepParam, ElementwiseStepParam
 
 
 class MegatronDion(Optimizer):
@@ -43,7 +44,7 @@ class MegatronDion(Optimizer):
                  extra_scale_factor: float = 0.2, split_qkv: bool = False, split_linear: bool = False,
                  max_concurrent_tasks: Optional[int] = None, *, codec=None, sketch_seed: int = 0,
                  coalesce_local: bool = True, local_streams: int = 2, coalesce_max_entries: int = 16,
-                 defer_error_feedback: bool = False, pipeline_lookahead: int = 0):
+                 defer_error_feedback: bool = True, pipeline_lookahead: int = 0):
         if isinstance(params, (list, tuple)):
             for pg in params:
                 if isinstance(pg, dict) and "wd_mult" in pg:
@@ -83,6 +84,9 @@ class MegatronDion(Optimizer):
         self._codec = codec
         self._defer_ef = bool(defer_error_feedback)
         self._profile_records: List[Tuple[str, float]] = []
+        # algorithm.py:146: per-step scratch the reference's adapter clears on offload
+        # (dion_distrib_optimizer.py:4284-4306 calls optimizer._buffer_cache.clear())
+        self._buffer_cache: Dict[str, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ backend
     @property
@@ -107,6 +111,18 @@ class MegatronDion(Optimizer):
     def state_dict(self):
         self.flush_error_feedback()
         return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        """Drop every pending error feedback, then load.
+
+        The loaded momentum is an eager value (state_dict() flushed it before saving), so a
+        pending factor pair of the live run must not ride on it.  Megatron's Dion restore
+        keeps the live state's underscore keys (distrib_dion/checkpoint_io.py:308) but calls
+        this method first (distrib_optimizer.py:740 inside DionDistributedOptimizer.
+        load_state_dict, dion_distrib_optimizer.py:4218-4260), so the pending key is gone by
+        then."""
+        drop_pending_error_feedback(self)
+        return super().load_state_dict(state_dict)
 
     # ------------------------------------------------------------------ plugin surface
     def enable_distributed_mode(self, *, route_step_params=None) -> None:
@@ -304,6 +320,7 @@ class MegatronDion(Optimizer):
         if elementwise:
             # runtime.py:314-315: the elementwise task runs after the Dion batches
             self._apply_elementwise_batches(elementwise)
+        self._buffer_cache.clear()  # algorithm.py:219
         if profile:
             torch.cuda.synchronize()
             self._profile_records.append(("step", time.perf_counter() - t0))
@@ -334,22 +351,45 @@ def _as_dtype(d):
 
 
 # ---------------------------------------------------------------------------- standalone routing
+def is_dion_param(param: torch.Tensor, name: str = "") -> bool:
+    """distrib_dion/parameter.py:34-57 for a stand-alone model: 2D, not opted out
+    (`use_dion=False`), not sequence-parallel, not an embedding / output / LM-head table.
+    Everything else takes the elementwise branch (bootstrap.py:565-576)."""
+    if getattr(param, "use_dion", None) is False or param.dim() != 2:
+        return False
+    for flag in ("sequence_parallel", "average_gradients_across_tp_domain", "is_embedding_or_output_parameter",
+                 "is_lm_head_parameter"):
+        if getattr(param, flag, False):
+            return False
+    return not any(k in name for k in ("embedding", "output_layer", "lm_head"))
+
+
 def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str, torch.Tensor]],
-                      replicate_group=None, base_seed: int = 0) -> Dict[str, torch.Tensor]:
+                      replicate_group=None, base_seed: int = 0, dion_predicate=None) -> Dict[str, torch.Tensor]:
     """Stand-alone adapter: state init + `route_step_params` for plain data parallelism.
 
     Plays the part of the reference's DionDistributedOptimizer routing
     (distrib_dion/bootstrap.py:519-606 -> batches.py:971 build_dion_batches) for
-    users outside Megatron and for the benchmark: params sorted by uid, one
-    batch per `batch_world_size` same-key matrices.  G of each step is taken
-    from `param.main_grad` (Megatron's grad buffer view, bf16 or fp32) when
-    present, else from `param.grad`.
+    users outside Megatron and for the benchmark: 2D Dion params (`dion_predicate`,
+    default `is_dion_param`) sorted by uid, one batch per `batch_world_size` same-key
+    matrices; every other param with a gradient becomes an ElementwiseStepParam
+    (AdamW / Lion).  As in Megatron, elementwise gradients arrive already reduced across
+    replicas (only Dion buckets skip the replica all-reduce,
+    param_and_grad_buffer.py:649-698).  G of each step is taken from `param.main_grad` (Megatron's grad
+    buffer view, bf16 or fp32) when present, else from `param.grad`.
     """
     group = optimizer.param_groups[0]
     rf = float(group.get("rank_fraction", optimizer.defaults["rank_fraction"]))
     mult = int(optimizer.defaults.get("rank_multiple_of", 1))
+    pred = dion_predicate or is_dion_param
     metas = {}
+    group_of = {id(p): g for g in optimizer.param_groups for p in g["params"]}
+    dion_named, ew_named = [], []
     for name, p in named_params:
+        if not pred(p, name):
+            ew_named.append((name, p))
+            continue
+        dion_named.append((name, p))
         mpc = optimizer._mixed_precision_config
         state, cfg = init_dion_state(p, rank_fraction=rf, rank_multiple_of=mult, base_seed=base_seed,
                                      param_uid=(name,), param_name=name,
@@ -360,23 +400,31 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
         metas[name] = (cfg, DionDistMeta(shape=tuple(p.shape), global_shape=tuple(p.shape), rank_fraction=rf,
                                          is_transposed=cfg.is_transposed, param_uid=(name,), is_dion_param=True,
                                          param_name=name, param_config=cfg))
-    ordered = sorted(named_params, key=lambda kv: kv[0])
+    ordered = sorted(dion_named, key=lambda kv: kv[0])
+
+    def grad_of(p):
+        g = getattr(p, "main_grad", None)
+        return p.grad if g is None else g
 
     def route():
         steps = []
         for name, p in ordered:
-            g = getattr(p, "main_grad", None)
-            if g is None:
-                g = p.grad
+            g = grad_of(p)
             if g is None:
                 continue
             cfg, meta = metas[name]
             steps.append(DionStepParam(param=p, grad=g, optimizer_state=optimizer.state[p],
-                                       optim_group=group, config=cfg, dist_meta=meta))
+                                       optim_group=group_of.get(id(p), group), config=cfg, dist_meta=meta))
         batches = build_dion_batches(
             dion_params=steps, get_replicate_group=lambda: replicate_group,
             group_size=lambda g: dist.get_world_size(g))
-        return batches, []
+        elementwise = []
+        for _, p in ew_named:
+            g = grad_of(p)
+            if g is not None:
+                elementwise.append(ElementwiseStepParam(param=p, grad=g, optimizer_state=optimizer.state[p],
+                                                        optim_group=group_of.get(id(p), group)))
+        return batches, elementwise
 
     optimizer.enable_distributed_mode(route_step_params=route)
     return {name: p for name, p in named_params}

@@ -106,6 +106,56 @@ def validate_update_contract(optimizer, *, optim_groups, optimizer_states, dist_
             f"step={optimizer._step_count} expected={rows[0]} mismatched={[rows[i] for i in bad]}")
 
 
+def _shape_of(meta, state, fallback):
+    st = state or {}
+    shape = st.get("per_expert_global_shape") or st.get("global_shape") \
+        or getattr(meta, "per_expert_global_shape", None) or getattr(meta, "global_shape", None) or fallback
+    return tuple(int(d) for d in shape)
+
+
+def check_supported_batch(optimizer, *, batch_group, batch_collectives, configs, dist_metas, optimizer_states,
+                          param_shapes, real_batch_size: int) -> None:
+    """Refuse the batches this codec cannot compute, before any kernel runs.
+
+    The reference's adapter emits "fsdp" / "fsdp_tp" batches (distrib_dion/batches.py:571-584)
+    whose entries are FS row/column shards or TP shards, with FS/TP collectives attached
+    (types.py:149-158) and a q_norm / ortho group.  Treating those shards as whole matrices
+    would orthonormalise and normalise a local piece while scaling the LR by the global
+    shape: wrong updates with no error.  Only the whole-matrix data-parallel kind ("ddp",
+    runtime.py:1379-1496) is computed here; anything else raises
+    [DION_UNSUPPORTED_KERNEL_KIND]."""
+    def world(g):
+        try:
+            return int(dist.get_world_size(g))
+        except Exception:  # a stand-in group object (the reference's unit-test fakes)
+            return len(tuple(getattr(g, "ranks", ()) or ())) or 2
+
+    kind = str(getattr(batch_group, "kernel_kind", "ddp"))
+    why = None
+    if kind != "ddp":
+        why = f"kernel_kind={kind!r}"
+    elif getattr(batch_group, "ortho_group", None) is not None and world(batch_group.ortho_group) > 1:
+        why = "a distributed ortho_group (TP-sharded P)"
+    elif getattr(batch_group, "q_norm_group", None) is not None and world(batch_group.q_norm_group) > 1:
+        why = "a q_norm_group (FS-sharded column norm)"
+    elif batch_collectives is not None and (
+            getattr(batch_collectives, "fs_collective", None) is not None
+            or any(len(tuple(getattr(batch_collectives, f, None) or ())) for f in
+                   ("tp_q_gathers", "fs_p_collectives", "tp_r_collectives", "tp_q_reshards"))):
+        why = "FS/TP batch collectives"
+    else:
+        for i in range(int(real_batch_size)):
+            local = tuple(int(d) for d in param_shapes[i])
+            glob = _shape_of(dist_metas[i], optimizer_states[i], local)
+            if local != glob:
+                why = f"entry {i} is a shard: local shape {local} != global shape {glob}"
+                break
+    if why is not None:
+        raise RuntimeError(
+            f"[DION_UNSUPPORTED_KERNEL_KIND] step={optimizer._step_count}: {why}; this codec computes "
+            "whole-matrix data-parallel ('ddp') batches only (FS/TP-sharded Dion is not built)")
+
+
 def _sketch_seed(optimizer, batch_cache_key: int, entry: int) -> int:
     """Per (step, matrix) sketch seed; the reference's sketch is unseeded (ortho.py:659-661)."""
     base = int(getattr(optimizer, "_sketch_seed", 0))
@@ -136,6 +186,9 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     if real <= 0:
         return
     param_shapes = list(param_shapes) if param_shapes else [tuple(p.shape) for p in params]
+    check_supported_batch(optimizer, batch_group=batch_group, batch_collectives=batch_collectives, configs=configs,
+                          dist_metas=dist_metas, optimizer_states=optimizer_states, param_shapes=param_shapes,
+                          real_batch_size=real)
     validate_update_contract(optimizer, optim_groups=optim_groups, optimizer_states=optimizer_states,
                              dist_metas=dist_metas, param_shapes=param_shapes, real_batch_size=real)
     group = getattr(batch_group, "replicate_group", None)
@@ -352,6 +405,15 @@ def flush_pending_error_feedback(optimizer, get_codec) -> int:
         transposed = pend[0].shape[0] != M.shape[0]  # P has n rows iff transposed (m_P = n != m)
         _apply_pending(codec, M, Q, pend, int(M.shape[0]), int(M.shape[1]), transposed)
         count += 1
+    return count
+
+
+def drop_pending_error_feedback(optimizer) -> int:
+    """Forget every deferred error feedback (the momentum is about to be replaced)."""
+    count = 0
+    for st in optimizer.state.values():
+        if isinstance(st, dict) and st.pop(_PENDING_EF, None) is not None:
+            count += 1
     return count
 
 

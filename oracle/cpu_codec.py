@@ -1,0 +1,88 @@
+"""Codec backend built from the CPU oracle.  TEST INFRASTRUCTURE ONLY.
+
+Lets the multi-process (gloo) tests -- and bench.py's `cpu_baseline` leg -- drive the
+product's batch runtime and collective schedule (megatron_dion_amd/runtime.py) on
+CPU tensors with the oracle's arithmetic (oracle/dion_oracle.py).  It is injected
+explicitly (`MegatronDion(..., codec=OracleCodec())`); the product never constructs
+it and has no CPU fallback of its own.
+"""
+import torch
+
+from . import dion_oracle as O
+
+
+class OracleCodec:
+    name = "oracle-cpu"
+
+    def __init__(self, sketch_lookup=None, hyper_eps=1e-8, deferred=False):
+        self.sketch_lookup = sketch_lookup  # fn(P (1, m_P, r)) -> sketch (1, k, m_P) or None
+        self.deferred = deferred            # offer the deferred-EF pass A (host-logic tests)
+
+    def supports_deferred_ef(self, m, n, r, transposed, state_dtype=torch.float32):
+        return self.deferred
+
+    def project_p_ef(self, grads, momentums, qs, P, nonzero, transposed, ef_P, ef_R, alpha):
+        for b, M in enumerate(momentums):
+            if ef_P[b] is not None:
+                upd = (ef_R[b] @ ef_P[b].mT) if transposed else (ef_P[b] @ ef_R[b].mT)
+                M.add_(upd * alpha)
+        self.project_p(grads, momentums, qs, P, nonzero, transposed)
+
+    def project_p(self, grads, momentums, qs, P, nonzero, transposed):
+        for b, M in enumerate(momentums):
+            if grads is not None:
+                M.add_(grads[b].to(M.dtype))
+            X = M.mT if transposed else M
+            P[b] = X @ qs[b].to(X.dtype)          # bf16 state: a bf16 matmul (runtime.py:1607-1616)
+            nonzero[b] = int(bool((M != 0).any()))
+
+    def orthonormalize(self, P, m, n, transposed, seed, oversample=1.25, sketch=None, state_dtype=torch.float32):
+        for b in range(P.shape[0]):
+            S = sketch
+            if S is None and self.sketch_lookup is not None:
+                S = self.sketch_lookup(P[b:b + 1])
+            gen = torch.Generator().manual_seed(int(seed) & ((1 << 63) - 1))
+            out = O.orthogonalize(P[b:b + 1], oversample, sketch=S, generator=gen)
+            P[b:b + 1] = out.to(state_dtype)      # ortho.py:123 casts back to P's dtype
+
+    def round_bf16(self, X):
+        X.copy_(X.to(torch.bfloat16).float())
+
+    def project_r(self, momentums, P, R, transposed):
+        for b, M in enumerate(momentums):
+            X = M.mT if transposed else M
+            R[b] = X.mT @ P[b].to(X.dtype)
+
+    def fixup_colnorm(self, P, R, qs, nonzero, eps, m, n, transposed):
+        B = len(qs)
+        Q = torch.stack(qs, 0)
+        zero = (nonzero[:B] == 0).view(B, 1, 1)
+        P[:B] = torch.where(zero, torch.zeros_like(P[:B]), P[:B].nan_to_num())
+        R[:B] = torch.where(zero, Q.nan_to_num(), R[:B].nan_to_num())
+        Qn = O.column_normalize(R[:B], eps)
+        for b in range(B):
+            qs[b].copy_(Qn[b])
+
+    def ef_apply(self, momentums, params, P, R, qs, nonzero, mu, lr, wd, scaled_lr, transposed):
+        dt = qs[0].dtype  # the state dtype: factors carry it (kernels.py:54-83, 229-276)
+        for b in range(len(qs)):
+            Pb, Rb = P[b].to(dt), R[b].to(dt)
+            if momentums is not None:
+                upd = (Rb @ Pb.mT) if transposed else (Pb @ Rb.mT)
+                momentums[b].add_(upd * (-(1.0 - mu)))
+            if params is not None:
+                W = params[b]
+                if wd > 0:
+                    W.mul_(1 - lr * wd)
+                delta = (qs[b] @ Pb.mT) if transposed else (Pb @ qs[b].mT)
+                W.add_(delta.to(W.dtype), alpha=-scaled_lr)
+
+    def grad_sum_sq(self, grads, out):
+        out += O.grad_sum_sq_fp64(grads).to(out.device)
+
+    def elementwise_adamw(self, params, grads, first_moments, second_moments, **kw):
+        O.elementwise_adamw(params, grads, first_moments, second_moments, **kw)
+
+    def elementwise_lion(self, params, grads, first_moments, **kw):
+        O.elementwise_lion(params, grads, first_moments, **kw)
+

@@ -8,10 +8,11 @@ Three layers of evidence, all through the product path (HIP kernels via the C AB
   3. full size: Llama-3-8B shapes at r = 64 checked through size-independent
      properties (P^T P = I, Freivalds probes of R = X^T P and of the M/W updates).
 
-Tolerances (fp32 everywhere, TF32 off like the reference):
-  W, M: max |a-b| / max |b| <= 2e-5;  Q (column-normalised): <= 1e-4 after the
-  per-column sign alignment only where the sketch differs.  Integer results
-  (r, orientation, batch membership, zero flags) are compared exactly.
+Tolerances (fp32 everywhere, TF32 off like the reference; SURVEY.md 8(c)'s spec):
+  W, M, Q: max |a-b| / max |b| <= 1e-5 (Q after the per-column sign alignment only
+  where the sketch differs).  Integer results (r, orientation, batch membership, zero
+  flags) are compared exactly.  The optimizer runs with its default deferred error
+  feedback; M is read after flush_error_feedback() (the eager value).
 """
 import math
 
@@ -25,8 +26,8 @@ from tests._golden import Case, case_names
 
 pytestmark = pytest.mark.gpu
 
-TOL_WM = 2e-5
-TOL_Q = 1e-4
+TOL_WM = 1e-5
+TOL_Q = 1e-5
 
 
 def _dev():
@@ -86,6 +87,7 @@ def test_golden_replay_through_optimizer(name):
 
         opt._sketch_override = sketches
         opt.step()
+        opt.flush_error_feedback()
         torch.cuda.synchronize()
         for n in names:
             p = params[n]
@@ -110,6 +112,7 @@ def test_golden_rank_deficient_stays_finite_and_consistent():
     opt.state[p]["Q"].copy_(case.t(0, 0, f"{n}_Q0").to(dev))
     p.grad = case.t(0, 0, f"{n}_G").to(dev)
     opt.step()
+    opt.flush_error_feedback()
     torch.cuda.synchronize()
     P, R = opt._last_batch_factors
     for t in (p, opt.state[p]["momentum"], opt.state[p]["Q"], P, R):
@@ -160,7 +163,9 @@ def _run_gpu_local(mats, r, transposed, hyper, sketches=None):
     batch = DionBatch(batch_key=(), entries=tuple(entries), real_batch_size=len(entries),
                       batch_group=DionBatchGroup(batch_world_size=1))
     opt._step_count = 1
-    AsyncRuntime([run_dion_batch_async(opt, batch, sketches=sketches)], 3).run()
+    with torch.no_grad():
+        AsyncRuntime([run_dion_batch_async(opt, batch, sketches=sketches)], 3).run()
+    opt.flush_error_feedback()
     torch.cuda.synchronize()
     return [(p.detach().cpu(), opt.state[p]["momentum"].cpu(), opt.state[p]["Q"].cpu()) for p in params]
 

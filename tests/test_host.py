@@ -230,3 +230,155 @@ def test_local_path_end_to_end_with_oracle_codec(deferred):
             for got, key in checks:
                 ref = case.t(0, step, f"{n}_{key}")
                 assert (got.detach() - ref).abs().max().item() <= 1e-6 * ref.abs().max().item()
+
+
+# ---------------------------------------------------------------------------------------------- boundary guard
+def _one_batch(kind="ddp", shard=False, collectives=None):
+    from megatron_dion_amd.types import (DionBatch, DionBatchCollectives, DionBatchEntry, DionBatchGroup,
+                                         DionParamConfig)
+    from tests._cpu_codec import OracleCodec
+
+    p = torch.nn.Parameter(torch.randn(64, 48) * 0.02)
+    opt = mda.MegatronDion([p], rank_fraction=0.25, codec=OracleCodec())
+    local = (32, 48) if shard else (64, 48)
+    st = {"momentum": torch.zeros(*local), "Q": torch.randn(48, 12), "r": 12, "local_shape": local,
+          "global_shape": (64, 48)}
+    opt.state[p].update(st)
+    entry = DionBatchEntry(param=p, grad=torch.zeros(*local), optimizer_state=opt.state[p],
+                           optim_group=opt.param_groups[0], config=DionParamConfig(use_low_rank_sync=True),
+                           dist_meta=DionDistMeta(global_shape=(64, 48)), momentum=st["momentum"],
+                           q_tensor=st["Q"], param_shape=local)
+    batch = DionBatch(batch_key=(), entries=(entry,), real_batch_size=1,
+                      batch_group=DionBatchGroup(kernel_kind=kind, batch_world_size=1),
+                      batch_collectives=collectives or DionBatchCollectives())
+    return opt, batch
+
+
+@pytest.mark.parametrize("case", ["fsdp", "fsdp_tp", "shard", "fs_collective"])
+def test_unsupported_kernel_kinds_are_refused_before_any_work(case):
+    """FS/TP batches must not run as whole matrices (distrib_dion/batches.py:571-584)."""
+    from megatron_dion_amd.runtime import run_dion_batch_async
+    from megatron_dion_amd.types import DionBatchCollectives
+
+    kind = case if case.startswith("fsdp") else "ddp"
+    coll = DionBatchCollectives(fs_collective=object()) if case == "fs_collective" else None
+    opt, batch = _one_batch(kind=kind, shard=case == "shard", collectives=coll)
+    M0 = batch.momentums[0].clone()
+    with pytest.raises(RuntimeError, match=r"\[DION_UNSUPPORTED_KERNEL_KIND\]"):
+        for _ in run_dion_batch_async(opt, batch):
+            pass
+    assert torch.equal(batch.momentums[0], M0)  # nothing ran
+
+
+def test_ddp_batch_passes_the_guard():
+    from megatron_dion_amd.runtime import run_dion_batch_async
+
+    opt, batch = _one_batch()
+    opt._step_count = 1
+    with torch.no_grad():
+        for _ in run_dion_batch_async(opt, batch):
+            pass
+    assert torch.isfinite(batch.params[0]).all()
+
+
+# ---------------------------------------------------------------------------------------------- drop-in defaults
+def test_deferred_error_feedback_is_the_drop_in_default():
+    """INTEGRATION.md's Megatron kwargs construct exactly the benchmarked optimizer."""
+    p = torch.nn.Parameter(torch.zeros(8, 8))
+    opt = mda.MegatronDion([p], codec=object())
+    assert opt._defer_ef is True
+    assert isinstance(opt._buffer_cache, dict)  # cleared by DionDistributedOptimizer.offload_to_cpu
+
+
+def _ckpt_run(steps_before, steps_after, interrupt):
+    """Deferred-EF run over two matrices with a Megatron-style save / restore in the middle:
+    save = the adapter's state_dict() chain (distrib_optimizer.py:651 calls optimizer.state_dict())
+    followed by reading optimizer.state without '_' keys (checkpoint_io.py:247-268); restore =
+    optimizer.load_state_dict() (distrib_optimizer.py:740) then new tensors for every
+    persistent key, keeping the live '_' keys (checkpoint_io.py:271-336)."""
+    from megatron_dion_amd.optimizer import attach_dp_routing
+    from megatron_dion_amd.runtime import _PENDING_EF
+    from tests._cpu_codec import OracleCodec
+
+    torch.manual_seed(0)
+    named = [("a", torch.nn.Parameter(torch.randn(64, 48) * 0.02)),
+             ("b", torch.nn.Parameter(torch.randn(40, 96) * 0.02))]
+    sk = {}
+
+    def sketch(P):
+        key = tuple(P.shape)
+        if key not in sk:
+            sk[key] = torch.randn(1, 128, P.shape[-2], generator=torch.Generator().manual_seed(P.shape[-2])) / 128 ** .5
+        return sk[key]
+
+    opt = mda.MegatronDion([p for _, p in named], rank_fraction=0.25,
+                           codec=OracleCodec(sketch_lookup=sketch, deferred=True))
+    attach_dp_routing(opt, named)
+
+    def step(i):
+        g = torch.Generator().manual_seed(10 + i)
+        for _, p in named:
+            p.grad = (torch.randn(p.shape, generator=g) * 1e-3).to(torch.bfloat16).float()
+        opt.step()
+
+    for i in range(steps_before):
+        step(i)
+    if interrupt:
+        opt.state_dict()  # the save chain flushes the pending error feedback
+        saved = {n: {k: (v.clone() if torch.is_tensor(v) else v) for k, v in opt.state[p].items()
+                     if not k.startswith("_")} for n, p in named}
+        assert all(_PENDING_EF not in opt.state[p] for _, p in named)
+        step(steps_before)  # the run goes on, then is rolled back to the checkpoint
+        for n, p in named:
+            p.data.copy_(saved[n]["param"] if "param" in saved[n] else p.data)
+        live = {n: {k: v for k, v in opt.state[p].items() if k.startswith("_")} for n, p in named}
+        assert all(_PENDING_EF in live[n] for n in live)  # the live run holds a pending EF
+        opt.load_state_dict(opt.state_dict())  # drops pending; the adapter then restores tensors
+        for n, p in named:
+            restored = {k: v for k, v in opt.state[p].items() if k.startswith("_")}
+            for k, v in saved[n].items():
+                restored[k] = v.clone() if torch.is_tensor(v) else v
+            opt.state[p] = restored
+        return opt, named, step, saved
+    return opt, named, step, None
+
+
+def test_checkpoint_round_trip_with_deferred_error_feedback():
+    """Restoring a checkpoint must not apply the live run's stale pending EF."""
+    from megatron_dion_amd.runtime import _PENDING_EF
+
+    ref_opt, ref_named, ref_step, _ = _ckpt_run(3, 0, False)
+    ref_opt.flush_error_feedback()
+    # interrupted run: 3 steps, save, 1 more step, restore params + state from the checkpoint
+    opt, named, step, saved = _ckpt_run(3, 0, True)
+    for (n, p), (_, q) in zip(named, ref_named):
+        p.data.copy_(q.data)  # the weights of the checkpointed step (the payload's "param")
+        assert _PENDING_EF not in opt.state[p]
+        assert torch.equal(opt.state[p]["momentum"], ref_opt.state[q]["momentum"])
+    for i in range(3, 5):
+        step(i)
+        ref_step(i)
+    opt.flush_error_feedback()
+    ref_opt.flush_error_feedback()
+    for (_, p), (_, q) in zip(named, ref_named):
+        assert torch.allclose(p, q, rtol=0, atol=1e-7)
+        assert torch.allclose(opt.state[p]["momentum"], ref_opt.state[q]["momentum"], rtol=0, atol=1e-9)
+
+
+def test_standalone_routing_sends_non_dion_params_to_the_elementwise_branch():
+    """bootstrap.py:565-576 via attach_dp_routing: 1D / embedding / output params -> ElementwiseStepParam."""
+    from megatron_dion_amd.optimizer import attach_dp_routing, is_dion_param
+
+    named = [("layers.0.linear_fc1.weight", torch.nn.Parameter(torch.zeros(64, 32))),
+             ("layers.0.norm.weight", torch.nn.Parameter(torch.ones(32))),
+             ("embedding.word_embeddings.weight", torch.nn.Parameter(torch.zeros(100, 32))),
+             ("output_layer.weight", torch.nn.Parameter(torch.zeros(100, 32)))]
+    for _, p in named:
+        p.grad = torch.zeros_like(p)
+    opt = mda.MegatronDion([p for _, p in named], rank_fraction=0.25, codec=object())
+    attach_dp_routing(opt, named)
+    batches, ew = opt._route_step_params()
+    assert [b.dist_metas[0].param_name for b in batches] == ["layers.0.linear_fc1.weight"]
+    assert sorted(id(e.param) for e in ew) == sorted(id(p) for _, p in named[1:])
+    assert "Q" not in opt.state[named[1][1]]
+    assert is_dion_param(named[0][1], named[0][0]) and not is_dion_param(named[2][1], named[2][0])
