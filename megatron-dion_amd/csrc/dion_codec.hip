@@ -2280,7 +2280,7 @@ __device__ __forceinline__ void rpe_load(RowStepE<GDT>& S, const float* __restri
     }
 }
 
-template <int RB, int GDT>
+template <int RB, int GDT, bool STORE = true>
 __device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRBE][RB], const bf16x8* tq,
                                             const bf16x8* rs, const Split3 (&F)[kRBE][RB / 2], bool has_ef,
                                             float* __restrict__ M, long ld_m, int j, int lane, uint32_t& nzb) {
@@ -2316,7 +2316,7 @@ __device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRBE]
         } else if constexpr (GDT == DION_DTYPE_F32) {
           S.x[rb][c] += S.gf[rb][c];
         }
-        st_part(reinterpret_cast<f32x4*>(M + rb * 16 * ld_m + j + 16 * c), S.x[rb][c]);
+        if constexpr (STORE) st_part(reinterpret_cast<f32x4*>(M + rb * 16 * ld_m + j + 16 * c), S.x[rb][c]);
       }
   }
 #pragma unroll
@@ -2338,8 +2338,19 @@ __device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRBE]
   }
 }
 
+// TJ line stores: the updated M tile goes back through the wave's LDS tile and leaves in
+// whole 128-B lines with the non-temporal policy (tuning knob, DION_PA_STLINES)
+// measured on the Llama fc1 group (16 x 28672 x 4096): 4.10 -> 3.84 ms with both (r02)
+#ifndef DION_PA_STLINES
+#define DION_PA_STLINES 1
+#endif
+#ifndef DION_PA_NTLD
+#define DION_PA_NTLD 1
+#endif
+
 template <int RB, int GDT, int PD, bool TJ>
 __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_ef_kernel(const EfProjArgs e) {
+  constexpr bool kLineStore = TJ && DION_PA_STLINES;
   constexpr int R = 16 * RB;
   constexpr int KK = RB / 2;
   __shared__ bf16x8 tq[2][RB * 3 * 64];
@@ -2369,7 +2380,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_ef_kernel(const
     G = static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 4 * g;
   else if constexpr (GDT == DION_DTYPE_F32)
     G = static_cast<const float*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 4 * g;
-  const float* __restrict__ Mw = a.m[b] + static_cast<long>(row_base + (lane >> 3)) * a.ld_m + 4 * (lane & 7);
+  float* __restrict__ Mw = a.m[b] + static_cast<long>(row_base + (lane >> 3)) * a.ld_m + 4 * (lane & 7);
   const float* __restrict__ Rp = e.efr[b];
   const bool has_ef = Rp != nullptr;
 
@@ -2407,7 +2418,8 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_ef_kernel(const
     if constexpr (TJ) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        T.x[q >> 1][q & 1] = *reinterpret_cast<const f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j);
+        T.x[q >> 1][q & 1] = DION_PA_NTLD ? ld_stream(reinterpret_cast<const f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j))
+                                          : *reinterpret_cast<const f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j);
       rpe_load<GDT>(T, nullptr, G, 0, a.ld_g, j);
     } else {
       rpe_load<GDT>(T, M, G, a.ld_m, a.ld_g, j);
@@ -2427,6 +2439,22 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_ef_kernel(const
         const int r = 16 * rb + t, k = 4 * c + g;
         T.x[rb][c] = xw[r * 8 + (k ^ ((r >> 1) & 7))];
       }
+  };
+  // the inverse: MFMA layout -> LDS -> whole-line non-temporal stores
+  auto xstore = [&](const RowStepE<GDT>& T, int j) {
+    f32x4* xw = xt[TJ ? wave : 0];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int r = 16 * rb + t, k = 4 * c + g;
+        xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[rb][c];
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 8 * q + (lane >> 3), k = lane & 7;
+      st_stream(reinterpret_cast<f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j), xw[r * 8 + (k ^ ((r >> 1) & 7))]);
+    }
   };
   SplitCopyN<NQ, 64 * kPaNW> TA;
   SplitCopyN<NR, 64 * kPaNW> EA;
@@ -2453,7 +2481,8 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_ef_kernel(const
         if (has_ef) split_copy_load_n(EA, rsp + static_cast<long>(cj(j + 32) / 32) * NR, tid);
       }
       if constexpr (TJ) xpose(S[k]);
-      rpe_compute<RB, GDT>(S[k], acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, cj(j), lane, nzb);
+      rpe_compute<RB, GDT, !kLineStore>(S[k], acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, cj(j), lane, nzb);
+      if constexpr (kLineStore) xstore(S[k], cj(j));
       if (!more) break;
       split_copy_store_n(TA, tq[cur ^ 1], tid);
       if (has_ef) split_copy_store_n(EA, rs[cur ^ 1], tid);
@@ -2477,6 +2506,11 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_ef_kernel(const
 // lane (t, g) holds columns 2t, 2t + 1 of rows 16 h + 4 g + q (h = 0, 1; q = 0..3):
 // per half h that is the EF accumulator's slice, and per column the 8 rows are
 // the projection's k-run (KMAP 1).
+// cache policy of the transposed pass A's bf16 G loads (64-B row pieces): 1 = nt (tuning knob)
+#ifndef DION_CPE_GNT
+#define DION_CPE_GNT 1
+#endif
+
 template <int GDT>
 struct ColStepE {
   f32x2 x[2][4];
@@ -2494,7 +2528,9 @@ __device__ __forceinline__ void cpe_load(ColStepE<GDT>& S, const float* __restri
       const long row = i0 + 16 * h + q;
       S.x[h][q] = ld_stream(reinterpret_cast<const f32x2*>(M + row * ld_m));
       if constexpr (GDT == DION_DTYPE_BF16)
-        S.gb[h][q] = ld_stream(reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(G) + row * ld_g));
+        S.gb[h][q] = DION_CPE_GNT
+                         ? ld_stream(reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(G) + row * ld_g))
+                         : *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(G) + row * ld_g);
       else if constexpr (GDT == DION_DTYPE_F32)
         S.gf[h][q] = ld_stream(reinterpret_cast<const f32x2*>(static_cast<const float*>(G) + row * ld_g));
     }
@@ -2680,10 +2716,19 @@ __device__ __forceinline__ void rpx_compute(const RowStepE<DION_DTYPE_NONE>& S, 
   }
 }
 
+// TJ loads for the pass-B row kernel: M arrives in whole 128-B lines with the
+// non-temporal policy and is turned into the MFMA layout through a wave-private LDS
+// tile, as in rowproj_ef_kernel (tuning knob, DION_PBX_TJ)
+#ifndef DION_PBX_TJ
+#define DION_PBX_TJ 0
+#endif
+
 template <int RB>
 __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
+  constexpr bool TJ = DION_PBX_TJ && kRBE == 2;
   __shared__ bf16x8 tq[2][RB * 3 * 64];
+  __shared__ f32x4 xt[TJ ? 4 : 1][TJ ? 32 * 8 : 1];
   const BlockXYZ blk = xcd_block();
   const int b = blk.z;
   const int kc = blk.y;
@@ -2699,6 +2744,33 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
   const int j_rot = walk_rotation(blk, j_len);
   auto cj = [&](int j) { const int x = j - j_begin + j_rot; return j_begin + (x >= j_len ? x - j_len : x); };
   const float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 4 * g;
+  const float* __restrict__ Mw = a.m[b] + static_cast<long>(row_base + (lane >> 3)) * a.ld_m + 4 * (lane & 7);
+  auto xload = [&](RowStepE<DION_DTYPE_NONE>& T, int j) {
+    if constexpr (TJ) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        T.x[q >> 1][q & 1] = ld_stream(reinterpret_cast<const f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j));
+    } else {
+      rpe_load<DION_DTYPE_NONE>(T, M, nullptr, a.ld_m, 0, j);
+    }
+  };
+  auto xpose = [&](RowStepE<DION_DTYPE_NONE>& T) {
+    if constexpr (TJ) {
+      f32x4* xw = xt[wave];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 8 * q + (lane >> 3), k = lane & 7;
+        xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[q >> 1][q & 1];
+      }
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int r = 16 * rb + t, k = 4 * c + g;
+          T.x[rb][c] = xw[r * 8 + (k ^ ((r >> 1) & 7))];
+        }
+    }
+  };
 
   f32x4 acc[kRBE][RB];
 #pragma unroll
@@ -2710,7 +2782,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
   constexpr int NQ = RB * 3 * 64;
   const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
   SplitCopy<NQ> TA;
-  rpe_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, cj(j_begin));
+  xload(SA, cj(j_begin));
   split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j_begin) / 32) * NQ, tid);
   split_copy_store<NQ>(TA, tq[0], tid);
   __syncthreads();
@@ -2718,9 +2790,10 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
   for (int j0 = j_begin; j0 < j_end; j0 += 64) {
     const bool more = j0 + 32 < j_end;
     if (more) {
-      rpe_load<DION_DTYPE_NONE>(SB, M, nullptr, a.ld_m, 0, cj(j0 + 32));
+      xload(SB, cj(j0 + 32));
       split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j0 + 32) / 32) * NQ, tid);
     }
+    xpose(SA);
     rpx_compute<RB>(SA, acc, tq[cur], lane);
     if (!more) break;
     split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
@@ -2728,9 +2801,10 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
     cur ^= 1;
     const bool more2 = j0 + 64 < j_end;
     if (more2) {
-      rpe_load<DION_DTYPE_NONE>(SA, M, nullptr, a.ld_m, 0, cj(j0 + 64));
+      xload(SA, cj(j0 + 64));
       split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j0 + 64) / 32) * NQ, tid);
     }
+    xpose(SB);
     rpx_compute<RB>(SB, acc, tq[cur], lane);
     if (!more2) break;
     split_copy_store<NQ>(TA, tq[cur ^ 1], tid);

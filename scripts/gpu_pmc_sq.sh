@@ -1,0 +1,19 @@
+# MFMA / VALU / wait counters of the streaming kernels (one GPU box call).
+# Each counter group is its own rocprofv3 --pmc pass (at most 8 SQ and 2 GRBM counters
+# per pass, MI355X_MICROARCH.md "rocprofv3 PMC slots"), over scripts/dev/kbench.py,
+# which runs one codec op on a Llama-size batch of 16 matrices (r = 64).
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for OP in ${OPS:-pa_ef pa_ef_T pb pb_T w w_T}; do
+  i=0
+  for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+             "SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES" \
+             "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+    timeout -s KILL 120 rocprofv3 --pmc $grp -d "$PWD/gpurun_out/pmcsq_${OP}_$i" -o run --output-format csv -- python scripts/dev/kbench.py $OP 2 > gpurun_out/pmcsq_${OP}_$i.log 2>&1
+    rc=$?; echo "pmc $OP group $i rc=$rc"; if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmcsq_${OP}_$i.log; exit $rc; fi
+    i=$((i+1))
+  done
+done
+python scripts/pmc_sq_summary.py gpurun_out > gpurun_out/pmc_sq.json
+echo "summary rc=$?"
