@@ -79,7 +79,7 @@ KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("project_p_ef", True): ("colproj_ef_kernel<4, 2>", 1),
              ("ef_apply_w", False): ("rank_stream_kernel<4, false, 8, 2>", 1),
              ("ef_apply_w", True): ("rank_stream_kernel<4, false, 8, 2>", 1),
-             ("project_r", False): ("colproj_x6_kernel<4, 4>", 1),
+             ("project_r", False): ("colproj_h3_kernel<4, 4, 4>", 1),
              ("project_r", True): ("rowproj_x6_kernel<4>", 1),
              ("ef_apply", False): ("rank_stream_kernel<4, false, 8, 2>", 2),
              ("ef_apply", True): ("rank_stream_kernel<4, false, 8, 2>", 2)}
@@ -246,10 +246,14 @@ def install_loopback(world):
 
 
 def kernel_names(r):
-    """KERNEL_OF / KERNEL_OF_BF16 with the rank-block template argument of rank r (dispatch_rb)."""
+    """KERNEL_OF / KERNEL_OF_BF16 with the rank-block template argument of rank r (dispatch_rb);
+    the h3 pass-B column kernel keeps 2 columns per lane at r > 64 (colh3_ct)."""
     rb = {1: 1, 2: 2, 3: 4, 4: 4}.get((r + 15) // 16, 8)
     table = KERNEL_OF_BF16 if BYTES_PER_ELEM is BYTES_PER_ELEM_BF16 else KERNEL_OF
-    return {k: (name.replace("<4", f"<{rb}", 1), n) for k, (name, n) in table.items()}
+    out = {k: (name.replace("<4", f"<{rb}", 1), n) for k, (name, n) in table.items()}
+    if r > 64 and ("project_r", False) in out:
+        out[("project_r", False)] = (f"colproj_h3_kernel<{rb}, 4, 2>", 1)
+    return out
 
 
 def launch_ranks(args) -> int:

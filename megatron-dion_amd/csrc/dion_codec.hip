@@ -161,6 +161,7 @@ struct ProjArgs {
   int vec;                 // 16-byte loads allowed
   const void* tsplit;      // thin operand pre-split (presplit_kernel layout 0, KMAP 0) for the x6 kernels
   long ts_stride;          // 16-byte units per matrix of tsplit
+  const float* tinv;       // h3 kernels: 1 / scale of each matrix's thin-operand split
 };
 
 // ============================================================================
@@ -2720,7 +2721,7 @@ __device__ __forceinline__ void rpx_compute(const RowStepE<DION_DTYPE_NONE>& S, 
 // non-temporal policy and is turned into the MFMA layout through a wave-private LDS
 // tile, as in rowproj_ef_kernel (tuning knob, DION_PBX_TJ)
 #ifndef DION_PBX_TJ
-#define DION_PBX_TJ 0
+#define DION_PBX_TJ 1
 #endif
 
 template <int RB>
@@ -2931,6 +2932,211 @@ __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : (NW >= 8 ? DION_COLX6_M
 }
 
 // ============================================================================
+// fp16x3 ("h3") products.  Each fp32 operand is scaled by a power of two s and split
+// exactly into two fp16 limbs, x s = hi + lo + e with |e| <= 2^-22 |x s|; the three
+// products hi.hi + hi.lo + lo.hi (v_mfma_f32_16x16x32_f16, exact products, fp32
+// accumulation) give the fp32 product to ~2^-22 relative, with HALF the MFMA work of
+// the bf16x6 split (fp16 has 11 mantissa bits to bf16's 8).  fp16's narrow exponent is
+// handled by the scale: s maps the block's |x| maximum into [2^14, 2^15) (no overflow);
+// any element down to 2^-17 of that maximum keeps both limbs normal, and smaller ones
+// err by at most 2^-40 of the maximum in absolute terms.  Zero / NaN / inf maxima keep
+// s = 1 or shrink it, so NaN and inf propagate as in fp32.
+// ============================================================================
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+struct Split2h {
+  f16x8 hi, lo;
+};
+
+// power-of-two scale s (and 1/s) with amax * s in [2^14, 2^15); clamped to normal floats
+__device__ __forceinline__ float h3_scale(float amax, float& inv) {
+  const int be = static_cast<int>((__float_as_uint(amax) >> 23) & 0xFFu);  // biased exponent
+  int es = 127 + 14 - (be - 127);                                           // 2^(14 - e)
+  es = es < 1 ? 1 : (es > 254 ? 254 : es);
+  inv = __uint_as_float(static_cast<uint32_t>(254 - es) << 23);
+  return __uint_as_float(static_cast<uint32_t>(es) << 23);
+}
+
+__device__ __forceinline__ void split2h(const f32x4& a, const f32x4& b, float s, Split2h& o) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = (j < 4 ? a[j] : b[j - 4]) * s;
+    const _Float16 h = static_cast<_Float16>(x);
+    o.hi[j] = h;
+    o.lo[j] = static_cast<_Float16>(x - static_cast<float>(h));
+  }
+}
+
+// D += A B with both operands h3-split: the two small cross terms first
+__device__ __forceinline__ f32x4 mfma3h(const Split2h& A, const Split2h& B, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A.lo, B.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A.hi, B.lo, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A.hi, B.hi, acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ float max8abs(const f32x4& a, const f32x4& b) {
+  return fmaxf(fmaxf(fmaxf(fabsf(a[0]), fabsf(a[1])), fmaxf(fabsf(a[2]), fabsf(a[3]))),
+               fmaxf(fmaxf(fabsf(b[0]), fabsf(b[1])), fmaxf(fabsf(b[2]), fabsf(b[3]))));
+}
+
+// per-matrix max |x| of a small factor (rows x r fp32), as the float's bit pattern
+// (non-negative floats order like their bits; a NaN sorts above inf)
+struct AbsMaxArgs {
+  const float* src[MAXB];
+  uint32_t* out;  // (batch,) zero-initialised
+  long count;     // values per matrix
+};
+
+__global__ void __launch_bounds__(256) absmax_kernel(const AbsMaxArgs a) {
+  const int b = blockIdx.y;
+  const float* __restrict__ src = a.src[b];
+  uint32_t m = 0;
+  if (src != nullptr)
+    for (long i = static_cast<long>(blockIdx.x) * 256 + threadIdx.x; i < a.count; i += static_cast<long>(gridDim.x) * 256)
+      m = max(m, __float_as_uint(src[i]) & 0x7FFFFFFFu);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), off, 64)));
+  if ((threadIdx.x & 63) == 0) atomicMax(&a.out[b], m);
+}
+
+// h3 pre-split of a small factor in the MFMA operand layout of presplit_kernel layout 0
+// (grp = (row / 32) RB + cb; lane (t, g) <- rows 32 blk + kmap(g, e), column 16 cb + t),
+// two fp16 limbs per 8 values: dst[(grp * 2 + part) * 64 + lane], scale from amax[b]
+struct Presplit16Args {
+  const float* src[MAXB];
+  f16x8* dst;
+  const uint32_t* amax;  // (batch,) max |x| bits
+  float* inv_scale;      // (batch,) 1 / s, written by the blocks of x = 0
+  long stride;           // f16x8 units per matrix
+  int rows, r, kmap;
+};
+
+__global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a) {
+  const int b = blockIdx.y;
+  const float* __restrict__ src = a.src[b];
+  if (src == nullptr) return;
+  float inv;
+  const float s = h3_scale(__uint_as_float(a.amax[b]), inv);
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.inv_scale[b] = inv;
+  const long items = static_cast<long>(a.rows) * a.r / 8;
+  const long item = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
+  if (item >= items) return;
+  const int ln = static_cast<int>(item & 63);
+  const long grp = item >> 6;
+  const int t = ln & 15, g = ln >> 4;
+  const int RB = a.r / 16;
+  const long blk = grp / RB;
+  const int cb = static_cast<int>(grp - blk * RB);
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = a.kmap == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
+    v[e] = src[(blk * 32 + k) * a.r + 16 * cb + t];
+  }
+  Split2h sp;
+  split2h(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, s, sp);
+  f16x8* d = a.dst + b * a.stride + (grp * 2) * 64 + ln;
+  d[0] = sp.hi;
+  d[64] = sp.lo;
+}
+
+// ---- pass B, not transposed (R = M^T P), h3 products.  Geometry and loads of
+// colproj_x6_kernel; the roles are swapped so the streamed M is the B operand: lane
+// (t, g) holds column CT t + c of rows 8 g + e, i.e. B[k = 8 g + e][col t], and the
+// per-step scale of that column is the max over the four lanes (t, g = 0..3).  The
+// pre-split P is the A operand (A[row j = 16 cb + t'][k]), one scale per matrix.  Each
+// step's product lands in a fresh accumulator D[j][col] (lane (t, g): R rows CT t + c,
+// r columns 16 cb + 4 g + q) and is added as acc += D / s_col.
+template <int RB, int NW, int CT>
+__global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : 2) colproj_h3_kernel(const ProjArgs a) {
+  constexpr int R = 16 * RB;
+  constexpr int NQ = RB * 2 * 64;  // f16x8 units of one K-step's P split
+  __shared__ f16x8 tq[2][NQ];
+  const BlockXYZ blk = xcd_block_col();
+  const int b = blk.z;
+  const int kc = blk.y;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int col_base = blk.x * (16 * CT * NW) + wave * (16 * CT);
+  const int i_begin = kc * a.kchunk;
+  const int i_end = min(a.rows, i_begin + a.kchunk);
+  const float* __restrict__ M = a.m[b] + static_cast<long>(8 * g) * a.ld_m + col_base + CT * t;
+
+  f32x4 acc[CT][RB];
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
+  SplitCopyN<NQ, 64 * NW> TA;
+  constexpr int PD = kColX6PD;
+  ColStepX6<CT> S[PD];
+#pragma unroll
+  for (int k = 0; k < PD - 1; ++k)
+    if (i_begin + 32 * k < i_end) cpx_load<CT>(S[k], M, a.ld_m, i_begin + 32 * k);
+  split_copy_load_n(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
+  split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
+  __syncthreads();
+  int cur = 0;
+  for (int i0 = i_begin; i0 < i_end; i0 += 32 * PD) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      const int i = i0 + 32 * k;
+      if (i >= i_end) break;
+      const bool more = i + 32 < i_end;
+      if (i + 32 * (PD - 1) < i_end) cpx_load<CT>(S[(k + PD - 1) % PD], M, a.ld_m, i + 32 * (PD - 1));
+      if (more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
+      {
+        const ColStepX6<CT>& X = S[k];
+        Split2h B[CT];
+        float inv[CT];
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          const f32x4 lo4{X.x[0][c], X.x[1][c], X.x[2][c], X.x[3][c]};
+          const f32x4 hi4{X.x[4][c], X.x[5][c], X.x[6][c], X.x[7][c]};
+          float m8 = max8abs(lo4, hi4);
+          m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
+          m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
+          const float s = h3_scale(m8, inv[c]);
+          split2h(lo4, hi4, s, B[c]);
+        }
+#pragma unroll
+        for (int cb = 0; cb < RB; ++cb) {
+          Split2h A;
+          A.hi = tq[cur][(cb * 2 + 0) * 64 + lane];
+          A.lo = tq[cur][(cb * 2 + 1) * 64 + lane];
+#pragma unroll
+          for (int c = 0; c < CT; ++c) {
+            const f32x4 d = mfma3h(A, B[c], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[c][cb][q] = fmaf(d[q], inv[c], acc[c][cb][q]);
+          }
+        }
+      }
+      if (!more) break;
+      split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // P's per-matrix scale, then lane (t, g): R row CT t + c, columns 16 cb + 4 g .. + 3
+  const float ps = a.tinv[b];
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(col_base + CT * t + c) * R + 16 * cb + 4 * g) =
+          acc[c][cb] * ps;
+}
+
+// ============================================================================
 // host side
 // ============================================================================
 namespace {
@@ -3035,7 +3241,34 @@ int rank_stream_variant() {
 }
 
 // pre-split thin operand of the x6 projections (rows = the contraction index)
-size_t thin_presplit_bytes(int rows, int r, int batch) { return static_cast<size_t>(rows) * r * 6 * batch; }
+size_t thin_presplit_bytes(int rows, int r, int batch) { return static_cast<size_t>(rows) * r * 6 * batch + 1024; }
+
+// pass B through the fp16x3 column kernel (colproj_h3_kernel) instead of bf16x6 (tuning knob)
+#ifndef DION_PB_H3
+#define DION_PB_H3 1
+#endif
+// columns per lane of colproj_h3_kernel (2: 8-byte loads, 4: 16-byte loads; tuning knob)
+#ifndef DION_COLH3_CT
+#define DION_COLH3_CT 4
+#endif
+constexpr int kColH3CT = DION_COLH3_CT;
+// r > 64 (RB = 8) keeps 2 columns per lane: 4 would need 256+ VGPRs (one wave per SIMD)
+constexpr int colh3_ct(int r) { return r > 64 ? 2 : kColH3CT; }
+bool colh3_ok(int rows, int cols, int r) {
+  return DION_PB_H3 && rows % 32 == 0 && cols % (16 * colh3_ct(r) * kColX6NW) == 0;
+}
+Geo colh3_geo(int rows, int cols, int batch, int r) {
+  Geo g;
+  g.gx = static_cast<int>(ceil_div(cols, 16 * colh3_ct(r) * kColX6NW));
+  long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
+  long maxc = ceil_div(rows, 256);
+  long nc = want < maxc ? want : maxc;
+  if (nc < 1) nc = 1;
+  g.kchunk = round_up(ceil_div(rows, nc), 32);
+  g.nchunk = static_cast<int>(ceil_div(rows, g.kchunk));
+  g.out_rows = cols;
+  return g;
+}
 
 // pre-split streamed factor P (m_P x r per matrix) of the rank-update kernels
 size_t ef_presplit_bytes(int mp, int r, int batch) { return static_cast<size_t>(mp) * r * 6 * batch; }
@@ -3160,17 +3393,52 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
   const bool x6 = fast && gdt == DION_DTYPE_NONE &&
                   (row_mode ? rows % (64 * kRBE) == 0
                             : (rows % 32 == 0 && cols % ((r >= 64 ? 32 : 64) * kColX6NW) == 0));
+  const bool h3 = fast && gdt == DION_DTYPE_NONE && !row_mode && colh3_ok(rows, cols, r);
   const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, x6 ? 64 * kRBE : (fast ? 64 * kRB : 128))
+                 : h3      ? colh3_geo(rows, cols, batch, r)
                  : x6      ? colx6_geo(rows, cols, batch, r)
                            : colproj_geo(rows, cols, batch, false);
   const size_t slab = (slab_bytes(geo, batch, r) + 255) / 256 * 256;
   const int thin_rows = row_mode ? cols : rows;  // the contraction index
-  const size_t need = slab + (x6 ? thin_presplit_bytes(thin_rows, r, batch) : 0);
+  const size_t need = slab + ((x6 || h3) ? thin_presplit_bytes(thin_rows, r, batch) : 0);
   if (need > ws_bytes || (need > 0 && ws == nullptr))
     return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
   ProjArgs a;
   memset(&a, 0, sizeof(a));
-  if (x6) {
+  if (h3) {
+    // fp16x3: the thin operand's per-matrix |max|, then its two fp16 limbs
+    char* base = static_cast<char*>(ws) + slab;
+    const long per = static_cast<long>(thin_rows) * r;
+    const size_t sbytes = (static_cast<size_t>(per) * 4 * batch + 255) / 256 * 256;
+    uint32_t* amax = reinterpret_cast<uint32_t*>(base + sbytes);
+    float* inv = reinterpret_cast<float*>(base + sbytes + 256);
+    hipError_t me = hipMemsetAsync(amax, 0, sizeof(uint32_t) * batch, st);
+    if (me != hipSuccess) return fail(DION_E_LAUNCH, "memset: %s", hipGetErrorString(me));
+    AbsMaxArgs ma;
+    memset(&ma, 0, sizeof(ma));
+    for (int b = 0; b < batch; ++b) ma.src[b] = thin[b];
+    ma.out = amax;
+    ma.count = per;
+    const long mblocks = ceil_div(per, 256) < 64 ? ceil_div(per, 256) : 64;
+    hipLaunchKernelGGL(absmax_kernel, dim3(static_cast<unsigned>(mblocks), batch), dim3(256), 0, st, ma);
+    Presplit16Args pa;
+    memset(&pa, 0, sizeof(pa));
+    for (int b = 0; b < batch; ++b) pa.src[b] = thin[b];
+    pa.dst = reinterpret_cast<f16x8*>(base);
+    pa.amax = amax;
+    pa.inv_scale = inv;
+    pa.stride = per / 8 * 2;
+    pa.rows = thin_rows;
+    pa.r = r;
+    pa.kmap = 0;
+    const dim3 pgrid(static_cast<unsigned>(ceil_div(per / 8, 256)), batch);
+    hipLaunchKernelGGL(presplit16_kernel, pgrid, dim3(256), 0, st, pa);
+    int rc = check_launch("presplit16(thin)");
+    if (rc != DION_OK) return rc;
+    a.tsplit = pa.dst;
+    a.ts_stride = pa.stride;
+    a.tinv = inv;
+  } else if (x6) {
     // the thin operand split into bf16 limbs once per call, in the MFMA B-operand layout
     PresplitArgs pa;
     memset(&pa, 0, sizeof(pa));
@@ -3215,6 +3483,8 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
       constexpr int GD = decltype(Gc)::value;
       if (x6 && row_mode)
         hipLaunchKernelGGL((rowproj_x6_kernel<RB>), grid, dim3(256), 0, st, a);
+      else if (h3)
+        hipLaunchKernelGGL((colproj_h3_kernel<RB, kColX6NW, colh3_ct(16 * RB)>), grid, dim3(64 * kColX6NW), 0, st, a);
       else if (x6)
         hipLaunchKernelGGL((colproj_x6_kernel<RB, kColX6NW>), grid, dim3(64 * kColX6NW), 0, st, a);
       else if (fast && row_mode)
@@ -3452,6 +3722,8 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
         } else {
           const size_t nx = slab_bytes(colx6_geo(d->m, d->n, chunk, d->r), chunk, d->r);
           if (nx > n) n = nx;
+          const size_t nh = slab_bytes(colh3_geo(d->m, d->n, chunk, d->r), chunk, d->r);
+          if (nh > n) n = nh;
         }
         if (op == DION_OP_PROJECT_R)
           n = (n + 255) / 256 * 256 + thin_presplit_bytes(row_mode ? d->n : d->m, d->r, chunk);
