@@ -41,7 +41,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 7
+#define DION_ABI_VERSION 8
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -149,6 +149,25 @@ int dion_project_r(const DionBatchDesc* desc, const float* const* M, const float
 int dion_fixup_colnorm(const DionBatchDesc* desc, float* P, float* R, float* const* Q,
                        const uint32_t* nonzero, float eps, void* ws, size_t ws_bytes,
                        dion_stream_t stream);
+
+/*
+ * The column norm split in two for the FS ("fsdp") kernel kind, where every rank holds a
+ * shard of R's rows and the sums of squares are all-reduced over the FS group between
+ * the halves (q_norm_group, runtime.py:965-1013):
+ *
+ * dion_fixup_colsum: the fix-up of dion_fixup_colnorm on P and R (in place; the zero
+ * test is the caller's local shard, as the reference's local M_batch) and
+ *   colsum[b][c] = sum_rows R_b[.][c]^2            (fp32, fixed order; kernels.py:207-210)
+ * `colsum` is (batch, r) fp32; scratch = dion_workspace_bytes(DION_OP_FIXUP_COLNORM).
+ *
+ * dion_colnorm_apply:  Q_b <- R_b / (sqrt(colsum_b) + eps)   (kernels.py:279-290;
+ * bf16 state: the quotient rounded to bf16).  `colsum` is the reduced (batch, r) sum.
+ */
+int dion_fixup_colsum(const DionBatchDesc* desc, float* P, float* R, const void* const* Q,
+                      const uint32_t* nonzero, float* colsum, void* ws, size_t ws_bytes,
+                      dion_stream_t stream);
+int dion_colnorm_apply(const DionBatchDesc* desc, const float* R, void* const* Q, const float* colsum,
+                       float eps, dion_stream_t stream);
 
 /*
  * Error feedback + weight update (kernels.py:54-154, 229-276; runtime.py:1105-1113):

@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # DION_LIB_PATH: load another build of the same ABI (kernel-variant A/B runs during tuning)
 LIB_PATH = os.environ.get("DION_LIB_PATH") or os.path.join(HERE, "csrc", "libdion_codec.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -42,6 +42,8 @@ EXPORTED = (
     "dion_orthonormalize",
     "dion_project_r",
     "dion_fixup_colnorm",
+    "dion_fixup_colsum",
+    "dion_colnorm_apply",
     "dion_ef_apply",
     "dion_round_bf16",
     "dion_grad_sum_sq",
@@ -90,6 +92,8 @@ _SIGNATURES = {
                             ctypes.c_int),
     "dion_project_r": ([_DESC, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_fixup_colnorm": ([_DESC, _P, _P, _PP, _P, ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "dion_fixup_colsum": ([_DESC, _P, _P, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "dion_colnorm_apply": ([_DESC, _P, _PP, _P, ctypes.c_float, _P], ctypes.c_int),
     "dion_ef_apply": ([_DESC, _PP, _PP, _P, _P, _PP, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                        ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_round_bf16": ([_P, ctypes.c_int64, _P], ctypes.c_int),

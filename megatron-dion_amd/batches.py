@@ -19,7 +19,7 @@ from typing import Callable, Dict, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
-from .types import DionBatch, DionBatchCollectives, DionBatchEntry, DionBatchGroup
+from .types import DionAxisCollective, DionBatch, DionBatchCollectives, DionBatchEntry, DionBatchGroup
 
 
 def _norm_dim(dim, has_axis: bool) -> int:
@@ -77,20 +77,39 @@ def _group_key(bg: DionBatchGroup) -> tuple:
             tuple(_ranks(g) for g in bg.sync_groups))
 
 
-def resolve_dp_batch_group(config, *, replicate_group, group_size: Callable) -> DionBatchGroup:
-    """DP/RP-only form of resolve_batch_group (batches.py:496-603): no TP/FS axes."""
-    if getattr(config, "use_tp_shard", False) or getattr(config, "use_fs_shard", False):
-        raise RuntimeError("[DION_UNSUPPORTED_SHARDING] TP/FS-sharded Dion params are outside the DP codec path")
+def resolve_dp_batch_group(config, *, replicate_group, group_size: Callable, fs_group=None) -> DionBatchGroup:
+    """resolve_batch_group (batches.py:496-603) for the DP/RP and FS axes (no TP).
+
+    An FS-sharded entry with an FS group of size > 1 gets the "fsdp" kind: batch size = FS
+    world, q_norm group = FS group, and with low-rank sync over replicas the
+    low_rank_replicate_group (:571-603).  Everything else is "ddp" over the replicate group."""
+    if getattr(config, "use_tp_shard", False):
+        raise RuntimeError("[DION_UNSUPPORTED_SHARDING] TP-sharded Dion params are outside this codec's path")
     world = group_size(replicate_group) if replicate_group is not None else 1
-    sync = (replicate_group,) if (config.use_low_rank_sync and replicate_group is not None and world > 1) else ()
+    sync = [replicate_group] if (config.use_low_rank_sync and replicate_group is not None and world > 1) else []
+    if bool(getattr(config, "use_fs_shard", False)):
+        if fs_group is None:
+            raise RuntimeError("[DION_MISSING_BATCH_FS_GROUP] an FS-sharded Dion param needs its FS group")
+        fs_world = group_size(fs_group)
+        if fs_world > 1:
+            sync.append(fs_group)
+            low = replicate_group if (config.use_low_rank_sync and replicate_group is not None and world > 1) else None
+            return DionBatchGroup(kernel_kind="fsdp", replicate_group=replicate_group, q_norm_group=fs_group,
+                                  low_rank_replicate_group=low, batch_world_size=int(fs_world),
+                                  sync_groups=tuple(sync))
     return DionBatchGroup(kernel_kind="ddp", replicate_group=replicate_group, batch_world_size=int(world),
-                          sync_groups=sync)
+                          sync_groups=tuple(sync))
 
 
 def build_dion_batches(*, dion_params: Sequence, get_replicate_group: Callable,
                        group_size: Callable = None, batch_key_cache: Optional[dict] = None,
-                       **_unused) -> List[DionBatch]:
-    """Group, order, chunk and pad routed Dion params into DionBatch objects."""
+                       resolve_fs_group_from_meta: Optional[Callable] = None, **_unused) -> List[DionBatch]:
+    """Group, order, chunk and pad routed Dion params into DionBatch objects.
+
+    FS-sharded params (config.use_fs_shard) take their FS group from
+    `resolve_fs_group_from_meta(dist_meta, expect_group=True)` (batches.py:971 takes the same
+    callback) and form "fsdp" batches of FS-world entries with an FS collective covering every
+    entry (build_batch_collectives, batches.py:606-770)."""
     group_size = group_size or (lambda g: dist.get_world_size(g))
     replicate_group = get_replicate_group()
     grouped: Dict[tuple, list] = {}
@@ -102,7 +121,11 @@ def build_dion_batches(*, dion_params: Sequence, get_replicate_group: Callable,
         local_shape = state.get("local_shape") or tuple(sp.param.shape)
         global_shape = state.get("global_shape") or getattr(meta, "global_shape", None)
         per_expert = state.get("per_expert_global_shape") or getattr(meta, "per_expert_global_shape", None)
-        bg = resolve_dp_batch_group(cfg, replicate_group=replicate_group, group_size=group_size)
+        fs_group = None
+        if bool(getattr(cfg, "use_fs_shard", False)):
+            fs_group = resolve_fs_group_from_meta(meta, expect_group=True) if resolve_fs_group_from_meta \
+                else getattr(meta, "fs_group", None)
+        bg = resolve_dp_batch_group(cfg, replicate_group=replicate_group, group_size=group_size, fs_group=fs_group)
         key = (build_batch_key(local_shape, cfg, sp.grad.dtype, global_shape=global_shape,
                                per_expert_global_shape=per_expert,
                                tensor_row_shard_sizes=getattr(meta, "tensor_row_shard_sizes", None),
@@ -135,9 +158,14 @@ def build_dion_batches(*, dion_params: Sequence, get_replicate_group: Callable,
                     optim_group=tmpl.optim_group, config=tmpl.config, dist_meta=None,
                     momentum=torch.zeros_like(tmpl.momentum), q_tensor=torch.zeros_like(tmpl.q_tensor),
                     param_shape=tmpl.param_shape))
+            coll = DionBatchCollectives()
+            if bg.kernel_kind == "fsdp":
+                fs = bg.q_norm_group
+                coll = DionBatchCollectives(fs_collective=DionAxisCollective(
+                    indices=tuple(range(size)), process_group=fs, world_size=int(group_size(fs)),
+                    rank=int(dist.get_rank(fs))))
             batches.append(DionBatch(batch_key=key, entries=tuple(entries), real_batch_size=real,
-                                     batch_cache_key=cache_key, batch_group=bg,
-                                     batch_collectives=DionBatchCollectives()))
+                                     batch_cache_key=cache_key, batch_group=bg, batch_collectives=coll))
             cache_key += real
     return batches
 

@@ -217,6 +217,35 @@ class HipDionCodec:
                                          self._stream())
         _lib.check(rc, "dion_fixup_colnorm")
 
+    def fixup_colsum(self, P: torch.Tensor, R: torch.Tensor, qs: List[torch.Tensor], nonzero: torch.Tensor,
+                     colsum: torch.Tensor, m: int, n: int, transposed: bool) -> None:
+        """FS kind, first half of the column norm: fix-up of P and R (kernels.py:157-204, local zero
+        test) and the local fp32 column sums of squares of R into colsum (B, r)
+        (kernels.py:207-210).  The caller all-reduces colsum over the FS group."""
+        B = len(qs)
+        if B == 0:
+            return
+        r = int(P.shape[2])
+        if colsum.dtype != torch.float32 or not colsum.is_contiguous() or colsum.numel() < B * r:
+            raise RuntimeError("[DION_BAD_COLSUM] colsum must be a contiguous fp32 (batch, r) buffer")
+        d = self._desc(B, m, n, r, transposed, state_dtype=_state_dtype(None, qs))
+        ws = self.workspace(d, _lib.OP_FIXUP_COLNORM)
+        rc = self.lib.dion_fixup_colsum(ctypes.byref(d), P.data_ptr(), R.data_ptr(), _ptrs(qs), nonzero.data_ptr(),
+                                        colsum.data_ptr(), ws.data_ptr(), ws.numel(), self._stream())
+        _lib.check(rc, "dion_fixup_colsum")
+
+    def colnorm_apply(self, R: torch.Tensor, qs: List[torch.Tensor], colsum: torch.Tensor, eps: float,
+                      m: int, n: int, transposed: bool) -> None:
+        """FS kind, second half: Q_b <- R_b / (sqrt(colsum_b) + eps) (kernels.py:279-290)."""
+        B = len(qs)
+        if B == 0:
+            return
+        r = int(R.shape[2])
+        d = self._desc(B, m, n, r, transposed, state_dtype=_state_dtype(None, qs))
+        rc = self.lib.dion_colnorm_apply(ctypes.byref(d), R.data_ptr(), _ptrs(qs), colsum.data_ptr(), float(eps),
+                                         self._stream())
+        _lib.check(rc, "dion_colnorm_apply")
+
     def ef_apply(self, momentums: Optional[List[torch.Tensor]], params: Optional[List[torch.Tensor]],
                  P: torch.Tensor, R: torch.Tensor, qs: List[torch.Tensor], nonzero: torch.Tensor,
                  mu: float, lr: float, wd: float, scaled_lr: float, transposed: bool) -> None:

@@ -1341,6 +1341,46 @@ __global__ void __launch_bounds__(256) colnorm_apply_kernel(const FixArgs a) {
   }
 }
 
+// FS column norm, first half: the chunk partials of fixup_partial_kernel summed in fixed order
+__global__ void __launch_bounds__(256) colsum_reduce_kernel(const FixArgs a, float* __restrict__ colsum) {
+  const int b = blockIdx.x;
+  for (int c = threadIdx.x; c < a.r; c += 256) {
+    float s = 0.f;
+    const float* pp = a.part + static_cast<long>(b) * a.nchunk * a.r + c;
+    for (int k = 0; k < a.nchunk; ++k) s += pp[static_cast<long>(k) * a.r];
+    colsum[static_cast<long>(b) * a.r + c] = s;
+  }
+}
+
+// FS column norm, second half: Q <- R / (sqrt(colsum) + eps) with the all-reduced sums
+__global__ void __launch_bounds__(256) colnorm_given_kernel(const FixArgs a, const float* __restrict__ colsum) {
+  __shared__ float denom[256];
+  const int b = blockIdx.y, ch = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int r = a.r, nq = a.nq, tpc = a.tpc;
+  if (tid < r) denom[tid] = sqrtf(colsum[static_cast<long>(b) * r + tid]) + a.eps;
+  __syncthreads();
+  const float* R = a.R + static_cast<long>(b) * nq * r;
+  float* Q = a.q[b];
+  const int c = tid % r, p = tid / r;
+  const int row0 = ch * a.rows_per_chunk;
+  const int row1 = min(nq, row0 + a.rows_per_chunk);
+  if (p < tpc) {
+    const float d = denom[c];
+    for (int row = row0 + p; row < row1; row += tpc) {
+      const long idx = static_cast<long>(row) * r + c;
+      if (a.q_bf16) {
+        const uint32_t u = __float_as_uint(R[idx] / d);
+        reinterpret_cast<uint16_t*>(Q)[idx] = ((u & 0x7FFFFFFFu) > 0x7F800000u)
+                                                  ? static_cast<uint16_t>((u >> 16) | 0x40u)
+                                                  : static_cast<uint16_t>((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+      } else {
+        Q[idx] = R[idx] / d;
+      }
+    }
+  }
+}
+
 // P <- z ? 0 : nan_to_num(P) for the real entries (kernels.py:185-188)
 __global__ void __launch_bounds__(256) pfix_kernel(float* __restrict__ P, const uint32_t* __restrict__ nonzero,
                                                    long per_entry, int batch) {
@@ -4042,6 +4082,87 @@ int dion_fixup_colnorm(const DionBatchDesc* d, float* P, float* R, float* const*
     if (rc != DION_OK) return rc;
     hipLaunchKernelGGL(colnorm_apply_kernel, dim3(a.nchunk, nb), dim3(256), 0, st, a);
     rc = check_launch("fixup_colnorm");
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_fixup_colsum(const DionBatchDesc* d, float* P, float* R, const void* const* Q, const uint32_t* nonzero,
+                      float* colsum, void* ws, size_t ws_bytes, dion_stream_t stream) {
+  int rc = validate(d);
+  if (rc != DION_OK) return rc;
+  if (P == nullptr || R == nullptr || Q == nullptr || nonzero == nullptr || colsum == nullptr)
+    return fail(DION_E_INVALID, "null argument");
+  if (d->batch == 0) return DION_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int mp = d->transposed ? d->n : d->m;
+  const int nq = d->transposed ? d->m : d->n;
+  const int r = d->r;
+  {
+    const long per = static_cast<long>(mp) * r;
+    long blocks = ceil_div(per * d->batch, 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(pfix_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, P, nonzero, per, d->batch);
+    rc = check_launch("pfix");
+    if (rc != DION_OK) return rc;
+  }
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    FixArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int b = 0; b < nb; ++b) {
+      if (Q[b0 + b] == nullptr) return fail(DION_E_INVALID, "null Q at %d", b0 + b);
+      a.q[b] = static_cast<float*>(const_cast<void*>(Q[b0 + b]));
+    }
+    a.q_bf16 = d->m_dtype == DION_DTYPE_BF16 ? 1 : 0;
+    a.R = R + static_cast<long>(b0) * nq * r;
+    a.nonzero = nonzero + b0;
+    a.nq = nq;
+    a.r = r;
+    a.tpc = 256 / r;
+    a.rows_per_chunk = 256;
+    a.nchunk = static_cast<int>(ceil_div(nq, a.rows_per_chunk));
+    if (ws_bytes < sizeof(float) * static_cast<size_t>(nb) * a.nchunk * r || ws == nullptr)
+      return fail(DION_E_WORKSPACE, "fixup needs %zu workspace bytes", sizeof(float) * static_cast<size_t>(nb) * a.nchunk * r);
+    a.part = static_cast<float*>(ws);
+    hipLaunchKernelGGL(fixup_partial_kernel, dim3(a.nchunk, nb), dim3(256), 0, st, a);
+    rc = check_launch("fixup_partial");
+    if (rc != DION_OK) return rc;
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(nb), dim3(256), 0, st, a, colsum + static_cast<long>(b0) * r);
+    rc = check_launch("colsum_reduce");
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_colnorm_apply(const DionBatchDesc* d, const float* R, void* const* Q, const float* colsum, float eps,
+                       dion_stream_t stream) {
+  int rc = validate(d);
+  if (rc != DION_OK) return rc;
+  if (R == nullptr || Q == nullptr || colsum == nullptr) return fail(DION_E_INVALID, "null argument");
+  if (d->batch == 0) return DION_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int nq = d->transposed ? d->m : d->n;
+  const int r = d->r;
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    FixArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int b = 0; b < nb; ++b) {
+      if (Q[b0 + b] == nullptr) return fail(DION_E_INVALID, "null Q at %d", b0 + b);
+      a.q[b] = static_cast<float*>(Q[b0 + b]);
+    }
+    a.q_bf16 = d->m_dtype == DION_DTYPE_BF16 ? 1 : 0;
+    a.R = const_cast<float*>(R) + static_cast<long>(b0) * nq * r;
+    a.nq = nq;
+    a.r = r;
+    a.tpc = 256 / r;
+    a.rows_per_chunk = 256;
+    a.nchunk = static_cast<int>(ceil_div(nq, a.rows_per_chunk));
+    a.eps = eps;
+    hipLaunchKernelGGL(colnorm_given_kernel, dim3(a.nchunk, nb), dim3(256), 0, st, a,
+                       colsum + static_cast<long>(b0) * r);
+    rc = check_launch("colnorm_given");
     if (rc != DION_OK) return rc;
   }
   return DION_OK;

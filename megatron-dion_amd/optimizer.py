@@ -365,7 +365,8 @@ def is_dion_param(param: torch.Tensor, name: str = "") -> bool:
 
 
 def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str, torch.Tensor]],
-                      replicate_group=None, base_seed: int = 0, dion_predicate=None) -> Dict[str, torch.Tensor]:
+                      replicate_group=None, base_seed: int = 0, dion_predicate=None, fs_group=None,
+                      fs_shards: Optional[Dict[str, tuple]] = None) -> Dict[str, torch.Tensor]:
     """Stand-alone adapter: state init + `route_step_params` for plain data parallelism.
 
     Plays the part of the reference's DionDistributedOptimizer routing
@@ -377,6 +378,11 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
     replicas (only Dion buckets skip the replica all-reduce,
     param_and_grad_buffer.py:649-698).  G of each step is taken from `param.main_grad` (Megatron's grad
     buffer view, bf16 or fp32) when present, else from `param.grad`.
+
+    FS sharding (the reference's default topology, FS = DP): `fs_shards[name] =
+    (global_shape, fs_shard_dim, start, end)` marks `param` as this rank's shard of a matrix
+    sharded over `fs_group` (distrib_dion/parameter.py:424-466); those params form "fsdp"
+    batches of FS-world entries.
     """
     group = optimizer.param_groups[0]
     rf = float(group.get("rank_fraction", optimizer.defaults["rank_fraction"]))
@@ -391,15 +397,23 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
             continue
         dion_named.append((name, p))
         mpc = optimizer._mixed_precision_config
+        spec = (fs_shards or {}).get(name)
+        fs_world = int(dist.get_world_size(fs_group)) if (spec is not None and fs_group is not None) else 1
         state, cfg = init_dion_state(p, rank_fraction=rf, rank_multiple_of=mult, base_seed=base_seed,
                                      param_uid=(name,), param_name=name,
                                      momentum_dtype=_as_dtype(getattr(mpc, "momentum_dtype", None)),
                                      q_dtype=_as_dtype(getattr(mpc, "q_dtype", None)),
-                                     use_low_rank_sync=optimizer.use_low_rank_sync)
+                                     use_low_rank_sync=optimizer.use_low_rank_sync,
+                                     fs_shard=None if spec is None else (tuple(spec[0]), spec[1], spec[2], spec[3],
+                                                                         fs_world))
         optimizer.state[p].update(state)
-        metas[name] = (cfg, DionDistMeta(shape=tuple(p.shape), global_shape=tuple(p.shape), rank_fraction=rf,
-                                         is_transposed=cfg.is_transposed, param_uid=(name,), is_dion_param=True,
-                                         param_name=name, param_config=cfg))
+        meta = DionDistMeta(shape=tuple(p.shape), global_shape=tuple(state["global_shape"]), rank_fraction=rf,
+                            is_transposed=cfg.is_transposed, param_uid=(name,), is_dion_param=True,
+                            param_name=name, param_config=cfg, local_shape=tuple(p.shape))
+        if spec is not None:
+            meta.extra.update(fs_group=fs_group, fs_shard_dim=int(spec[1]), fs_start_idx=int(spec[2]),
+                              fs_end_idx=int(spec[3]), fs_world_size=fs_world)
+        metas[name] = (cfg, meta)
     ordered = sorted(dion_named, key=lambda kv: kv[0])
 
     def grad_of(p):
@@ -417,7 +431,8 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
                                        optim_group=group_of.get(id(p), group), config=cfg, dist_meta=meta))
         batches = build_dion_batches(
             dion_params=steps, get_replicate_group=lambda: replicate_group,
-            group_size=lambda g: dist.get_world_size(g))
+            group_size=lambda g: dist.get_world_size(g),
+            resolve_fs_group_from_meta=lambda meta, expect_group=True: meta.extra.get("fs_group"))
         elementwise = []
         for _, p in ew_named:
             g = grad_of(p)

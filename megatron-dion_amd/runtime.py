@@ -76,8 +76,10 @@ def _group_world(group) -> int:
 
 
 def is_replicated(batch) -> bool:
-    """True when the batch exchanges factors with replicas (replicate group size > 1)."""
-    return _group_world(getattr(getattr(batch, "batch_group", None), "replicate_group", None)) > 1
+    """True when the batch exchanges factors with other ranks: replicas (replicate group size > 1)
+    or FS shards (the "fsdp" kind)."""
+    bg = getattr(batch, "batch_group", None)
+    return _group_world(getattr(bg, "replicate_group", None)) > 1 or str(getattr(bg, "kernel_kind", "ddp")) == "fsdp"
 
 
 def validate_update_contract(optimizer, *, optim_groups, optimizer_states, dist_metas, param_shapes,
@@ -121,8 +123,9 @@ def check_supported_batch(optimizer, *, batch_group, batch_collectives, configs,
     whose entries are FS row/column shards or TP shards, with FS/TP collectives attached
     (types.py:149-158) and a q_norm / ortho group.  Treating those shards as whole matrices
     would orthonormalise and normalise a local piece while scaling the LR by the global
-    shape: wrong updates with no error.  Only the whole-matrix data-parallel kind ("ddp",
-    runtime.py:1379-1496) is computed here; anything else raises
+    shape: wrong updates with no error.  Computed here: the whole-matrix data-parallel kind
+    ("ddp", runtime.py:1379-1496) and the FS kind without TP ("fsdp", runtime.py:1201-1293,
+    1729-1795); anything else (TP-sharded P / Q, "fsdp_tp") raises
     [DION_UNSUPPORTED_KERNEL_KIND]."""
     def world(g):
         try:
@@ -132,28 +135,44 @@ def check_supported_batch(optimizer, *, batch_group, batch_collectives, configs,
 
     kind = str(getattr(batch_group, "kernel_kind", "ddp"))
     why = None
-    if kind != "ddp":
+    tp_colls = batch_collectives is not None and any(
+        len(tuple(getattr(batch_collectives, f, None) or ())) for f in ("tp_q_gathers", "tp_r_collectives",
+                                                                         "tp_q_reshards"))
+    if kind not in ("ddp", "fsdp"):
         why = f"kernel_kind={kind!r}"
     elif getattr(batch_group, "ortho_group", None) is not None and world(batch_group.ortho_group) > 1:
         why = "a distributed ortho_group (TP-sharded P)"
-    elif getattr(batch_group, "q_norm_group", None) is not None and world(batch_group.q_norm_group) > 1:
-        why = "a q_norm_group (FS-sharded column norm)"
-    elif batch_collectives is not None and (
-            getattr(batch_collectives, "fs_collective", None) is not None
-            or any(len(tuple(getattr(batch_collectives, f, None) or ())) for f in
-                   ("tp_q_gathers", "fs_p_collectives", "tp_r_collectives", "tp_q_reshards"))):
-        why = "FS/TP batch collectives"
+    elif tp_colls or any(bool(getattr(c, "use_tp_shard", False)) for c in configs[:int(real_batch_size)]):
+        why = "TP-sharded entries / TP batch collectives"
+    elif kind == "fsdp":
+        fs = getattr(batch_collectives, "fs_collective", None) if batch_collectives is not None else None
+        if fs is None or int(getattr(fs, "world_size", 1)) <= 1:
+            why = "an fsdp batch without its FS collective"
+        elif not all(bool(getattr(c, "use_fs_shard", False)) for c in configs[:int(real_batch_size)]):
+            why = "an fsdp batch with entries that are not FS shards"
+        elif len(param_shapes) != int(fs.world_size) or len(tuple(fs.indices)) != len(param_shapes):
+            why = f"fsdp batch size {len(param_shapes)} != FS world {fs.world_size} ([DION_FSONLY_BATCH_SIZE_MISMATCH])"
+        elif any(optimizer_states[i] is not None and getattr(optimizer_states[i].get("momentum"), "dtype", None)
+                 == torch.bfloat16 for i in range(int(real_batch_size))):
+            why = "bf16 momentum with the fsdp kind (not built)"
     else:
-        for i in range(int(real_batch_size)):
-            local = tuple(int(d) for d in param_shapes[i])
-            glob = _shape_of(dist_metas[i], optimizer_states[i], local)
-            if local != glob:
-                why = f"entry {i} is a shard: local shape {local} != global shape {glob}"
-                break
+        if getattr(batch_group, "q_norm_group", None) is not None and world(batch_group.q_norm_group) > 1:
+            why = "a q_norm_group on a ddp batch (FS-sharded column norm)"
+        elif batch_collectives is not None and (
+                getattr(batch_collectives, "fs_collective", None) is not None
+                or len(tuple(getattr(batch_collectives, "fs_p_collectives", None) or ()))):
+            why = "FS batch collectives on a ddp batch"
+        else:
+            for i in range(int(real_batch_size)):
+                local = tuple(int(d) for d in param_shapes[i])
+                glob = _shape_of(dist_metas[i], optimizer_states[i], local)
+                if local != glob:
+                    why = f"entry {i} is a shard: local shape {local} != global shape {glob}"
+                    break
     if why is not None:
         raise RuntimeError(
             f"[DION_UNSUPPORTED_KERNEL_KIND] step={optimizer._step_count}: {why}; this codec computes "
-            "whole-matrix data-parallel ('ddp') batches only (FS/TP-sharded Dion is not built)")
+            "whole-matrix data-parallel ('ddp') batches and FS-sharded ('fsdp') batches without TP")
 
 
 def _sketch_seed(optimizer, batch_cache_key: int, entry: int) -> int:
@@ -196,6 +215,11 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     use_low_rank = bool(optimizer.use_low_rank_sync) and W > 1 and any(
         bool(c.use_low_rank_sync) for c in configs)
     real_grads = [g for g in (grads or [])[:real]] if grads is not None else []
+    if str(getattr(batch_group, "kernel_kind", "ddp")) == "fsdp":
+        yield from _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, optim_groups, real_grads,
+                                    optimizer_states, param_shapes, real, batch_cache_key, batch_group,
+                                    batch_collectives, commit_updates, use_low_rank, sketches)
+        return
 
     if W > 1 and not use_low_rank and real_grads:
         # runtime.py:439-491: dense all-reduce of the gradients across replicas
@@ -377,6 +401,149 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         sink(P[:real], R[:real])
 
 
+def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, optim_groups, real_grads,
+                     optimizer_states, param_shapes, real, batch_cache_key, batch_group, batch_collectives,
+                     commit_updates, use_low_rank, sketches):
+    """One FS ("fsdp") batch: the reference's default Dion topology (FS = DP,
+    megatron/training/initialize.py:79-81).  Entry i of the batch is this rank's shard of
+    matrix i, sharded along fs_shard_dim, and the orientation puts the sharded dim on the
+    contraction side (dion/state.py:304-310), so P_local = X_local Q_local is a partial sum:
+
+      M += G (the local shard); P = X Q (partial)                      pass A, local
+      reduce-scatter(sum) over the FS group -> this rank's entry      runtime.py:1201-1216 / :1751-1757
+        (+ all-reduce(avg) over the replicate group with low-rank sync, :1218-1228)
+      orthonormalise it (zero for a padded entry), all-gather          :1229-1293 / :1758-1795
+      R = X^T P (this shard's rows of R)                               pass B, local
+        (+ all-reduce(avg) over the replicate group with low-rank sync, :1284-1291)
+      fix-up with this shard's zero test; local column sums of R^2, all-reduced (sum) over
+        the q_norm group (the FS group), Q = R / (sqrt(sum) + eps)     kernels.py:157-210, runtime.py:965-1013
+      error feedback on the shard; weight update with the GLOBAL shape's scaled LR  runtime.py:1015-1113
+    """
+    codec = optimizer.codec
+    fs = batch_collectives.fs_collective
+    fs_group, fs_world, fs_rank = fs.process_group, int(fs.world_size), int(fs.rank)
+    indices = tuple(int(i) for i in fs.indices)
+    if sorted(indices) != list(range(len(params))):
+        raise RuntimeError(f"[DION_FSONLY_GATHER_PERMUTATION_INVALID] batch_size={len(params)} indices={indices}")
+    rgroup = getattr(batch_group, "low_rank_replicate_group", None)
+    rworld = _group_world(rgroup)
+    group = getattr(batch_group, "replicate_group", None)
+    if not use_low_rank and _group_world(group) > 1 and real_grads:
+        # runtime.py:1553-1558 -> :439-491: dense all-reduce of the shard gradients across replicas
+        op = dist.ReduceOp.AVG if optimizer.defaults.get("rp_average_in_collective", True) else dist.ReduceOp.SUM
+        works = [dist.all_reduce(g, op=op, group=group, async_op=True) for g in real_grads]
+        yield
+        for w in works:
+            w.wait()
+    B = len(params)
+    m, n = (int(d) for d in param_shapes[0])
+    transposed = bool(configs[0].is_transposed)
+    r = int(Qs[0].shape[1])
+    mp, nq = factor_rows(m, n, transposed)
+    dev = momentums[0].device
+    oversample = float(optimizer.defaults["rcqr_oversample"])
+    P = torch.zeros((B, mp, r), dtype=torch.float32, device=dev)
+    nonzero = torch.zeros((B,), dtype=torch.int32, device=dev)
+    defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
+             and (commit_updates is None or all(c is None for c in commit_updates[:real]))
+             and codec.supports_deferred_ef(m, n, r, transposed))
+    _project_with_pending(codec, real_grads, momentums, Qs, P, nonzero, optimizer_states, real, m, n, transposed,
+                          defer)
+    # reduce-scatter(sum): this rank receives entry fs_rank summed over the FS shards
+    P_own = torch.empty((1, mp, r), dtype=torch.float32, device=dev)
+    work = dist.reduce_scatter_tensor(P_own, P, op=dist.ReduceOp.SUM, group=fs_group, async_op=True)
+    yield
+    work.wait()
+    if use_low_rank and rworld > 1:
+        work = dist.all_reduce(P_own, op=dist.ReduceOp.AVG, group=rgroup, async_op=True)  # runtime.py:367-369
+        yield
+        work.wait()
+    own = indices[fs_rank]
+    if own >= real or dist_metas[own] is None:
+        P_own.zero_()  # a padded entry stays inert (runtime.py:1242-1248)
+    else:
+        S = None if sketches is None else sketches.get(own)
+        codec.orthonormalize(P_own, m, n, transposed, _sketch_seed(optimizer, batch_cache_key, own), oversample,
+                             sketch=None if S is None else S.reshape(1, *S.shape[-2:]).contiguous(),
+                             state_dtype=momentums[0].dtype)
+    gathered = torch.empty_like(P)
+    work = dist.all_gather_into_tensor(gathered, P_own, group=fs_group, async_op=True)
+    yield
+    work.wait()
+    if indices == tuple(range(B)):
+        P = gathered
+    else:
+        for k, idx in enumerate(indices):
+            P[idx].copy_(gathered[k])
+    R = torch.zeros((B, nq, r), dtype=torch.float32, device=dev)
+    codec.project_r(list(momentums[:real]), P, R, transposed)
+    if use_low_rank and rworld > 1:
+        work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=rgroup, async_op=True)
+        yield
+        work.wait()
+    colsum = torch.empty((real, r), dtype=torch.float32, device=dev)
+    codec.fixup_colsum(P, R, list(Qs[:real]), nonzero, colsum, m, n, transposed)
+    qgroup = getattr(batch_group, "q_norm_group", None)
+    if qgroup is not None:
+        work = dist.all_reduce(colsum, op=dist.ReduceOp.SUM, group=qgroup, async_op=True)
+        yield
+        work.wait()
+    codec.colnorm_apply(R, list(Qs[:real]), colsum, float(optimizer.defaults["epsilon"]), m, n, transposed)
+    _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim_groups, optimizer_states,
+                   dist_metas, real, m, n, transposed, defer, commit_updates)
+
+
+def _project_with_pending(codec, real_grads, momentums, Qs, P, nonzero, optimizer_states, real, m, n, transposed,
+                          defer):
+    """Pass A: M (+ the pending error feedback of the previous step) += G; P = X Q."""
+    pending = [optimizer_states[i].pop(_PENDING_EF, None) if optimizer_states[i] is not None else None
+               for i in range(real)]
+    if any(p is not None for p in pending):
+        alphas = {p[2] for p in pending if p is not None}
+        if defer and len(alphas) == 1:
+            codec.project_p_ef(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed,
+                               [p[0] if p is not None else None for p in pending],
+                               [p[1] if p is not None else None for p in pending], alphas.pop())
+            return
+        for i, p in enumerate(pending):
+            if p is not None:
+                _apply_pending(codec, momentums[i], Qs[i], p, m, n, transposed)
+    codec.project_p(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed)
+
+
+def _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim_groups, optimizer_states,
+                   dist_metas, real, m, n, transposed, defer, commit_updates):
+    """Error feedback (now, or pending for the next pass A) and the weight update with the
+    global shape's scaled LR (runtime.py:1015-1113, kernels.py:25-51)."""
+    grp = optim_groups[0] or {}
+    st0 = optimizer_states[0] or {}
+    gshape = st0.get("per_expert_global_shape") or st0.get("global_shape") \
+        or getattr(dist_metas[0], "global_shape", None) or (m, n)
+    lr = float(grp.get("lr", optimizer.defaults["lr"]))
+    mu = float(grp.get("mu", optimizer.defaults["mu"]))
+    wd = float(grp.get("weight_decay", optimizer.defaults["weight_decay"] * float(grp.get("wd_mult", 1.0))))
+    rank_fraction = float(grp.get("rank_fraction", optimizer.defaults.get("rank_fraction", 0.25)))
+    scaled = scaled_lr_for_shape(lr=lr, m_global=int(gshape[0]), n_global=int(gshape[1]),
+                                 scale_mode=optimizer.defaults.get("scale_mode", "spectral"),
+                                 rank_fraction=rank_fraction,
+                                 extra_scale_factor=optimizer.defaults.get("extra_scale_factor", 0.2))
+    if defer:
+        codec.ef_apply(None, list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd, scaled, transposed)
+        for i in range(real):
+            optimizer_states[i][_PENDING_EF] = (P[i], R[i], -(1.0 - mu))
+    else:
+        codec.ef_apply(list(momentums[:real]), list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd,
+                       scaled, transposed)
+    if commit_updates is not None:
+        for i in range(real):
+            if commit_updates[i] is not None:
+                commit_updates[i](params[i], momentums[i])
+    optimizer._last_batch_factors = (P, R) if getattr(optimizer, "_keep_factors", False) else None
+    sink = getattr(optimizer, "_factor_sink", None)
+    if sink is not None:
+        sink(P[:real], R[:real])
+
+
 # optimizer-state key of a pending (deferred) error feedback: (P_b, R_b, alpha).  The
 # leading underscore keeps it out of the reference's persistent checkpoint state
 # (distrib_dion/checkpoint_io.py:247-266); MegatronDion.flush_error_feedback()
@@ -479,7 +646,7 @@ def coalesce_local_batches(batches, max_entries: int = 64):
     out = []
     for b in batches:
         bg = b.batch_group
-        if _group_world(getattr(bg, "replicate_group", None)) > 1 or int(b.real_batch_size) != len(b.params):
+        if is_replicated(b) or int(b.real_batch_size) != len(b.params):
             out.append(b)
             continue
         if out and isinstance(out[-1], DionBatch) and getattr(out[-1], "_coalesced", False) \

@@ -62,24 +62,44 @@ def init_q(q_global_shape: Tuple[int, int], seed: int, device, dtype=torch.float
 def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_of: int = 1,
                     base_seed: int = 0, param_uid=None, param_name: str = "",
                     momentum_dtype: Optional[torch.dtype] = None, q_dtype: Optional[torch.dtype] = None,
-                    use_low_rank_sync: bool = True) -> Tuple[dict, DionParamConfig]:
-    """Fresh optimizer state + config for one 2D parameter (no TP/FS sharding).
+                    use_low_rank_sync: bool = True, fs_shard=None) -> Tuple[dict, DionParamConfig]:
+    """Fresh optimizer state + config for one 2D parameter (no TP sharding).
 
+    `param` is the whole matrix, or with `fs_shard = (global_shape, fs_shard_dim, start, end,
+    fs_world)` this rank's FS shard of it (rows [start, end) for dim 0, columns for dim 1;
+    distrib_dion/parameter.py:424-466).  The rank r and the low-rank rule use the global shape
+    (state.py:159-230); the orientation follows the shard dim (dim 0 -> transposed, dim 1 ->
+    not, state.py:304-310) so the sharded dim is always the contraction side of P = X Q; Q is
+    the seeded global Q's rows [start, end) (state.py:50-109, the CPU stream).
     `momentum_dtype` / `q_dtype` follow DionMixedPrecisionConfig (dion/state.py:502-514,
     544-547): None keeps the parameter's dtype; the speedrun sets both to bf16."""
     if param.dim() != 2:
         raise RuntimeError(f"[DION_NOT_2D] shape={tuple(param.shape)}")
-    m, n = (int(d) for d in param.shape)
-    transposed = is_transposed_shape(m, n)
+    ml, nl = (int(d) for d in param.shape)
+    if fs_shard is None:
+        m, n = ml, nl
+        transposed = is_transposed_shape(m, n)
+        dim, start, end, fs_world = -1, 0, (n if not transposed else m), 1
+    else:
+        (m, n), dim, start, end, fs_world = fs_shard
+        m, n, dim = int(m), int(n), int(dim)
+        if dim not in (0, 1):
+            raise RuntimeError(f"[DION_BAD_FS_SHARD_DIM] fs_shard_dim={dim}")
+        if (ml, nl) != ((end - start, n) if dim == 0 else (m, end - start)):
+            raise RuntimeError(f"[DION_BAD_FS_SHARD] local {(ml, nl)} vs global {(m, n)} dim {dim} [{start}, {end})")
+        transposed = dim == 0
     r = rank_for_shape(m, n, rank_fraction, rank_multiple_of)
     q_shape = (m if transposed else n, r)
     seed = q_seed_from_param_key(base_seed=base_seed, param_uid=param_uid, param_name=param_name,
                                  q_global_shape=q_shape, is_transposed=transposed)
+    q = init_q(q_shape, seed, "cpu", dtype=q_dtype or param.dtype)
+    if fs_shard is not None:
+        q = q[start:end]
     state = {
         "momentum": torch.zeros_like(param, dtype=momentum_dtype or param.dtype),
-        "Q": init_q(q_shape, seed, param.device, dtype=q_dtype or param.dtype),
+        "Q": q.contiguous().to(param.device),
         "r": r,
-        "local_shape": (m, n),
+        "local_shape": (ml, nl),
         "global_shape": (m, n),
     }
     cfg = DionParamConfig(
@@ -87,4 +107,6 @@ def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_
         use_low_rank_sync=bool(use_low_rank_sync) and should_use_low_rank_sync(
             global_shape=(m, n), r_global=r, rank_fraction=rank_fraction),
     )
+    if fs_shard is not None:
+        cfg.has_fs_shard, cfg.use_fs_shard, cfg.fs_shard_dim = True, int(fs_world) > 1, dim
     return state, cfg

@@ -112,6 +112,16 @@ class DionBatchGroup:
 
 
 @dataclass
+class DionAxisCollective:
+    """One grouped FS/TP collective over a shared axis (types.py:140-147): the process group,
+    its size, this rank's index in it, and the batch entries it covers."""
+    indices: Tuple[int, ...] = ()
+    process_group: Any = None
+    world_size: int = 1
+    rank: int = 0
+
+
+@dataclass
 class DionBatchCollectives:
     """TP/FS collectives of a batch (types.py:149-158); empty on the pure DP path."""
     tp_q_gathers: Tuple[Any, ...] = ()

@@ -63,6 +63,19 @@ class OracleCodec:
         for b in range(B):
             qs[b].copy_(Qn[b])
 
+    def fixup_colsum(self, P, R, qs, nonzero, colsum, m, n, transposed):
+        B = len(qs)
+        Q = torch.stack(qs, 0)
+        zero = (nonzero[:B] == 0).view(B, 1, 1)
+        P[:B] = torch.where(zero, torch.zeros_like(P[:B]), P[:B].nan_to_num())
+        R[:B] = torch.where(zero, Q.nan_to_num().to(R.dtype), R[:B].nan_to_num())
+        colsum[:B] = R[:B].to(torch.float32).square().sum(dim=-2)
+
+    def colnorm_apply(self, R, qs, colsum, eps, m, n, transposed):
+        for b in range(len(qs)):
+            qn = R[b].to(torch.float32) / (colsum[b].sqrt() + eps)
+            qs[b].copy_(qn.to(qs[b].dtype))
+
     def ef_apply(self, momentums, params, P, R, qs, nonzero, mu, lr, wd, scaled_lr, transposed):
         dt = qs[0].dtype  # the state dtype: factors carry it (kernels.py:54-83, 229-276)
         for b in range(len(qs)):

@@ -24,6 +24,8 @@ Reference files (all under `/root/reference/megatron/core/optimizer/`):
   dion/kernels.py:207-210,279-290  column sum-of-squares + normalize_columns
   dion/kernels.py:229-276 + runtime.py:1105-1132  weight update and Q commit
   dion/state.py:179-188      rank rule;  state.py:220-230 low-rank-sync rule
+  dion/runtime.py:1729-1795, :965-1013  the FS ("fsdp") kind: RS(sum)/ortho/AG of the
+                             partial P, shard-local R / fix-up / EF, column norm over shards
 """
 
 from __future__ import annotations
@@ -192,8 +194,11 @@ def _project(mats: Sequence[DionMatrix]):
 
 
 def _finish(mats: Sequence[DionMatrix], X, Qb, P, R, real: int, hyper: DionHyper,
-            m_global: int, n_global: int):
-    """runtime.py:1838-1901: fix-up, error feedback, column norm, weight update, Q commit."""
+            m_global: int, n_global: int, colsum_reduce=None):
+    """runtime.py:1838-1901: fix-up, error feedback, column norm, weight update, Q commit.
+
+    `colsum_reduce(col_sum_sq)` (FS kind) returns the column sums of squares summed over
+    the q_norm group (runtime.py:994-1001); the local sums are used otherwise."""
     P, R = fix_all_zero_or_nan(P, R, Qb, X, real)
     transposed = mats[0].transposed
     alpha = -(1.0 - hyper.mu)
@@ -203,7 +208,12 @@ def _finish(mats: Sequence[DionMatrix], X, Qb, P, R, real: int, hyper: DionHyper
     for i in range(real):
         mats[i].M.mul_(1.0)
         mats[i].M.add_(upd[i])
-    Qn = column_normalize(R[:real], hyper.epsilon)
+    if colsum_reduce is None:
+        Qn = column_normalize(R[:real], hyper.epsilon)
+    else:
+        # kernels.py:207-210 local_column_sum_sq, summed over the shards, then :279-290
+        col = colsum_reduce(R[:real].to(torch.float32).square().sum(dim=-2, keepdim=True))
+        Qn = (R[:real].to(torch.float32) / col.sqrt().add_(hyper.epsilon)).to(R.dtype)
     s = scaled_lr_for_shape(lr=hyper.lr, m_global=m_global, n_global=n_global,
                             scale_mode=hyper.scale_mode,
                             rank_fraction=hyper.rank_fraction,
@@ -294,6 +304,65 @@ def _replicated_batch_gen(per_rank: List[List[DionMatrix]], real: int, hyper: Di
         for i in range(real):
             per_rank[w][i].trace["P_raw"] = P_avg[i].clone()
         _finish(per_rank[w], X, Qb, P_views[w], R.clone(), real, hyper, m, n)
+
+
+def _fs_batch_gen(per_rank: List[List[DionMatrix]], real: int, hyper: DionHyper, sketch_fn,
+                  m_global: int, n_global: int, indices=None):
+    """Generator over all FS ranks of one "fsdp" batch (FS world W, no replicas), yielding where
+    dion/runtime.py yields on its FS-only path (:1729-1795; RP = 1, so no low-rank sync):
+
+      every rank: M += G; X = M or M^T (its shard); P_k = X_k @ Q_k, a partial sum over the
+        sharded dim (the orientation follows fs_shard_dim, dion/state.py:304-310)
+      reduce_scatter(sum) [yield] -> rank k holds sum_k' P_k'[indices[k]]; orthogonalize it
+        (zero for a padded entry, :1766-1777); all_gather [yield] (permuted back by indices)
+      every rank: R_k = X_k^T @ P (its rows of R); fix-up with ITS shard's zero test
+        (kernels.py:157-204 on the local M_batch); error feedback on its shard
+      column norm: local fp32 sums of squares all-reduced (sum) over the FS group
+        (q_norm_group, :994-1001) [yield]; Q_k = R_k / (sqrt(sum) + eps)
+      weight update of its shard with the GLOBAL shape's scaled LR (:1056-1090)
+
+    per_rank[k] holds rank k's B = W entries (padded entries carry zero G/M/Q); the reduce-
+    scatter sums in rank order.  `sketch_fn(rank, entry, P)`."""
+    W = len(per_rank)
+    B = len(per_rank[0])
+    idx_of = list(indices) if indices is not None else list(range(W))
+    proj = [_project(mats) for mats in per_rank]
+    P_sum = proj[0][2].clone()
+    for k in range(1, W):
+        P_sum = P_sum + proj[k][2]
+    yield                                                   # reduce-scatter in flight
+    P_ortho = torch.zeros_like(P_sum)
+    for k in range(W):
+        idx = idx_of[k]
+        if idx >= real:
+            continue
+        S = sketch_fn(k, idx, P_sum[idx:idx + 1]) if sketch_fn is not None else None
+        P_ortho[idx] = orthogonalize(P_sum[idx:idx + 1], hyper.rcqr_oversample, sketch=S)[0]
+    yield                                                   # all-gather in flight
+    Rs = [proj[k][0].mT @ P_ortho for k in range(W)]
+    fixed = []
+    for k in range(W):
+        X, Qb, _ = proj[k]
+        fixed.append(fix_all_zero_or_nan(P_ortho.clone(), Rs[k], Qb, X, real))
+    sums = [f[1][:real].to(torch.float32).square().sum(dim=-2, keepdim=True) for f in fixed]
+    total = sums[0].clone()
+    for k in range(1, W):
+        total = total + sums[k]
+    yield                                                   # column-norm all-reduce in flight
+    for k in range(W):
+        X, Qb, _ = proj[k]
+        for i in range(real):
+            per_rank[k][i].trace["P_raw"] = P_sum[i].clone()
+        _finish(per_rank[k], X, Qb, P_ortho.clone(), Rs[k], real, hyper, m_global, n_global,
+                colsum_reduce=lambda _local, _t=total: _t)
+
+
+def dion_step_fs(batches, hyper: DionHyper, sketch_fn=None, max_concurrent: int = 3) -> None:
+    """One optimizer step over FS ("fsdp") batches, every FS rank simulated.
+
+    `batches` is a list of (per_rank, real, (m_global, n_global)) as _fs_batch_gen takes them."""
+    gens = (_fs_batch_gen(per_rank, real, hyper, sketch_fn, mg, ng) for per_rank, real, (mg, ng) in batches)
+    run_async_runtime(gens, max_concurrent=max_concurrent)
 
 
 def run_async_runtime(generators, max_concurrent: int = 3) -> None:

@@ -9,8 +9,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 GOLDEN = os.path.join(HERE, "golden")
 
 
-def manifest():
-    with open(os.path.join(GOLDEN, "manifest.json")) as fh:
+def manifest(name="manifest.json"):
+    with open(os.path.join(GOLDEN, name)) as fh:
         return json.load(fh)
 
 
@@ -19,15 +19,17 @@ def case_names():
 
 
 class Case:
+    MANIFEST = "manifest.json"
+
     def __init__(self, name):
-        man = manifest()
+        man = manifest(self.MANIFEST)
         self.hyper = man["hyper"]
         self.entry = next(c for c in man["cases"] if c["name"] == name)
         self.name = name
         self.world = int(self.entry["world"])
         self.steps = int(self.entry["steps"])
-        self.r = int(self.entry["r"])
-        self.mats = [(n, int(m), int(k)) for n, m, k in self.entry["mats"]]
+        self.r = int(self.entry.get("r", 0))  # FS captures carry r per matrix (shards)
+        self.mats = [(n, int(m), int(k)) for n, m, k, *_ in self.entry["mats"]]
         with np.load(os.path.join(GOLDEN, name + ".npz")) as z:
             self.arr = {k: z[k] for k in z.files}
 
@@ -69,3 +71,22 @@ class Case:
         scale = max(p_in.abs().max().item(), 1e-30)
         assert best_err <= 1e-4 * scale, f"closest ortho input differs by {best_err}"
         return best["S"]
+
+
+def fs_case_names():
+    return [c["name"] for c in manifest("manifest_fs.json")["cases"]]
+
+
+class FsCase(Case):
+    """An FS ("fsdp") capture (make_golden_fs.py): per-rank local shards of each matrix."""
+    MANIFEST = "manifest_fs.json"
+
+    @property
+    def rank_fraction(self):
+        return float(self.entry["rf"])
+
+    def shard(self, rank, name):
+        return self.entry["rank_meta"][rank]["shards"][name]
+
+    def fs_dim(self, name):
+        return next(int(d) for n, _, _, d in self.entry["mats"] if n == name)
