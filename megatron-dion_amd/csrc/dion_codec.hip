@@ -2089,6 +2089,8 @@ struct EfProjArgs {
   const u32x4* rsplit;     // R'_b pre-split, A-operand layout
   long split_stride;
   float alpha;
+  const uint32_t* amax;    // h3 kernels: (3, batch) max |x| bits of Q, R', P'
+  const float* inv;        // h3 kernels: (2, batch) 1 / scale of the Q and R' splits
 };
 
 // Pre-split of a small factor (rows x r fp32) into hi/mid/lo bf16, laid out so a
@@ -3040,16 +3042,17 @@ __global__ void __launch_bounds__(256) absmax_kernel(const AbsMaxArgs a) {
   if ((threadIdx.x & 63) == 0) atomicMax(&a.out[b], m);
 }
 
-// h3 pre-split of a small factor in the MFMA operand layout of presplit_kernel layout 0
-// (grp = (row / 32) RB + cb; lane (t, g) <- rows 32 blk + kmap(g, e), column 16 cb + t),
-// two fp16 limbs per 8 values: dst[(grp * 2 + part) * 64 + lane], scale from amax[b]
+// h3 pre-split of a small factor in the MFMA operand layouts of presplit_kernel, two fp16
+// limbs per 8 values: dst[(grp * 2 + part) * 64 + lane], scale from amax[b]
+//   layout 0 (B-operand-style):  grp = (row / 32) RB + cb; lane (t, g) <- rows 32 blk + kmap(g, e), column 16 cb + t
+//   layout 1 (A-operand-style):  grp = (row / 16) KK + kk; lane (t, g) <- row 16 blk + t, columns 32 kk + 8 g + e
 struct Presplit16Args {
   const float* src[MAXB];
   f16x8* dst;
   const uint32_t* amax;  // (batch,) max |x| bits
   float* inv_scale;      // (batch,) 1 / s, written by the blocks of x = 0
   long stride;           // f16x8 units per matrix
-  int rows, r, kmap;
+  int rows, r, kmap, layout;
 };
 
 __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a) {
@@ -3065,14 +3068,23 @@ __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a)
   const int ln = static_cast<int>(item & 63);
   const long grp = item >> 6;
   const int t = ln & 15, g = ln >> 4;
-  const int RB = a.r / 16;
-  const long blk = grp / RB;
-  const int cb = static_cast<int>(grp - blk * RB);
   float v[8];
+  if (a.layout == 0) {
+    const int RB = a.r / 16;
+    const long blk = grp / RB;
+    const int cb = static_cast<int>(grp - blk * RB);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = a.kmap == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
-    v[e] = src[(blk * 32 + k) * a.r + 16 * cb + t];
+    for (int e = 0; e < 8; ++e) {
+      const int k = a.kmap == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
+      v[e] = src[(blk * 32 + k) * a.r + 16 * cb + t];
+    }
+  } else {
+    const int KK = a.r / 32;
+    const long blk = grp / KK;
+    const int kk = static_cast<int>(grp - blk * KK);
+    const float* p = src + (blk * 16 + t) * a.r + 32 * kk + 8 * g;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = p[e];
   }
   Split2h sp;
   split2h(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, s, sp);
@@ -3174,6 +3186,215 @@ __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : 2) colproj_h3_kernel(co
     for (int cb = 0; cb < RB; ++cb)
       *reinterpret_cast<f32x4*>(out + static_cast<long>(col_base + CT * t + c) * R + 16 * cb + 4 * g) =
           acc[c][cb] * ps;
+}
+
+// ---- pass A, not transposed, h3 products (fp16x3): rowproj_ef_kernel's geometry, TJ
+// line loads and line stores; the error feedback's fixed operands (P', R') carry
+// per-matrix scales, and in the projection the streamed X is the B operand (lane (t, g)
+// holds row 16 rb + t, k-run KMAP 1) with a per-step scale per row (max over the lanes
+// (t, g = 0..3)), Q the A operand: each step lands in a fresh accumulator
+// D[16 cb + 4 g + q][row t] and is added as acc += D / s_row.
+template <int RB, int GDT, int PD>
+__global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(const EfProjArgs e) {
+  constexpr int R = 16 * RB;
+  constexpr int KK = RB / 2;
+  constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;  // f16x8 units of one K-step's splits
+  __shared__ f16x8 tq[2][NQ];
+  __shared__ f16x8 rs[2][NR];
+  __shared__ f32x4 xt[kPaNW][32 * 8];
+  const ProjArgs& a = e.p;
+  const BlockXYZ blk = xcd_block();
+  const int b = blk.z;
+  const int nb = gridDim.z;
+  const int kc = blk.y;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int row_base = blk.x * (16 * kRBE * kPaNW) + wave * (16 * kRBE);
+  const int j_begin = kc * a.kchunk;
+  const int j_end = min(a.cols, j_begin + a.kchunk);
+  const void* G = nullptr;
+  if constexpr (GDT == DION_DTYPE_BF16)
+    G = static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 4 * g;
+  else if constexpr (GDT == DION_DTYPE_F32)
+    G = static_cast<const float*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 4 * g;
+  float* __restrict__ Mw = a.m[b] + static_cast<long>(row_base + (lane >> 3)) * a.ld_m + 4 * (lane & 7);
+  const bool has_ef = e.efr[b] != nullptr;
+  const float invQ = e.inv[b];
+  const float invR = e.inv[nb + b];
+  float invF;
+  const float sF = h3_scale(fabsf(e.alpha) * __uint_as_float(e.amax[2 * nb + b]), invF);
+  const float efinv = invF * invR;
+
+  Split2h F[kRBE][KK];
+  if (has_ef) {
+#pragma unroll
+    for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const float* src = e.efp[b] + static_cast<long>(row_base + 16 * rb + t) * R + 32 * kk + 8 * g;
+        split2h(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), e.alpha * sF,
+                F[rb][kk]);
+      }
+  } else {
+#pragma unroll
+    for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) F[rb][kk] = Split2h{};
+  }
+
+  f32x4 acc[kRBE][RB];
+#pragma unroll
+  for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t nzb = 0;
+
+  const u32x4* qs = e.qsplit + b * e.split_stride;
+  const u32x4* rsp = e.rsplit + b * e.split_stride;
+  RowStepE<GDT> S[PD];
+  auto xload = [&](RowStepE<GDT>& T, int j) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      T.x[q >> 1][q & 1] = ld_stream(reinterpret_cast<const f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j));
+    rpe_load<GDT>(T, nullptr, G, 0, a.ld_g, j);
+  };
+  auto xpose = [&](RowStepE<GDT>& T) {
+    f32x4* xw = xt[wave];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 8 * q + (lane >> 3), k = lane & 7;
+      xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[q >> 1][q & 1];
+    }
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int r = 16 * rb + t, k = 4 * c + g;
+        T.x[rb][c] = xw[r * 8 + (k ^ ((r >> 1) & 7))];
+      }
+  };
+  auto xstore = [&](const RowStepE<GDT>& T, int j) {
+    f32x4* xw = xt[wave];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int r = 16 * rb + t, k = 4 * c + g;
+        xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[rb][c];
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 8 * q + (lane >> 3), k = lane & 7;
+      st_stream(reinterpret_cast<f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j), xw[r * 8 + (k ^ ((r >> 1) & 7))]);
+    }
+  };
+  auto compute = [&](RowStepE<GDT>& X, const f16x8* tqc, const f16x8* rsc) {
+    if (has_ef) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        f32x4 ev[kRBE];
+#pragma unroll
+        for (int rb = 0; rb < kRBE; ++rb) ev[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          Split2h A;
+          A.hi = rsc[((c * KK + kk) * 2 + 0) * 64 + lane];
+          A.lo = rsc[((c * KK + kk) * 2 + 1) * 64 + lane];
+#pragma unroll
+          for (int rb = 0; rb < kRBE; ++rb) ev[rb] = mfma3h(A, F[rb][kk], ev[rb]);
+        }
+#pragma unroll
+        for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) X.x[rb][c][q] = fmaf(ev[rb][q], efinv, X.x[rb][c][q]);
+      }
+    }
+#pragma unroll
+    for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        if constexpr (GDT == DION_DTYPE_BF16) {
+          const uint2 gv = X.gb[rb][c];
+          X.x[rb][c][0] += __uint_as_float(gv.x << 16);
+          X.x[rb][c][1] += __uint_as_float(gv.x & 0xFFFF0000u);
+          X.x[rb][c][2] += __uint_as_float(gv.y << 16);
+          X.x[rb][c][3] += __uint_as_float(gv.y & 0xFFFF0000u);
+        } else if constexpr (GDT == DION_DTYPE_F32) {
+          X.x[rb][c] += X.gf[rb][c];
+        }
+        nzb |= __float_as_uint(X.x[rb][c][0]) | __float_as_uint(X.x[rb][c][1]) | __float_as_uint(X.x[rb][c][2]) |
+               __float_as_uint(X.x[rb][c][3]);
+      }
+    Split2h Bx[kRBE];
+    float invx[kRBE];
+#pragma unroll
+    for (int rb = 0; rb < kRBE; ++rb) {
+      float m8 = max8abs(X.x[rb][0], X.x[rb][1]);
+      m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
+      m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
+      const float sx = h3_scale(m8, invx[rb]);
+      split2h(X.x[rb][0], X.x[rb][1], sx, Bx[rb]);
+    }
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      Split2h A;
+      A.hi = tqc[(cb * 2 + 0) * 64 + lane];
+      A.lo = tqc[(cb * 2 + 1) * 64 + lane];
+#pragma unroll
+      for (int rb = 0; rb < kRBE; ++rb) {
+        const f32x4 d = mfma3h(A, Bx[rb], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[rb][cb][q] = fmaf(d[q], invx[rb], acc[rb][cb][q]);
+      }
+    }
+  };
+
+  SplitCopyN<NQ, 64 * kPaNW> TA;
+  SplitCopyN<NR, 64 * kPaNW> EA;
+#pragma unroll
+  for (int k = 0; k < PD - 1; ++k)
+    if (j_begin + 32 * k < j_end) xload(S[k], j_begin + 32 * k);
+  split_copy_load_n(TA, qs + static_cast<long>(j_begin / 32) * NQ, tid);
+  split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
+  if (has_ef) {
+    split_copy_load_n(EA, rsp + static_cast<long>(j_begin / 32) * NR, tid);
+    split_copy_store_n(EA, reinterpret_cast<bf16x8*>(rs[0]), tid);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int j0 = j_begin; j0 < j_end; j0 += 32 * PD) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      const int j = j0 + 32 * k;
+      if (j >= j_end) break;
+      const bool more = j + 32 < j_end;
+      if (j + 32 * (PD - 1) < j_end) xload(S[(k + PD - 1) % PD], j + 32 * (PD - 1));
+      if (more) {
+        split_copy_load_n(TA, qs + static_cast<long>((j + 32) / 32) * NQ, tid);
+        if (has_ef) split_copy_load_n(EA, rsp + static_cast<long>((j + 32) / 32) * NR, tid);
+      }
+      xpose(S[k]);
+      compute(S[k], tq[cur], rs[cur]);
+      xstore(S[k], j);
+      if (!more) break;
+      split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+      if (has_ef) split_copy_store_n(EA, reinterpret_cast<bf16x8*>(rs[cur ^ 1]), tid);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(row_base + 16 * rb + t) * R + 16 * cb + 4 * g) =
+          acc[rb][cb] * invQ;
+  if (a.nonzero != nullptr && __any((nzb & 0x7FFFFFFFu) != 0u) && lane == 0) atomicOr(&a.nonzero[b], 1u);
 }
 
 // ============================================================================
@@ -3283,6 +3504,10 @@ int rank_stream_variant() {
 // pre-split thin operand of the x6 projections (rows = the contraction index)
 size_t thin_presplit_bytes(int rows, int r, int batch) { return static_cast<size_t>(rows) * r * 6 * batch + 1024; }
 
+// pass A (not transposed) through the fp16x3 row kernel (rowproj_efh3_kernel; tuning knob)
+#ifndef DION_PA_H3
+#define DION_PA_H3 1
+#endif
 // pass B through the fp16x3 column kernel (colproj_h3_kernel) instead of bf16x6 (tuning knob)
 #ifndef DION_PB_H3
 #define DION_PB_H3 1
@@ -3319,7 +3544,8 @@ size_t presplit_bytes(int nq, int r, int batch) { return 2 * 16 * presplit_strid
 
 // deferred-EF pass A (rowproj_ef_kernel / colproj_ef_kernel)
 bool proj_ef_ok(int m, int n, int r, bool transposed) {
-  if (r != 32 && r != 64) return false;
+  // r = 128 (the Mixtral config) only through the h3 row kernel
+  if (r != 32 && r != 64 && !(r == 128 && !transposed && DION_PA_H3)) return false;
   return transposed ? (n % 128 == 0 && m % 32 == 0) : (m % (16 * kRBE * kPaNW) == 0 && n % 32 == 0);
 }
 
@@ -3471,6 +3697,7 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     pa.rows = thin_rows;
     pa.r = r;
     pa.kmap = 0;
+    pa.layout = 0;
     const dim3 pgrid(static_cast<unsigned>(ceil_div(per / 8, 256)), batch);
     hipLaunchKernelGGL(presplit16_kernel, pgrid, dim3(256), 0, st, pa);
     int rc = check_launch("presplit16(thin)");
@@ -3863,10 +4090,52 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
     const size_t need = slab + presplit_bytes(nq, d->r, nb);
     if (need > ws_bytes || ws == nullptr)
       return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
-    const long sstride = static_cast<long>(presplit_stride(nq, d->r));
+    const bool h3 = !tr && DION_PA_H3;
+    const long sstride = h3 ? static_cast<long>(nq) * d->r / 4 : static_cast<long>(presplit_stride(nq, d->r));
     u32x4* qsplit = reinterpret_cast<u32x4*>(static_cast<char*>(ws) + slab);
     u32x4* rsplit = qsplit + sstride * nb;
-    {
+    uint32_t* amax = nullptr;
+    float* inv = nullptr;
+    if (h3) {
+      // fp16x3: per-matrix |max| of Q, R' and P', then the two fp16 limbs of Q and R'
+      char* tail = reinterpret_cast<char*>(rsplit + sstride * nb);
+      amax = reinterpret_cast<uint32_t*>(tail);
+      inv = reinterpret_cast<float*>(tail + 1024);
+      hipError_t me = hipMemsetAsync(amax, 0, sizeof(uint32_t) * 3 * nb, st);
+      if (me != hipSuccess) return fail(DION_E_LAUNCH, "memset: %s", hipGetErrorString(me));
+      AbsMaxArgs ma;
+      for (int which = 0; which < 3; ++which) {
+        memset(&ma, 0, sizeof(ma));
+        for (int b = 0; b < nb; ++b)
+          ma.src[b] = which == 0 ? Q[b0 + b] : (which == 1 ? ef->R[b0 + b] : ef->P[b0 + b]);
+        ma.out = amax + which * nb;
+        ma.count = static_cast<long>(which == 2 ? mp : nq) * d->r;
+        const long mb = ceil_div(ma.count, 256) < 64 ? ceil_div(ma.count, 256) : 64;
+        hipLaunchKernelGGL(absmax_kernel, dim3(static_cast<unsigned>(mb), nb), dim3(256), 0, st, ma);
+      }
+      Presplit16Args pa;
+      memset(&pa, 0, sizeof(pa));
+      pa.rows = nq;
+      pa.r = d->r;
+      pa.stride = sstride;
+      const dim3 pgrid(static_cast<unsigned>(ceil_div(static_cast<long>(nq) * d->r / 8, 256)), nb);
+      for (int b = 0; b < nb; ++b) pa.src[b] = Q[b0 + b];
+      pa.dst = reinterpret_cast<f16x8*>(qsplit);
+      pa.amax = amax;
+      pa.inv_scale = inv;
+      pa.layout = 0;
+      pa.kmap = 1;
+      hipLaunchKernelGGL(presplit16_kernel, pgrid, dim3(256), 0, st, pa);
+      for (int b = 0; b < nb; ++b) pa.src[b] = ef->R[b0 + b];
+      pa.dst = reinterpret_cast<f16x8*>(rsplit);
+      pa.amax = amax + nb;
+      pa.inv_scale = inv + nb;
+      pa.layout = 1;
+      pa.kmap = 0;
+      hipLaunchKernelGGL(presplit16_kernel, pgrid, dim3(256), 0, st, pa);
+      rc = check_launch("presplit16");
+      if (rc != DION_OK) return rc;
+    } else {
       PresplitArgs pa;
       memset(&pa, 0, sizeof(pa));
       pa.rows = nq;
@@ -3901,6 +4170,8 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
     e.qsplit = qsplit;
     e.rsplit = rsplit;
     e.split_stride = sstride;
+    e.amax = amax;
+    e.inv = inv;
     a.out = geo.nchunk > 1 ? static_cast<float*>(ws) : out;
     a.nonzero = nonzero ? nonzero + b0 : nullptr;
     a.rows = d->m;
@@ -3917,16 +4188,24 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
       constexpr int RB = decltype(RBc)::value;
       return dispatch_gdt(d->g_dtype, [&](auto Gc) {
         constexpr int GD = decltype(Gc)::value;
-        if (tr)
-          hipLaunchKernelGGL((colproj_ef_kernel<RB, GD>), grid, dim3(256), 0, st, e);
-        else if (pa_lines())
-          hipLaunchKernelGGL((rowproj_ef_kernel<RB, GD, 2, true>), grid, dim3(64 * kPaNW), 0, st, e);
-        else
-          hipLaunchKernelGGL((rowproj_ef_kernel<RB, GD, 2, false>), grid, dim3(64 * kPaNW), 0, st, e);
+        if constexpr (RB == 8) {  // r = 128: the h3 row kernel only (proj_ef_ok)
+          hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, 1>), grid, dim3(64 * kPaNW), 0, st, e);
+        } else {
+          if (tr)
+            hipLaunchKernelGGL((colproj_ef_kernel<RB, GD>), grid, dim3(256), 0, st, e);
+          else if (h3)
+            hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, 2>), grid, dim3(64 * kPaNW), 0, st, e);
+          else if (pa_lines())
+            hipLaunchKernelGGL((rowproj_ef_kernel<RB, GD, 2, true>), grid, dim3(64 * kPaNW), 0, st, e);
+          else
+            hipLaunchKernelGGL((rowproj_ef_kernel<RB, GD, 2, false>), grid, dim3(64 * kPaNW), 0, st, e);
+        }
         return check_launch(tr ? "colproj_ef" : "rowproj_ef");
       });
     };
-    rc = d->r == 32 ? go(std::integral_constant<int, 2>{}) : go(std::integral_constant<int, 4>{});
+    rc = d->r == 32    ? go(std::integral_constant<int, 2>{})
+         : d->r == 64  ? go(std::integral_constant<int, 4>{})
+                       : go(std::integral_constant<int, 8>{});
     if (rc != DION_OK) return rc;
     if (geo.nchunk > 1) {
       rc = launch_reduce(out, static_cast<const float*>(ws), geo.nchunk, static_cast<long>(geo.out_rows) * d->r, nb, st);

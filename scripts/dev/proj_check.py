@@ -29,6 +29,26 @@ if op.startswith("pb"):
         ecol = ((R[b].double() - ref).abs().amax(0) / ref.abs().amax(0)).max().item()
         print(f"{op} b{b}: maxrel {e:.3e}  worst per-column rel {ecol:.3e}")
         worst = max(worst, e)
+elif op.startswith("pa_ef"):
+    Gs = [(torch.randn(m, n, device=dev, generator=g) * 1e-3).to(torch.bfloat16) for _ in range(B)]
+    Pp = [torch.linalg.qr(torch.randn(mp, r, device=dev, generator=g))[0].contiguous() for _ in range(B)]
+    Rp = [(torch.randn(nq, r, device=dev, generator=g) * 1e-2).contiguous() for _ in range(B)]
+    Rp[0].mul_(torch.logspace(-2, 1, nq, device=dev)[:, None])
+    alpha = -0.05
+    X0 = [M.double().clone() for M in Ms]
+    Pout = torch.zeros(B, mp, r, device=dev)
+    nz = torch.zeros(B, dtype=torch.int32, device=dev)
+    codec.project_p_ef(Gs, Ms, Qs, Pout, nz, T, Pp, Rp, alpha)
+    torch.cuda.synchronize()
+    for b in range(B):
+        ef = (Rp[b].double() @ Pp[b].double().t()) if T else (Pp[b].double() @ Rp[b].double().t())
+        Mref = X0[b] + alpha * ef + Gs[b].double()
+        X = Mref.t() if T else Mref
+        ref = X @ Qs[b].double()
+        em = ((Ms[b].double() - Mref).abs().max() / Mref.abs().max()).item()
+        e = ((Pout[b].double() - ref).abs().max() / ref.abs().max()).item()
+        print(f"{op} b{b}: P maxrel {e:.3e}  M maxrel {em:.3e}")
+        worst = max(worst, e, em)
 else:
     Pout = torch.zeros(B, mp, r, device=dev)
     nz = torch.zeros(B, dtype=torch.int32, device=dev)
