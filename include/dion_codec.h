@@ -41,7 +41,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 8
+#define DION_ABI_VERSION 9
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -87,8 +87,10 @@ int dion_workspace_bytes(const DionBatchDesc* desc, int op, size_t* bytes);
 /*
  * Pass A.  For every matrix b:  M_b += G_b (when g_dtype != NONE),
  *   P_b = X_b Q_b  with X_b = M_b (or M_b^T when transposed), fp32 (TF32 off),
- *   nonzero[b] |= 1 if any element of the accumulated M_b is != 0.
- * `nonzero` must be zeroed by the caller before the call.
+ *   nonzero[b] != 0 iff some element of the accumulated M_b is != 0.
+ * `nonzero` must be zeroed by the caller before the call.  A nonzero flag carries the
+ * bit pattern of max |M_b| (fp32) when the kernel measured it, or a value >= 0x7F800000
+ * (inf's bits) when it did not; hand the array to dion_project_r as `m_absmax`.
  * Replaces runtime.py:1560-1566 (momentum accumulate), :1602-1616 (stack +
  * P = M Q) and the all-zero test of kernels.py:185 (is_all_zero).
  */
@@ -134,9 +136,14 @@ int dion_orthonormalize(const DionBatchDesc* desc, float* P, const float* sketch
 
 /*
  * Pass B.  R_b = X_b^T P_b  (n_Q x r), fp32.  runtime.py:1476-1477.
+ * `m_absmax` (optional, may be NULL): the `nonzero` flags pass A left for exactly these
+ * M_b.  A finite max |M_b| lets the fp16x3 kernel use one power-of-two scale per matrix
+ * instead of one per column and step (same accuracy, fewer instructions); other values
+ * or NULL select the per-step scales.
  */
 int dion_project_r(const DionBatchDesc* desc, const float* const* M, const float* P,
-                   float* R, void* ws, size_t ws_bytes, dion_stream_t stream);
+                   float* R, const uint32_t* m_absmax, void* ws, size_t ws_bytes,
+                   dion_stream_t stream);
 
 /*
  * fix_all_zero_or_nan (kernels.py:157-204) + column normalisation

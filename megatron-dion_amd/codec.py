@@ -190,8 +190,9 @@ class HipDionCodec:
         _lib.check(rc, "dion_orthonormalize")
 
     def project_r(self, momentums: List[torch.Tensor], P: torch.Tensor, R: torch.Tensor,
-                  transposed: bool) -> None:
-        """R = M^T P (or M P).  runtime.py:1476-1477."""
+                  transposed: bool, nonzero: Optional[torch.Tensor] = None) -> None:
+        """R = M^T P (or M P).  runtime.py:1476-1477.  `nonzero`: the flags project_p /
+        project_p_ef left for these momentums (their max |M|: fixed-scale pass B)."""
         B = len(momentums)
         if B == 0:
             return
@@ -200,6 +201,7 @@ class HipDionCodec:
         d = self._desc(B, m, n, r, transposed, M=momentums[0])
         ws = self.workspace(d, _lib.OP_PROJECT_R)
         rc = self.lib.dion_project_r(ctypes.byref(d), _ptrs(momentums), P.data_ptr(), R.data_ptr(),
+                                     None if nonzero is None else nonzero.data_ptr(),
                                      ws.data_ptr(), ws.numel(), self._stream())
         _lib.check(rc, "dion_project_r")
 

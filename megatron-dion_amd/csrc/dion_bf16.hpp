@@ -192,7 +192,7 @@ __global__ void __launch_bounds__(256) b16_proj_kernel(const B16ProjArgs a) {
         const int orow = o0 + 16 * rw + 4 * g + q, c = 16 * cb + t;
         if (orow < a.out_rows && c < a.r) out[static_cast<long>(orow) * a.r + c] = acc[rw][cb][q];
       }
-  if (a.nonzero != nullptr && __any(nz != 0u) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+  if (a.nonzero != nullptr && __any(nz != 0u) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
 }
 
 // tt[b][c][k] = c < r ? bf16(T_b[k][c]) : 0  for k < K (zero up to the stride Kp)

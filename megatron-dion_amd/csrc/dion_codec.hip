@@ -162,7 +162,14 @@ struct ProjArgs {
   const void* tsplit;      // thin operand pre-split (presplit_kernel layout 0, KMAP 0) for the x6 kernels
   long ts_stride;          // 16-byte units per matrix of tsplit
   const float* tinv;       // h3 kernels: 1 / scale of each matrix's thin-operand split
+  const uint32_t* mabs;    // pass B: pass A's flag per matrix (max |M_b| bits when measured) or null
 };
+
+// The nonzero flag pass A leaves per matrix (DionBatchDesc docs, dion_project_p): 0 iff
+// every element of the accumulated M_b is +-0; otherwise the bit pattern of max |M_b|
+// (non-negative floats order like their bits) when the kernel measured it, or kAbsUnknown
+// (inf's bits; NaN's sort above) when it did not.  Combined across blocks with atomicMax.
+constexpr uint32_t kAbsUnknown = 0x7F800000u;
 
 // ============================================================================
 // Row projection:  out[b][i][c] = sum_j X_b[i][j] * T_b[j][c]    (X = M (+ G))
@@ -291,7 +298,7 @@ __global__ void __launch_bounds__(256) rowproj_kernel(const ProjArgs a) {
         if (row < a.rows && c < r) out[static_cast<long>(row) * r + c] = acc[rb][cb][q];
       }
   if constexpr (GDT != DION_DTYPE_NONE) {
-    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
   }
 }
 
@@ -452,7 +459,7 @@ __global__ void __launch_bounds__(256) colproj_kernel(const ProjArgs a) {
         if (j < a.cols && c < r) out[static_cast<long>(j) * r + c] = acc[e][cb][q];
       }
   if constexpr (GDT != DION_DTYPE_NONE) {
-    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
   }
 }
 
@@ -678,7 +685,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_fast_kernel(cons
       for (int q = 0; q < 4; ++q)
         out[static_cast<long>(row_base + 16 * rb + 4 * g + q) * R + 16 * cb + t] = acc[rb][cb][q];
   if constexpr (GDT != DION_DTYPE_NONE) {
-    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
   }
 }
 
@@ -828,7 +835,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_fast_kernel(cons
       for (int q = 0; q < 4; ++q)
         out[static_cast<long>(col_base + 4 * (4 * g + q) + e) * R + 16 * cb + t] = acc[e][cb][q];
   if constexpr (GDT != DION_DTYPE_NONE) {
-    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+    if (a.nonzero != nullptr && __any(nz) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
   }
 }
 
@@ -2542,7 +2549,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_ef_kernel(const
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         out[static_cast<long>(row_base + 16 * rb + 4 * g + q) * R + 16 * cb + t] = acc[rb][cb][q];
-  if (a.nonzero != nullptr && __any((nzb & 0x7FFFFFFFu) != 0u) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+  if (a.nonzero != nullptr && __any((nzb & 0x7FFFFFFFu) != 0u) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
 }
 
 // ---- column kernel (transposed): block = 4 waves x 32 columns, step = 32 rows;
@@ -2738,7 +2745,7 @@ __global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) 
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         out[static_cast<long>(col_base + 2 * (4 * g + q) + c) * R + 16 * cb + t] = acc[c][cb][q];
-  if (a.nonzero != nullptr && __any((nzb & 0x7FFFFFFFu) != 0u) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+  if (a.nonzero != nullptr && __any((nzb & 0x7FFFFFFFu) != 0u) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
 }
 
 // ---- row projection, no gradient (pass B, transposed: R = M P):
@@ -2994,7 +3001,7 @@ struct Split2h {
 __device__ __forceinline__ float h3_scale(float amax, float& inv) {
   const int be = static_cast<int>((__float_as_uint(amax) >> 23) & 0xFFu);  // biased exponent
   int es = 127 + 14 - (be - 127);                                           // 2^(14 - e)
-  es = es < 1 ? 1 : (es > 254 ? 254 : es);
+  es = es < 1 ? 1 : (es > 253 ? 253 : es);  // s and inv both normal: inv == 1 / s exactly
   inv = __uint_as_float(static_cast<uint32_t>(254 - es) << 23);
   return __uint_as_float(static_cast<uint32_t>(es) << 23);
 }
@@ -3125,60 +3132,81 @@ __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : 2) colproj_h3_kernel(co
     for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
-  SplitCopyN<NQ, 64 * NW> TA;
-  constexpr int PD = kColX6PD;
-  ColStepX6<CT> S[PD];
+  // pass A's max |M_b| (when measured and finite): one power-of-two scale for the whole
+  // matrix, the products accumulate in place; else a scale per column and 32-row step
+  const uint32_t mab = a.mabs != nullptr ? a.mabs[b] : kAbsUnknown;
+  float finv = 1.f;
+  const float fs = h3_scale(__uint_as_float(mab), finv);
+  auto run = [&](auto FIXc) {
+    constexpr bool FIX = decltype(FIXc)::value;
+    SplitCopyN<NQ, 64 * NW> TA;
+    constexpr int PD = kColX6PD;
+    ColStepX6<CT> S[PD];
 #pragma unroll
-  for (int k = 0; k < PD - 1; ++k)
-    if (i_begin + 32 * k < i_end) cpx_load<CT>(S[k], M, a.ld_m, i_begin + 32 * k);
-  split_copy_load_n(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
-  split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
-  __syncthreads();
-  int cur = 0;
-  for (int i0 = i_begin; i0 < i_end; i0 += 32 * PD) {
+    for (int k = 0; k < PD - 1; ++k)
+      if (i_begin + 32 * k < i_end) cpx_load<CT>(S[k], M, a.ld_m, i_begin + 32 * k);
+    split_copy_load_n(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
+    split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
+    __syncthreads();
+    int cur = 0;
+    for (int i0 = i_begin; i0 < i_end; i0 += 32 * PD) {
 #pragma unroll
-    for (int k = 0; k < PD; ++k) {
-      const int i = i0 + 32 * k;
-      if (i >= i_end) break;
-      const bool more = i + 32 < i_end;
-      if (i + 32 * (PD - 1) < i_end) cpx_load<CT>(S[(k + PD - 1) % PD], M, a.ld_m, i + 32 * (PD - 1));
-      if (more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
-      {
-        const ColStepX6<CT>& X = S[k];
-        Split2h B[CT];
-        float inv[CT];
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          const f32x4 lo4{X.x[0][c], X.x[1][c], X.x[2][c], X.x[3][c]};
-          const f32x4 hi4{X.x[4][c], X.x[5][c], X.x[6][c], X.x[7][c]};
-          float m8 = max8abs(lo4, hi4);
-          m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
-          m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
-          const float s = h3_scale(m8, inv[c]);
-          split2h(lo4, hi4, s, B[c]);
-        }
-#pragma unroll
-        for (int cb = 0; cb < RB; ++cb) {
-          Split2h A;
-          A.hi = tq[cur][(cb * 2 + 0) * 64 + lane];
-          A.lo = tq[cur][(cb * 2 + 1) * 64 + lane];
+      for (int k = 0; k < PD; ++k) {
+        const int i = i0 + 32 * k;
+        if (i >= i_end) break;
+        const bool more = i + 32 < i_end;
+        if (i + 32 * (PD - 1) < i_end) cpx_load<CT>(S[(k + PD - 1) % PD], M, a.ld_m, i + 32 * (PD - 1));
+        if (more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
+        {
+          const ColStepX6<CT>& X = S[k];
+          Split2h B[CT];
+          float inv[CT];
 #pragma unroll
           for (int c = 0; c < CT; ++c) {
-            const f32x4 d = mfma3h(A, B[c], f32x4{0.f, 0.f, 0.f, 0.f});
+            const f32x4 lo4{X.x[0][c], X.x[1][c], X.x[2][c], X.x[3][c]};
+            const f32x4 hi4{X.x[4][c], X.x[5][c], X.x[6][c], X.x[7][c]};
+            if constexpr (FIX) {
+              split2h(lo4, hi4, fs, B[c]);
+            } else {
+              float m8 = max8abs(lo4, hi4);
+              m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
+              m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
+              const float sc = h3_scale(m8, inv[c]);
+              split2h(lo4, hi4, sc, B[c]);
+            }
+          }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) acc[c][cb][q] = fmaf(d[q], inv[c], acc[c][cb][q]);
+          for (int cb = 0; cb < RB; ++cb) {
+            Split2h A;
+            A.hi = tq[cur][(cb * 2 + 0) * 64 + lane];
+            A.lo = tq[cur][(cb * 2 + 1) * 64 + lane];
+#pragma unroll
+            for (int c = 0; c < CT; ++c) {
+              if constexpr (FIX) {
+                acc[c][cb] = mfma3h(A, B[c], acc[c][cb]);
+              } else {
+                const f32x4 d = mfma3h(A, B[c], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[c][cb][q] = fmaf(d[q], inv[c], acc[c][cb][q]);
+              }
+            }
           }
         }
+        if (!more) break;
+        split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+        __syncthreads();
+        cur ^= 1;
       }
-      if (!more) break;
-      split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
-      __syncthreads();
-      cur ^= 1;
     }
-  }
+  };
+  const bool fixed = mab < kAbsUnknown;
+  if (fixed)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
 
-  // P's per-matrix scale, then lane (t, g): R row CT t + c, columns 16 cb + 4 g .. + 3
-  const float ps = a.tinv[b];
+  // P's per-matrix scale (and M's, fixed mode), then lane (t, g): R row CT t + c, columns 16 cb + 4 g .. + 3
+  const float ps = a.tinv[b] * (fixed ? finv : 1.f);
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
 #pragma unroll
   for (int c = 0; c < CT; ++c)
@@ -3251,6 +3279,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
   uint32_t nzb = 0;
+  float mx = 0.f;  // max |M| over this wave's rows (m8 of every step)
 
   const u32x4* qs = e.qsplit + b * e.split_stride;
   const u32x4* rsp = e.rsplit + b * e.split_stride;
@@ -3335,6 +3364,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
       float m8 = max8abs(X.x[rb][0], X.x[rb][1]);
       m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
       m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
+      mx = fmaxf(mx, m8);
       const float sx = h3_scale(m8, invx[rb]);
       split2h(X.x[rb][0], X.x[rb][1], sx, Bx[rb]);
     }
@@ -3394,7 +3424,15 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
     for (int cb = 0; cb < RB; ++cb)
       *reinterpret_cast<f32x4*>(out + static_cast<long>(row_base + 16 * rb + t) * R + 16 * cb + 4 * g) =
           acc[rb][cb] * invQ;
-  if (a.nonzero != nullptr && __any((nzb & 0x7FFFFFFFu) != 0u) && lane == 0) atomicOr(&a.nonzero[b], 1u);
+  if (a.nonzero != nullptr) {
+    // the matrix's max |M| for pass B's fixed scale (colproj_h3_kernel); m8 ignores NaN,
+    // so an M of zeros and NaNs reports 1 (nonzero, tiny)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    const bool nz = __any((nzb & 0x7FFFFFFFu) != 0u);
+    const uint32_t mb = __float_as_uint(mx);
+    if (nz && lane == 0) atomicMax(&a.nonzero[b], mb > 1u ? mb : 1u);
+  }
 }
 
 // ============================================================================
@@ -3650,7 +3688,7 @@ int launch_reduce(float* out, const float* slab, int nchunk, long per_entry, int
 // One projection over up to MAXB matrices.  `row_mode`: reduce over columns.
 int run_projection(bool row_mode, int rows, int cols, int r, int batch, const void* const* G, float* const* M,
                    const float* const* thin, long ld_m, long ld_g, int gdt, float* out, uint32_t* nonzero,
-                   void* ws, size_t ws_bytes, hipStream_t st) {
+                   void* ws, size_t ws_bytes, hipStream_t st, const uint32_t* mabs = nullptr) {
   bool fast = row_mode ? rowproj_fast_ok(rows, cols, r) : colproj_fast_ok(rows, cols, r);
   fast = fast && (ld_m % 8) == 0 && (gdt == DION_DTYPE_NONE || (ld_g % 8) == 0);
   for (int b = 0; b < batch && fast; ++b)
@@ -3734,6 +3772,7 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
   }
   a.out = geo.nchunk > 1 ? static_cast<float*>(ws) : out;
   a.nonzero = nonzero;
+  a.mabs = mabs;
   a.rows = rows;
   a.cols = cols;
   a.r = r;
@@ -4215,8 +4254,8 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
   return DION_OK;
 }
 
-int dion_project_r(const DionBatchDesc* d, const float* const* M, const float* P, float* R, void* ws,
-                   size_t ws_bytes, dion_stream_t stream) {
+int dion_project_r(const DionBatchDesc* d, const float* const* M, const float* P, float* R,
+                   const uint32_t* m_absmax, void* ws, size_t ws_bytes, dion_stream_t stream) {
   int rc = validate(d);
   if (rc != DION_OK) return rc;
   if (M == nullptr || P == nullptr || R == nullptr) return fail(DION_E_INVALID, "null argument");
@@ -4242,7 +4281,8 @@ int dion_project_r(const DionBatchDesc* d, const float* const* M, const float* P
     const float* thin[MAXB];
     for (int b = 0; b < nb; ++b) thin[b] = P + static_cast<long>(b0 + b) * mp * d->r;
     rc = run_projection(d->transposed != 0, d->m, d->n, d->r, nb, nullptr, const_cast<float* const*>(M + b0), thin,
-                        ld_m, 0, DION_DTYPE_NONE, R + static_cast<long>(b0) * nq * d->r, nullptr, ws, ws_bytes, st);
+                        ld_m, 0, DION_DTYPE_NONE, R + static_cast<long>(b0) * nq * d->r, nullptr, ws, ws_bytes, st,
+                        m_absmax != nullptr ? m_absmax + b0 : nullptr);
     if (rc != DION_OK) return rc;
   }
   return DION_OK;

@@ -312,7 +312,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         yield
         work.wait()
         R = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
-        codec.project_r(list(momentums[:real]), P, R, transposed)
+        codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero)
         if use_low_rank:
             work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
             yield
@@ -347,7 +347,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
             work.wait()
         P = P[:B]
         R = torch.zeros((B, nq, r), dtype=torch.float32, device=dev)
-        codec.project_r(list(momentums[:real]), P, R, transposed)
+        codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero)
         if use_low_rank:
             work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
             yield
@@ -366,7 +366,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         if phase_marks:
             yield "stream"
         R = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
-        codec.project_r(list(momentums[:real]), P, R, transposed)
+        codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero)
 
     eps = float(optimizer.defaults["epsilon"])
     codec.fixup_colnorm(P, R, list(Qs[:real]), nonzero, eps, m, n, transposed)
@@ -476,7 +476,7 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         for k, idx in enumerate(indices):
             P[idx].copy_(gathered[k])
     R = torch.zeros((B, nq, r), dtype=torch.float32, device=dev)
-    codec.project_r(list(momentums[:real]), P, R, transposed)
+    codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero)
     if use_low_rank and rworld > 1:
         work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=rgroup, async_op=True)
         yield

@@ -48,7 +48,7 @@ class OracleCodec:
     def round_bf16(self, X):
         X.copy_(X.to(torch.bfloat16).float())
 
-    def project_r(self, momentums, P, R, transposed):
+    def project_r(self, momentums, P, R, transposed, nonzero=None):
         for b, M in enumerate(momentums):
             X = M.mT if transposed else M
             R[b] = X.mT @ P[b].to(X.dtype)

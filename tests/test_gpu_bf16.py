@@ -211,7 +211,7 @@ def test_bf16_llama_shape_properties(m, n):
     nz = torch.zeros(1, dtype=torch.int32, device=dev)
     codec.project_p([G], [M], [Q], P, nz, transposed)
     torch.cuda.synchronize()
-    assert torch.equal(M, X0) and int(nz[0]) == 1
+    assert torch.equal(M, X0) and int(nz[0]) != 0
     assert torch.equal(P, P.to(torch.bfloat16).float())
     Xo = (X0.t() if transposed else X0).double()
     v = torch.randn(r, 1, device=dev, dtype=torch.float64)
