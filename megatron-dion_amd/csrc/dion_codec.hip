@@ -3032,21 +3032,51 @@ __device__ __forceinline__ float max8abs(const f32x4& a, const f32x4& b) {
 // per-matrix max |x| of a small factor (rows x r fp32), as the float's bit pattern
 // (non-negative floats order like their bits; a NaN sorts above inf)
 struct AbsMaxArgs {
-  const float* src[MAXB];
-  uint32_t* out;  // (batch,) zero-initialised
-  long count;     // values per matrix
+  const float* src[3 * MAXB];  // group-major: matrix b of group k at k * nb + b (null: skipped)
+  uint32_t* out;               // (groups * nb,) zero-initialised, same order
+  long count[3];               // values per matrix of each group
+  int nb;                      // matrices per group
+  int vec;                     // every src 16-byte aligned and every count % 4 == 0
 };
 
+// all groups in one launch: blockIdx.y = k * nb + b, blocks stride over the matrix in
+// 16-byte loads (4 in flight per thread)
 __global__ void __launch_bounds__(256) absmax_kernel(const AbsMaxArgs a) {
-  const int b = blockIdx.y;
-  const float* __restrict__ src = a.src[b];
+  const int y = blockIdx.y;
+  const long count = a.count[y / a.nb];
+  const float* __restrict__ src = a.src[y];
   uint32_t m = 0;
-  if (src != nullptr)
-    for (long i = static_cast<long>(blockIdx.x) * 256 + threadIdx.x; i < a.count; i += static_cast<long>(gridDim.x) * 256)
-      m = max(m, __float_as_uint(src[i]) & 0x7FFFFFFFu);
+  if (src != nullptr) {
+    const long stride = static_cast<long>(gridDim.x) * 256;
+    long i = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
+    if (a.vec) {
+      const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
+      const long n4 = count / 4;
+      for (; i + 3 * stride < n4; i += 4 * stride) {
+        f32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = s4[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) m = max(m, __float_as_uint(v[u][q]) & 0x7FFFFFFFu);
+      }
+      for (; i < n4; i += stride) {
+        const f32x4 v = s4[i];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m = max(m, __float_as_uint(v[q]) & 0x7FFFFFFFu);
+      }
+    } else {
+      for (; i < count; i += stride) m = max(m, __float_as_uint(src[i]) & 0x7FFFFFFFu);
+    }
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), off, 64)));
-  if ((threadIdx.x & 63) == 0) atomicMax(&a.out[b], m);
+  // one atomic per block: many blocks hammering one address serialise at the L2
+  __shared__ uint32_t wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&a.out[y], max(max(wm[0], wm[1]), max(wm[2], wm[3])));
 }
 
 // h3 pre-split of a small factor in the MFMA operand layouts of presplit_kernel, two fp16
@@ -3107,6 +3137,9 @@ __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a)
 // pre-split P is the A operand (A[row j = 16 cb + t'][k]), one scale per matrix.  Each
 // step's product lands in a fresh accumulator D[j][col] (lane (t, g): R rows CT t + c,
 // r columns 16 cb + 4 g + q) and is added as acc += D / s_col.
+#ifndef DION_PBX
+#define DION_PBX 0  // dev experiments on colproj_h3_kernel's fixed-scale loop (0 = product)
+#endif
 template <int RB, int NW, int CT>
 __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : 2) colproj_h3_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
@@ -3166,7 +3199,12 @@ __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : 2) colproj_h3_kernel(co
             const f32x4 lo4{X.x[0][c], X.x[1][c], X.x[2][c], X.x[3][c]};
             const f32x4 hi4{X.x[4][c], X.x[5][c], X.x[6][c], X.x[7][c]};
             if constexpr (FIX) {
+#if DION_PBX == 2 || DION_PBX == 3  // dev experiment: no split (raw bits)
+              B[c].hi = __builtin_bit_cast(f16x8, lo4);
+              B[c].lo = __builtin_bit_cast(f16x8, hi4);
+#else
               split2h(lo4, hi4, fs, B[c]);
+#endif
             } else {
               float m8 = max8abs(lo4, hi4);
               m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
@@ -3183,7 +3221,11 @@ __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : 2) colproj_h3_kernel(co
 #pragma unroll
             for (int c = 0; c < CT; ++c) {
               if constexpr (FIX) {
+#if DION_PBX == 1 || DION_PBX == 3  // dev experiment: no MFMA
+                acc[c][cb][0] += static_cast<float>(B[c].hi[cb & 7]) + static_cast<float>(A.lo[c & 7]);
+#else
                 acc[c][cb] = mfma3h(A, B[c], acc[c][cb]);
+#endif
               } else {
                 const f32x4 d = mfma3h(A, B[c], f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
@@ -3653,6 +3695,22 @@ OrthoPlan ortho_plan(int mp, int r, int batch, float oversample) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// one absmax_kernel launch over `groups` groups of nb matrices (AbsMaxArgs order)
+void launch_absmax(AbsMaxArgs& ma, int groups, hipStream_t st) {
+  long most = 0;
+  bool vec = true;
+  for (int k = 0; k < groups; ++k) {
+    most = ma.count[k] > most ? ma.count[k] : most;
+    vec = vec && ma.count[k] % 4 == 0;
+    for (int b = 0; b < ma.nb; ++b) vec = vec && (ma.src[k * ma.nb + b] == nullptr || aligned16(ma.src[k * ma.nb + b]));
+  }
+  ma.vec = vec ? 1 : 0;
+  long bx = ceil_div(most, 256L * 16);  // >= 4 16-byte loads per thread, <= 32 blocks per matrix
+  bx = bx < 1 ? 1 : (bx > 32 ? 32 : bx);
+  hipLaunchKernelGGL(absmax_kernel, dim3(static_cast<unsigned>(bx), groups * ma.nb), dim3(256), 0, st, ma);
+}
+
+
 template <class F>
 int dispatch_rb(int r, F&& f) {
   switch (rblocks16(r)) {
@@ -3722,9 +3780,9 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     memset(&ma, 0, sizeof(ma));
     for (int b = 0; b < batch; ++b) ma.src[b] = thin[b];
     ma.out = amax;
-    ma.count = per;
-    const long mblocks = ceil_div(per, 256) < 64 ? ceil_div(per, 256) : 64;
-    hipLaunchKernelGGL(absmax_kernel, dim3(static_cast<unsigned>(mblocks), batch), dim3(256), 0, st, ma);
+    ma.count[0] = per;
+    ma.nb = batch;
+    launch_absmax(ma, 1, st);
     Presplit16Args pa;
     memset(&pa, 0, sizeof(pa));
     for (int b = 0; b < batch; ++b) pa.src[b] = thin[b];
@@ -4143,15 +4201,17 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
       hipError_t me = hipMemsetAsync(amax, 0, sizeof(uint32_t) * 3 * nb, st);
       if (me != hipSuccess) return fail(DION_E_LAUNCH, "memset: %s", hipGetErrorString(me));
       AbsMaxArgs ma;
-      for (int which = 0; which < 3; ++which) {
-        memset(&ma, 0, sizeof(ma));
-        for (int b = 0; b < nb; ++b)
-          ma.src[b] = which == 0 ? Q[b0 + b] : (which == 1 ? ef->R[b0 + b] : ef->P[b0 + b]);
-        ma.out = amax + which * nb;
-        ma.count = static_cast<long>(which == 2 ? mp : nq) * d->r;
-        const long mb = ceil_div(ma.count, 256) < 64 ? ceil_div(ma.count, 256) : 64;
-        hipLaunchKernelGGL(absmax_kernel, dim3(static_cast<unsigned>(mb), nb), dim3(256), 0, st, ma);
+      memset(&ma, 0, sizeof(ma));
+      for (int b = 0; b < nb; ++b) {
+        ma.src[b] = Q[b0 + b];
+        ma.src[nb + b] = ef->R[b0 + b];
+        ma.src[2 * nb + b] = ef->P[b0 + b];
       }
+      ma.out = amax;
+      ma.count[0] = ma.count[1] = static_cast<long>(nq) * d->r;
+      ma.count[2] = static_cast<long>(mp) * d->r;
+      ma.nb = nb;
+      launch_absmax(ma, 3, st);
       Presplit16Args pa;
       memset(&pa, 0, sizeof(pa));
       pa.rows = nq;

@@ -212,13 +212,39 @@ class MegatronDion(Optimizer):
         main = torch.cuda.current_stream(dev)
         for s in self._streams:
             s.wait_stream(main)
-        for i, b in enumerate(batches):
-            with torch.cuda.stream(self._streams[i % len(self._streams)]):
+        for b, si in self._stream_plan(batches):
+            with torch.cuda.stream(self._streams[si]):
                 for _ in run_dion_batch_async(self, b, sketches=sketches(b) if sketches else None):
                     raise RuntimeError("[DION_INTERNAL] a world-size-1 batch yielded")
         for s in self._streams:
             main.wait_stream(s)
         return True
+
+    def _stream_plan(self, batches):
+        """(batch, stream index) in issue order.  "rr": round robin in the reference's batch
+        order.  "stagger": largest launch groups first, each to the stream with the least
+        queued work (elements), except that stream 1 opens with the smallest group, so the
+        streams' latency-bound orthonormalisations do not fall together."""
+        n = len(self._streams)
+        order = os.environ.get("DION_LOCAL_ORDER", "stagger")
+        if order == "rr" or n < 2 or len(batches) < 3:
+            return [(b, i % n) for i, b in enumerate(batches)]
+
+        def work(b):
+            m, k = b.params[0].shape[-2:]
+            return int(b.real_batch_size) * int(m) * int(k)
+
+        rest = sorted(range(len(batches)), key=lambda i: -work(batches[i]))
+        first_small = rest.pop()  # the smallest group opens stream 1
+        load = [0] * n
+        plan = [(rest[0], 0), (first_small, 1)]
+        load[0] += work(batches[rest[0]])
+        load[1] += work(batches[first_small])
+        for i in rest[1:]:
+            si = min(range(n), key=lambda k: load[k])
+            plan.append((i, si))
+            load[si] += work(batches[i])
+        return [(batches[i], si) for i, si in plan]
 
     def _run_local_pipelined(self, batches, sketches) -> bool:
         """World-size-1 schedule, software-pipelined over two HIP streams.

@@ -20,6 +20,8 @@ Qs = [torch.randn(nq, r, device=dev) for _ in range(B)]
 P = torch.randn(B, mp, r, device=dev) * 0.01
 R = torch.randn(B, nq, r, device=dev) * 0.01
 nz = torch.ones(B, dtype=torch.int32, device=dev)
+# pass A's flags for these M (max |M| bits): the fixed-scale pass B ("pbf")
+nzf = torch.stack([M.abs().max() for M in Ms]).view(torch.int32).contiguous()
 def run():
     if op.startswith("pa_ef0"):
         codec.project_p_ef(Gs, Ms, Qs, P, nz, T, [None] * B, [None] * B, -0.05)
@@ -27,6 +29,8 @@ def run():
         codec.project_p_ef(Gs, Ms, Qs, P, nz, T, [P[i] for i in range(B)], [R[i] for i in range(B)], -0.05)
     elif op.startswith("pa"):
         codec.project_p(Gs, Ms, Qs, P, nz, T)
+    elif op.startswith("pbf"):
+        codec.project_r(Ms, P, R, T, nonzero=nzf)
     elif op.startswith("pb"):
         codec.project_r(Ms, P, R, T)
     elif op.startswith("w"):
