@@ -3213,20 +3213,46 @@ __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : 2) colproj_h3_kernel(co
               split2h(lo4, hi4, sc, B[c]);
             }
           }
+          if constexpr (FIX) {
+            // the three products term by term over all (c, cb): consecutive MFMAs are
+            // independent (a back-to-back dependent MFMA waits for its predecessor)
+            Split2h A[RB];
 #pragma unroll
-          for (int cb = 0; cb < RB; ++cb) {
-            Split2h A;
-            A.hi = tq[cur][(cb * 2 + 0) * 64 + lane];
-            A.lo = tq[cur][(cb * 2 + 1) * 64 + lane];
+            for (int cb = 0; cb < RB; ++cb) {
+              A[cb].hi = tq[cur][(cb * 2 + 0) * 64 + lane];
+              A[cb].lo = tq[cur][(cb * 2 + 1) * 64 + lane];
+            }
+#if DION_PBX == 1 || DION_PBX == 3  // dev experiment: no MFMA (every split value stays live)
 #pragma unroll
             for (int c = 0; c < CT; ++c) {
-              if constexpr (FIX) {
-#if DION_PBX == 1 || DION_PBX == 3  // dev experiment: no MFMA
-                acc[c][cb][0] += static_cast<float>(B[c].hi[cb & 7]) + static_cast<float>(A.lo[c & 7]);
+              const u32x4 hb = __builtin_bit_cast(u32x4, B[c].hi) ^ __builtin_bit_cast(u32x4, B[c].lo);
+              acc[c][0] = __builtin_bit_cast(f32x4, __builtin_bit_cast(u32x4, acc[c][0]) ^ hb);
+            }
 #else
-                acc[c][cb] = mfma3h(A, B[c], acc[c][cb]);
+#pragma unroll
+            for (int c = 0; c < CT; ++c)
+#pragma unroll
+              for (int cb = 0; cb < RB; ++cb)
+                acc[c][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].lo, B[c].hi, acc[c][cb], 0, 0, 0);
+#pragma unroll
+            for (int c = 0; c < CT; ++c)
+#pragma unroll
+              for (int cb = 0; cb < RB; ++cb)
+                acc[c][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].hi, B[c].lo, acc[c][cb], 0, 0, 0);
+#pragma unroll
+            for (int c = 0; c < CT; ++c)
+#pragma unroll
+              for (int cb = 0; cb < RB; ++cb)
+                acc[c][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].hi, B[c].hi, acc[c][cb], 0, 0, 0);
 #endif
-              } else {
+          } else {
+#pragma unroll
+            for (int cb = 0; cb < RB; ++cb) {
+              Split2h A;
+              A.hi = tq[cur][(cb * 2 + 0) * 64 + lane];
+              A.lo = tq[cur][(cb * 2 + 1) * 64 + lane];
+#pragma unroll
+              for (int c = 0; c < CT; ++c) {
                 const f32x4 d = mfma3h(A, B[c], f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
                 for (int q = 0; q < 4; ++q) acc[c][cb][q] = fmaf(d[q], inv[c], acc[c][cb][q]);
