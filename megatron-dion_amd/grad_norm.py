@@ -1,15 +1,32 @@
 """Dion term of the gradient norm, on device.
 
-Mirrors /root/reference/megatron/core/optimizer/distrib_dion/grad_norm.py:144-258
-(`_dion_grad_norm_sq`), which Megatron calls before the step when gradient
-clipping is on:
-  * no replica group (or size 1): the fp64 sum of squares of the local Dion
-    gradients (:166-172);
-  * replica group of size W > 1: the gradients are copied into one flat buffer per
-    dtype, all-reduced across the replicas with the replicate op (AVG when
-    `rp_average_in_collective`, else SUM; runtime.py:361-364) and the sum of squares
-    of the reduced buffer is taken (:214-233).  The local gradients are not modified.
-    With `count_dion_grad=False` the all-reduce still runs and None is returned.
+Megatron calls this before the step when gradient clipping is on.  The reference,
+/root/reference/megatron/core/optimizer/distrib_dion/grad_norm.py:144-258
+(`_dion_grad_norm_sq`), returns the fp64 sum of squares of the Dion gradients:
+  * no replica group (or size 1): of the local gradients (:166-172);
+  * replica group of size W > 1: of the gradients reduced across the replicas with the
+    replicate op (AVG when `rp_average_in_collective`, else SUM; runtime.py:361-364).  It
+    copies every Dion gradient into one flat buffer per dtype and ALL-REDUCES it
+    (:214-233) -- a dense exchange of the whole gradient, which is exactly the traffic
+    Dion's low-rank sync exists to avoid.  Local gradients are not modified.  With
+    `count_dion_grad=False` the collective still runs and None is returned.
+
+This module keeps the returned value and replaces the exchange:
+  * mode="exact" (default): the same number with half the traffic and bounded memory.
+    The gradients are packed, in `chunk_bytes` pieces (not one flat copy of the whole set:
+    the reference's copy is 14 GB on Llama-3-8B), into a staging buffer that is
+    REDUCE-SCATTERED with the replicate op: each rank receives 1/W of the reduced chunk,
+    squares and sums it on device, and one all-reduce of the fp64 scalar (SUM) gives
+    every rank the total.  Per rank that moves (W-1)/W of the gradient bytes instead of
+    the all-reduce's 2 (W-1)/W, and nothing is all-gathered back.  The reduced values
+    are those of the reference's all-reduce (same op, same dtype); the fp64 sum runs in
+    a different order (per shard, then across shards), so the total agrees to fp64
+    rounding, not bitwise.
+  * mode="local_bound": no gradient traffic at all.  Returns mean_i ||G_i||^2 over the
+    replicas (one scalar all-reduce), which bounds ||mean_i G_i||^2 from above (convexity
+    of the square), so clipping with it never clips less than the exact norm would.
+    An opt-in deviation from the reference's number, for runs where the dense exchange
+    costs more than the conservative clip.
 The sum of squares runs in the HIP kernel `dion_grad_sum_sq` (fp64, exact squares,
 fixed order), reading each gradient once in its own dtype: the reference's chunked
 `.to(float64)` copies (:54-68) disappear.  The reference's dense-RP reduced-gradient
@@ -26,6 +43,7 @@ import torch.distributed as dist
 __all__ = ["dion_grad_norm_sq", "dion_grad_norm", "as_matrices"]
 
 _FLAT_COLS = 1 << 20
+_CHUNK_BYTES = 256 << 20
 
 
 def as_matrices(flat: torch.Tensor) -> List[torch.Tensor]:
@@ -42,14 +60,70 @@ def as_matrices(flat: torch.Tensor) -> List[torch.Tensor]:
     return out
 
 
+def _abi_views(g: torch.Tensor) -> List[torch.Tensor]:
+    """A gradient as matrices the kernel accepts: 2-D row-major ones as they are (n fits
+    int32), anything else through its flat view (non-2D or very wide grads
+    would overflow the descriptor's int32 n)."""
+    if g.dim() == 2 and g.stride(1) == 1 and g.shape[1] <= _FLAT_COLS:
+        return [g]
+    return as_matrices(g.detach().reshape(-1))
+
+
 def _replicate_op(optimizer):
     avg = bool(getattr(optimizer, "defaults", {}).get("rp_average_in_collective", True))
     return dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
 
 
+def _local_sum_sq(codec, grads, device) -> torch.Tensor:
+    total = torch.zeros(1, dtype=torch.float64, device=device)
+    mats = [m for g in grads for m in _abi_views(g)]
+    if mats:
+        codec.grad_sum_sq(mats, total)
+    return total
+
+
+def _reduced_sum_sq(codec, members, op, group, world, device, dtype, chunk_bytes) -> torch.Tensor:
+    """fp64 sum of squares of the replica-reduced `members` (one dtype), by chunked
+    reduce-scatter; this rank's partial (the caller sums the partials over the group)."""
+    total = torch.zeros(1, dtype=torch.float64, device=device)
+    esize = torch.empty((), dtype=dtype).element_size()
+    cap = max(world, (max(chunk_bytes // esize, world) // world) * world)
+    numel = sum(int(g.numel()) for g in members)
+    staging = torch.empty(min(cap, -(-numel // world) * world), dtype=dtype, device=device)
+    fill = 0
+
+    def flush(n):
+        if n == 0:
+            return
+        padded = -(-n // world) * world
+        if padded > n:
+            staging[n:padded].zero_()  # zeros reduce to zeros and add nothing
+        shard = torch.empty(padded // world, dtype=dtype, device=device)
+        dist.reduce_scatter_tensor(shard, staging[:padded], op=op, group=group)
+        codec.grad_sum_sq(as_matrices(shard), total)
+
+    for g in members:
+        flat = g.detach().reshape(-1)
+        pos = 0
+        while pos < flat.numel():
+            take = min(int(flat.numel()) - pos, staging.numel() - fill)
+            staging[fill:fill + take].copy_(flat[pos:pos + take])
+            fill += take
+            pos += take
+            if fill == staging.numel():
+                flush(fill)
+                fill = 0
+    flush(fill)
+    return total
+
+
 def dion_grad_norm_sq(optimizer, grads: Sequence[torch.Tensor], *, count_dion_grad: bool = True,
-                      replica_group=None) -> Optional[torch.Tensor]:
-    """Sum of squares (fp64, shape (1,), on the gradients' device) of the Dion gradients."""
+                      replica_group=None, mode: str = "exact",
+                      chunk_bytes: int = _CHUNK_BYTES) -> Optional[torch.Tensor]:
+    """Sum of squares (fp64, shape (1,), on the gradients' device) of the Dion gradients
+    (of their replica reduction when `replica_group` has more than one rank)."""
+    if mode not in ("exact", "local_bound"):
+        raise RuntimeError(f"[DION_INVALID_GRAD_NORM_MODE] mode={mode!r}")
     grads = [g for g in grads if g is not None]
     if not grads:
         return None
@@ -57,29 +131,23 @@ def dion_grad_norm_sq(optimizer, grads: Sequence[torch.Tensor], *, count_dion_gr
     world = dist.get_world_size(replica_group) if (replica_group is not None and dist.is_initialized()) else 1
     dev = grads[0].device
     if world <= 1:
-        if not count_dion_grad:
-            return None
-        total = torch.zeros(1, dtype=torch.float64, device=dev)
-        codec.grad_sum_sq([g if g.dim() == 2 else g.reshape(1, -1) for g in grads], total)
-        return total
+        return _local_sum_sq(codec, grads, dev) if count_dion_grad else None
+    if mode == "local_bound":
+        total = _local_sum_sq(codec, grads, dev)
+        dist.all_reduce(total, op=dist.ReduceOp.SUM, group=replica_group)
+        total /= world
+        return total if count_dion_grad else None
+    op = _replicate_op(optimizer)
     groups = {}
     for g in grads:
         groups.setdefault((g.dtype, g.device), []).append(g)
-    total = None
+    total = torch.zeros(1, dtype=torch.float64, device=dev)
     for (dtype, device), members in groups.items():
-        numel = sum(int(g.numel()) for g in members)
-        if numel <= 0:
+        if sum(int(g.numel()) for g in members) <= 0:
             continue
-        flat = torch.empty(numel, dtype=dtype, device=device)
-        cursor = 0
-        for g in members:
-            flat[cursor:cursor + g.numel()].copy_(g.detach().reshape(-1))
-            cursor += g.numel()
-        dist.all_reduce(flat, op=_replicate_op(optimizer), group=replica_group)
-        if count_dion_grad:
-            if total is None:
-                total = torch.zeros(1, dtype=torch.float64, device=device)
-            codec.grad_sum_sq(as_matrices(flat), total)
+        total += _reduced_sum_sq(codec, members, op, replica_group, world, device, dtype,
+                                 int(chunk_bytes)).to(dev)
+    dist.all_reduce(total, op=dist.ReduceOp.SUM, group=replica_group)
     return total if count_dion_grad else None
 
 

@@ -26,7 +26,7 @@ import torch.distributed as dist
 from torch.optim.optimizer import Optimizer
 
 from .batches import build_dion_batches
-from .runtime import (AsyncRuntime, coalesce_local_batches, coalesce_replicated_batches,
+from .runtime import (AsyncRuntime, DionStateMap, coalesce_local_batches, coalesce_replicated_batches,
                       drop_pending_error_feedback, flush_pending_error_feedback, is_replicated,
                       run_dion_batch_async)
 from .state import init_dion_state
@@ -62,6 +62,10 @@ class MegatronDion(Optimizer):
                         scale_mode=scale_mode, extra_scale_factor=extra_scale_factor, split_qkv=bool(split_qkv),
                         split_linear=bool(split_linear), algorithm="dion", step=0)
         super().__init__(params, defaults)
+        # states apply a deferred error feedback before any read of the momentum from
+        # outside the step (DionParamState), whoever creates or restores them
+        self.state = DionStateMap(self, self.state)
+        self._dion_in_step = False
         self._global_rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
         self.is_distributed_mode = False
         self.use_fs_collectives = use_fs_collectives
@@ -122,7 +126,9 @@ class MegatronDion(Optimizer):
         load_state_dict, dion_distrib_optimizer.py:4218-4260), so the pending key is gone by
         then."""
         drop_pending_error_feedback(self)
-        return super().load_state_dict(state_dict)
+        out = super().load_state_dict(state_dict)
+        self.state = DionStateMap(self, self.state)
+        return out
 
     # ------------------------------------------------------------------ plugin surface
     def enable_distributed_mode(self, *, route_step_params=None) -> None:
@@ -331,6 +337,14 @@ class MegatronDion(Optimizer):
             raise RuntimeError(f"[DION_STEP_REQUIRES_DISTRIBUTED_MODE] step={self._step_count}")
         profile = os.environ.get("DION_PROFILE_SPLIT", "").lower() in ("1", "true", "yes")
         t0 = time.perf_counter() if profile else None
+        self._dion_in_step = True
+        try:
+            self._step_batches(profile, t0)
+        finally:
+            self._dion_in_step = False
+        return loss
+
+    def _step_batches(self, profile, t0):
         width = 3 if self.max_concurrent_tasks is None else int(self.max_concurrent_tasks)
         sketches = getattr(self, "_sketch_override", None)
         batches, elementwise = self._batches()
@@ -350,7 +364,6 @@ class MegatronDion(Optimizer):
         if profile:
             torch.cuda.synchronize()
             self._profile_records.append(("step", time.perf_counter() - t0))
-        return loss
 
 
 def _elementwise_moment(state, param, key, legacy, dtype):

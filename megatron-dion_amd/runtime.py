@@ -14,6 +14,8 @@ concurrent same-shape batches read each other's P).
 """
 from __future__ import annotations
 
+import collections
+import weakref
 from typing import Callable, Generator, Iterable, List, Optional
 
 import torch
@@ -264,8 +266,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
              and (commit_updates is None or all(c is None for c in commit_updates[:real]))
              and not bf16_state and codec.supports_deferred_ef(m, n, r, transposed))
-    pending = [optimizer_states[i].pop(_PENDING_EF, None) if optimizer_states[i] is not None else None
-               for i in range(real)]
+    pending = [_take_pending(optimizer_states[i]) for i in range(real)]
     if any(p is not None for p in pending):
         alphas = {p[2] for p in pending if p is not None}
         if defer and len(alphas) == 1:
@@ -387,7 +388,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         # weights now; this step's error feedback waits for the next pass A (or a flush)
         codec.ef_apply(None, list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd, scaled, transposed)
         for i in range(real):
-            optimizer_states[i][_PENDING_EF] = (P[i], R[i], -(1.0 - mu))
+            _record_pending(optimizer_states[i], P[i], R[i], -(1.0 - mu))
     else:
         codec.ef_apply(list(momentums[:real]), list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd,
                        scaled, transposed)
@@ -496,8 +497,7 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
 def _project_with_pending(codec, real_grads, momentums, Qs, P, nonzero, optimizer_states, real, m, n, transposed,
                           defer):
     """Pass A: M (+ the pending error feedback of the previous step) += G; P = X Q."""
-    pending = [optimizer_states[i].pop(_PENDING_EF, None) if optimizer_states[i] is not None else None
-               for i in range(real)]
+    pending = [_take_pending(optimizer_states[i]) for i in range(real)]
     if any(p is not None for p in pending):
         alphas = {p[2] for p in pending if p is not None}
         if defer and len(alphas) == 1:
@@ -530,7 +530,7 @@ def _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim
     if defer:
         codec.ef_apply(None, list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd, scaled, transposed)
         for i in range(real):
-            optimizer_states[i][_PENDING_EF] = (P[i], R[i], -(1.0 - mu))
+            _record_pending(optimizer_states[i], P[i], R[i], -(1.0 - mu))
     else:
         codec.ef_apply(list(momentums[:real]), list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd,
                        scaled, transposed)
@@ -544,11 +544,116 @@ def _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim
         sink(P[:real], R[:real])
 
 
-# optimizer-state key of a pending (deferred) error feedback: (P_b, R_b, alpha).  The
-# leading underscore keeps it out of the reference's persistent checkpoint state
-# (distrib_dion/checkpoint_io.py:247-266); MegatronDion.flush_error_feedback()
-# applies it before any state is saved.
+# optimizer-state key of a pending (deferred) error feedback: (P_b, R_b, alpha, M ref).
+# The leading underscore keeps it out of the reference's persistent checkpoint state
+# (distrib_dion/checkpoint_io.py:247-266), so the momentum must carry it before anything
+# outside the step reads it: DionParamState applies it on such a read, and
+# MegatronDion.flush_error_feedback() applies all of them.  The weak reference names the
+# momentum tensor the factors belong to: a restore that replaces the momentum
+# (checkpoint_io.py:300-330 keeps the live underscore keys) orphans the entry, and an
+# orphan is dropped, never applied to the restored value.
 _PENDING_EF = "_dion_pending_ef"
+
+
+def _record_pending(state, P_b, R_b, alpha) -> None:
+    M = dict.get(state, "momentum")
+    dict.__setitem__(state, _PENDING_EF, (P_b, R_b, alpha, weakref.ref(M) if M is not None else None))
+
+
+def _take_pending(state):
+    """Pop one state's pending error feedback as (P_b, R_b, alpha); None when there is none
+    or when it was recorded for a momentum tensor the state no longer holds."""
+    if state is None:
+        return None
+    pend = dict.pop(state, _PENDING_EF, None)
+    if pend is None:
+        return None
+    ref = pend[3] if len(pend) > 3 else None
+    if ref is not None and ref() is not dict.get(state, "momentum"):
+        return None
+    return pend[:3]
+
+
+class DionParamState(dict):
+    """A Dion parameter's optimizer state that applies its pending error feedback before
+    any read of the momentum from outside the step (`state["momentum"]`, `.get`,
+    `.items()`, `.values()`, copies, pickling): checkpoint writers such as the reference's
+    build_persistent_param_state (checkpoint_io.py:247-266, which iterates `state.items()`
+    and skips underscore keys) then save the eager momentum.  Inside MegatronDion.step
+    the read is plain, so the deferral is kept."""
+
+    __slots__ = ("_owner",)
+
+    def __init__(self, *args, owner=None, **kwargs):
+        super().__init__(*args, **kwargs)
+        self._owner = owner
+
+    def _sync(self):
+        if not dict.__contains__(self, _PENDING_EF):
+            return
+        opt = self._owner() if self._owner is not None else None
+        if opt is None or getattr(opt, "_dion_in_step", False):
+            return
+        pend = _take_pending(self)
+        if pend is not None:
+            M = dict.__getitem__(self, "momentum")
+            transposed = pend[0].shape[0] != M.shape[0]
+            _apply_pending(opt.codec, M, dict.__getitem__(self, "Q"), pend, int(M.shape[0]), int(M.shape[1]),
+                           transposed)
+
+    def __getitem__(self, key):
+        if key == "momentum":
+            self._sync()
+        return dict.__getitem__(self, key)
+
+    def get(self, key, default=None):
+        if key == "momentum":
+            self._sync()
+        return dict.get(self, key, default)
+
+    def items(self):
+        self._sync()
+        return dict.items(self)
+
+    def values(self):
+        self._sync()
+        return dict.values(self)
+
+    def copy(self):
+        self._sync()
+        return dict(dict.items(self))
+
+    def __reduce__(self):
+        self._sync()
+        return (dict, (dict(dict.items(self)),))
+
+
+class DionStateMap(collections.defaultdict):
+    """`optimizer.state` of MegatronDion: new entries, and plain dicts assigned by a
+    restore (checkpoint_io.py:351 `optimizer_state[param] = new_state`), become
+    DionParamState."""
+
+    def __init__(self, owner, *args):
+        super().__init__(None, *args)
+        self._owner_ref = weakref.ref(owner)
+        for k in list(dict.keys(self)):
+            dict.__setitem__(self, k, self._wrap(dict.__getitem__(self, k)))
+
+    def _wrap(self, v):
+        if type(v) is dict:
+            return DionParamState(v, owner=self._owner_ref)
+        return v
+
+    def __missing__(self, key):
+        v = DionParamState(owner=self._owner_ref)
+        dict.__setitem__(self, key, v)
+        return v
+
+    def __setitem__(self, key, value):
+        dict.__setitem__(self, key, self._wrap(value))
+
+    def __reduce__(self):
+        return (dict, (dict(dict.items(self)),))
 
 
 def _apply_pending(codec, M, Q, pending, m, n, transposed):
@@ -563,12 +668,12 @@ def flush_pending_error_feedback(optimizer, get_codec) -> int:
     """Apply every deferred error feedback held in `optimizer.state`; returns how many."""
     count = 0
     codec = None
-    for p, st in optimizer.state.items():
-        pend = st.pop(_PENDING_EF, None) if isinstance(st, dict) else None
+    for p, st in dict.items(optimizer.state):
+        pend = _take_pending(st) if isinstance(st, dict) else None
         if pend is None:
             continue
         codec = codec or get_codec()
-        M, Q = st["momentum"], st["Q"]
+        M, Q = dict.__getitem__(st, "momentum"), dict.__getitem__(st, "Q")
         transposed = pend[0].shape[0] != M.shape[0]  # P has n rows iff transposed (m_P = n != m)
         _apply_pending(codec, M, Q, pend, int(M.shape[0]), int(M.shape[1]), transposed)
         count += 1
@@ -578,8 +683,8 @@ def flush_pending_error_feedback(optimizer, get_codec) -> int:
 def drop_pending_error_feedback(optimizer) -> int:
     """Forget every deferred error feedback (the momentum is about to be replaced)."""
     count = 0
-    for st in optimizer.state.values():
-        if isinstance(st, dict) and st.pop(_PENDING_EF, None) is not None:
+    for st in dict.values(optimizer.state):
+        if isinstance(st, dict) and dict.pop(st, _PENDING_EF, None) is not None:
             count += 1
     return count
 

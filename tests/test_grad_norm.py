@@ -38,33 +38,15 @@ def test_as_matrices_fits_the_abi():
     assert mats[1][0, -1].item() == n - 1
 
 
-def test_replica_sum_reduce_known_answer(monkeypatch):
-    # test_dion_optimizer_contracts.py:576-624
+def test_local_sum_without_a_replica_group():
     import megatron_dion_amd.grad_norm as gn
 
-    reduce_ops = []
-    group = object()
-
-    def fake_all_reduce(tensor, op, group=None):
-        reduce_ops.append(op)
-        if op == dist.ReduceOp.SUM:
-            tensor.mul_(2.0)
-
-    monkeypatch.setattr(gn.dist, "is_initialized", lambda: True)
-    monkeypatch.setattr(gn.dist, "get_world_size", lambda g=None: 2)
-    monkeypatch.setattr(gn.dist, "all_reduce", fake_all_reduce)
     opt = SimpleNamespace(defaults={"rp_average_in_collective": False}, codec=OracleCodec())
     ga, gb = torch.tensor([1.0, 2.0]), torch.tensor([3.0])
-    total = gn.dion_grad_norm_sq(opt, [ga, gb], replica_group=group)
-    assert reduce_ops == [dist.ReduceOp.SUM]
-    assert total.item() == 2.0 ** 2 + 4.0 ** 2 + 6.0 ** 2
-    assert ga.tolist() == [1.0, 2.0] and gb.tolist() == [3.0]
-    reduce_ops.clear()
-    assert gn.dion_grad_norm_sq(opt, [ga, gb], replica_group=group, count_dion_grad=False) is None
-    assert reduce_ops == [dist.ReduceOp.SUM]
-    # no replica group: the local sum, no collective
-    reduce_ops.clear()
-    assert gn.dion_grad_norm_sq(opt, [ga, gb]).item() == 14.0 and reduce_ops == []
+    assert gn.dion_grad_norm_sq(opt, [ga, gb]).item() == 14.0
+    assert gn.dion_grad_norm_sq(opt, [ga, gb], count_dion_grad=False) is None
+    with pytest.raises(RuntimeError, match="DION_INVALID_GRAD_NORM_MODE"):
+        gn.dion_grad_norm_sq(opt, [ga], mode="bogus")
 
 
 def _free_port():
@@ -80,12 +62,27 @@ def _worker(rank, world, port, out_dir):
     import megatron_dion_amd.grad_norm as gn
     from tests._cpu_codec import OracleCodec as Codec
 
+    out = {}
+    # test_dion_optimizer_contracts.py:576-624's known answer, on two real ranks: the same
+    # local grads, replicate op SUM -> the norm of 2 g; local grads untouched; with
+    # count_dion_grad=False the collectives still run and None comes back
+    opt_sum = SimpleNamespace(defaults={"rp_average_in_collective": False}, codec=Codec())
+    ga, gb = torch.tensor([1.0, 2.0]), torch.tensor([3.0])
+    out["kat"] = gn.dion_grad_norm_sq(opt_sum, [ga, gb], replica_group=dist.group.WORLD)
+    out["kat_untouched"] = torch.tensor(ga.tolist() == [1.0, 2.0] and gb.tolist() == [3.0])
+    out["kat_none"] = torch.tensor(gn.dion_grad_norm_sq(opt_sum, [ga, gb], replica_group=dist.group.WORLD,
+                                                        count_dion_grad=False) is None)
     gen = torch.Generator().manual_seed(10 + rank)
     grads = [(torch.randn(48, 80, generator=gen) * 1e-3).to(torch.bfloat16),
-             torch.randn(33, 17, generator=gen), (torch.randn(8, 8, generator=gen)).to(torch.bfloat16)]
+             torch.randn(33, 17, generator=gen), (torch.randn(8, 8, generator=gen)).to(torch.bfloat16),
+             torch.randn(3, 5, 7, generator=gen)]
     opt = SimpleNamespace(defaults={"rp_average_in_collective": True}, codec=Codec())
-    total = gn.dion_grad_norm_sq(opt, grads, replica_group=dist.group.WORLD)
-    torch.save({"grads": grads, "total": total}, os.path.join(out_dir, f"rank{rank}.pt"))
+    out["total"] = gn.dion_grad_norm_sq(opt, grads, replica_group=dist.group.WORLD)
+    # tiny staging chunks: many reduce-scatters, ragged tails, padding
+    out["chunked"] = gn.dion_grad_norm_sq(opt, grads, replica_group=dist.group.WORLD, chunk_bytes=100)
+    out["bound"] = gn.dion_grad_norm_sq(opt, grads, replica_group=dist.group.WORLD, mode="local_bound")
+    out["grads"] = grads
+    torch.save(out, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -94,10 +91,19 @@ def test_gloo_w2_grad_norm_of_the_averaged_gradient():
     with tempfile.TemporaryDirectory() as tmp:
         mp.start_processes(_worker, args=(2, _free_port(), tmp), nprocs=2, join=True, start_method="spawn")
         res = [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+    for r in range(2):
+        assert res[r]["kat"].item() == 2.0 ** 2 + 4.0 ** 2 + 6.0 ** 2
+        assert bool(res[r]["kat_untouched"]) and bool(res[r]["kat_none"])
     # the reference's semantics: all-reduce(AVG) in the gradient dtype, then the fp64 sum of squares
     avg = [((a.float() + b.float()) / 2).to(a.dtype) if a.dtype == torch.bfloat16 else (a + b) / 2
            for a, b in zip(res[0]["grads"], res[1]["grads"])]
     ref = O.grad_sum_sq_fp64(avg).item()
     for r in range(2):
         assert res[r]["total"].item() == pytest.approx(ref, rel=1e-6)
+        assert res[r]["chunked"].item() == pytest.approx(ref, rel=1e-6)
     assert res[0]["total"].item() == res[1]["total"].item()
+    # local_bound: the mean of the local squares, an upper bound of the exact value
+    bound = sum(O.grad_sum_sq_fp64(res[r]["grads"]).item() for r in range(2)) / 2
+    for r in range(2):
+        assert res[r]["bound"].item() == pytest.approx(bound, rel=1e-12)
+        assert res[r]["bound"].item() >= ref

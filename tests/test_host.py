@@ -290,12 +290,13 @@ def test_deferred_error_feedback_is_the_drop_in_default():
     assert isinstance(opt._buffer_cache, dict)  # cleared by DionDistributedOptimizer.offload_to_cpu
 
 
-def _ckpt_run(steps_before, steps_after, interrupt):
+def _ckpt_run(steps_before, steps_after, interrupt, via_load_state_dict=True):
     """Deferred-EF run over two matrices with a Megatron-style save / restore in the middle:
-    save = the adapter's state_dict() chain (distrib_optimizer.py:651 calls optimizer.state_dict())
-    followed by reading optimizer.state without '_' keys (checkpoint_io.py:247-268); restore =
-    optimizer.load_state_dict() (distrib_optimizer.py:740) then new tensors for every
-    persistent key, keeping the live '_' keys (checkpoint_io.py:271-336)."""
+    save = reading optimizer.state without '_' keys (checkpoint_io.py:247-268
+    build_persistent_param_state, which iterates `state.items()` and does NOT call
+    state_dict() first); restore = optionally optimizer.load_state_dict()
+    (distrib_optimizer.py:740), then new tensors for every persistent key, keeping the live
+    '_' keys (checkpoint_io.py:271-336)."""
     from megatron_dion_amd.optimizer import attach_dp_routing
     from megatron_dion_amd.runtime import _PENDING_EF
     from tests._cpu_codec import OracleCodec
@@ -324,18 +325,19 @@ def _ckpt_run(steps_before, steps_after, interrupt):
     for i in range(steps_before):
         step(i)
     if interrupt:
-        opt.state_dict()  # the save chain flushes the pending error feedback
+        assert all(_PENDING_EF in dict.keys(opt.state[p]) for _, p in named)  # deferred after a step
+        # the save reads the state directly: the read applies the pending error feedback
         saved = {n: {k: (v.clone() if torch.is_tensor(v) else v) for k, v in opt.state[p].items()
                      if not k.startswith("_")} for n, p in named}
-        assert all(_PENDING_EF not in opt.state[p] for _, p in named)
+        assert all(_PENDING_EF not in dict.keys(opt.state[p]) for _, p in named)
         step(steps_before)  # the run goes on, then is rolled back to the checkpoint
-        for n, p in named:
-            p.data.copy_(saved[n]["param"] if "param" in saved[n] else p.data)
-        live = {n: {k: v for k, v in opt.state[p].items() if k.startswith("_")} for n, p in named}
+        live = {n: {k: v for k, v in dict.items(opt.state[p]) if k.startswith("_")} for n, p in named}
         assert all(_PENDING_EF in live[n] for n in live)  # the live run holds a pending EF
-        opt.load_state_dict(opt.state_dict())  # drops pending; the adapter then restores tensors
+        if via_load_state_dict:
+            opt.load_state_dict(opt.state_dict())  # drops pending; the adapter then restores tensors
+            live = {n: {k: v for k, v in dict.items(opt.state[p]) if k.startswith("_")} for n, p in named}
         for n, p in named:
-            restored = {k: v for k, v in opt.state[p].items() if k.startswith("_")}
+            restored = dict(live[n])  # the live '_' keys (a stale pending EF, without load_state_dict)
             for k, v in saved[n].items():
                 restored[k] = v.clone() if torch.is_tensor(v) else v
             opt.state[p] = restored
@@ -343,17 +345,17 @@ def _ckpt_run(steps_before, steps_after, interrupt):
     return opt, named, step, None
 
 
-def test_checkpoint_round_trip_with_deferred_error_feedback():
-    """Restoring a checkpoint must not apply the live run's stale pending EF."""
-    from megatron_dion_amd.runtime import _PENDING_EF
-
+@pytest.mark.parametrize("via_load_state_dict", [True, False])
+def test_checkpoint_round_trip_with_deferred_error_feedback(via_load_state_dict):
+    """Save through a direct read of optimizer.state, restore that replaces the momentum
+    while keeping the live '_' keys: the saved momentum carries the pending EF and the
+    restored one never receives the live run's stale pending EF."""
     ref_opt, ref_named, ref_step, _ = _ckpt_run(3, 0, False)
     ref_opt.flush_error_feedback()
     # interrupted run: 3 steps, save, 1 more step, restore params + state from the checkpoint
-    opt, named, step, saved = _ckpt_run(3, 0, True)
+    opt, named, step, saved = _ckpt_run(3, 0, True, via_load_state_dict)
     for (n, p), (_, q) in zip(named, ref_named):
         p.data.copy_(q.data)  # the weights of the checkpointed step (the payload's "param")
-        assert _PENDING_EF not in opt.state[p]
         assert torch.equal(opt.state[p]["momentum"], ref_opt.state[q]["momentum"])
     for i in range(3, 5):
         step(i)
@@ -363,6 +365,26 @@ def test_checkpoint_round_trip_with_deferred_error_feedback():
     for (_, p), (_, q) in zip(named, ref_named):
         assert torch.allclose(p, q, rtol=0, atol=1e-7)
         assert torch.allclose(opt.state[p]["momentum"], ref_opt.state[q]["momentum"], rtol=0, atol=1e-9)
+
+
+def test_state_read_inside_the_step_keeps_the_deferral(monkeypatch):
+    """The batch builder reads state['momentum'] inside step(): no flush there, so the
+    deferred error feedback still rides on the next pass A (no late eager application)."""
+    import megatron_dion_amd.runtime as rt
+    from megatron_dion_amd.runtime import _PENDING_EF
+
+    calls = []
+    real = rt._apply_pending
+    monkeypatch.setattr(rt, "_apply_pending", lambda *a: (calls.append(1), real(*a)))
+    opt, named, step, _ = _ckpt_run(2, 0, False)
+    step(2)
+    assert calls == []
+    assert all(_PENDING_EF in dict.keys(opt.state[p]) for _, p in named)
+    _ = opt.state[named[1][1]]["momentum"]  # a read from outside the step applies it
+    assert calls == [1] and _PENDING_EF not in dict.keys(opt.state[named[1][1]])
+    assert type(opt.state[named[0][1]]).__name__ == "DionParamState"
+    opt.state[named[0][1]] = dict(dict.items(opt.state[named[0][1]]))  # a restore's plain dict
+    assert type(opt.state[named[0][1]]).__name__ == "DionParamState"
 
 
 def test_standalone_routing_sends_non_dion_params_to_the_elementwise_branch():
