@@ -5,7 +5,8 @@ Integer rules are bit-exact restatements of the reference:
   low-rank sync rule   dion/state.py:220-230 (should_use_low_rank_sync)
   orientation rule     dion/state.py:304-310 (is_transposed = m < n, no TP/FS)
   Q-init seed          dion/state.py:233-260 (blake2b of the param key)
-  Q-init values        dion/state.py:86-88 (CPU path: torch.randn(q_global_shape, generator=seed))
+  Q-init values        dion/state.py:50-109 (CPU: one torch.randn of the global shape;
+                       device: per-row Philox offsets, init_q)
 State layout follows dion/state.py:527-654: momentum = zeros like the param
 (m x n), Q = (n_Q x r), r, local_shape, global_shape.
 """
@@ -51,12 +52,38 @@ def q_seed_from_param_key(*, base_seed: int, param_uid, param_name: str,
     return int.from_bytes(hashlib.blake2b(key, digest_size=8).digest(), "little") & ((1 << 63) - 1)
 
 
-def init_q(q_global_shape: Tuple[int, int], seed: int, device, dtype=torch.float32) -> torch.Tensor:
-    """Q0 ~ N(0, 1): drawn on the CPU generator (the reference's CPU stream) then moved."""
-    gen = torch.Generator(device="cpu")
+def init_q(q_global_shape: Tuple[int, int], seed: int, device, dtype=torch.float32,
+           rows: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+    """Rows [rows[0], rows[1]) (default: all) of the seeded Q0 ~ N(0, 1) of the global shape,
+    drawn the way the reference draws on that device (dion/state.py:50-109,
+    _normal_q_submatrix):
+      * CPU: one torch.randn of the full global shape on a CPU generator, then the rows
+        (state.py:94-96);
+      * CUDA/HIP: every row from the device generator's Philox stream at the offset of the
+        row's first element rounded down to a multiple of 4, dropping the rounding prefix
+        (state.py:97-108), so any shard's rows are the full draw's rows.
+    Draws are made in `dtype` itself, as the reference does.  Pinned by the reference's
+    CPU captures (tests/test_host.py); the device stream is the same torch calls on the
+    same torch build, checked for shard consistency on the GPU (tests/test_gpu_parity.py)."""
+    q_rows, cols = (int(d) for d in q_global_shape)
+    r0, r1 = (0, q_rows) if rows is None else (int(rows[0]), int(rows[1]))
+    device = torch.device(device)
+    if device.type == "cpu":
+        gen = torch.Generator(device="cpu")
+        gen.manual_seed(int(seed))
+        q = torch.randn((q_rows, cols), generator=gen, dtype=dtype)
+        return q[r0:r1].contiguous()
+    gen = torch.Generator(device=device)
     gen.manual_seed(int(seed))
-    q = torch.randn(tuple(int(d) for d in q_global_shape), generator=gen, dtype=dtype)
-    return q.to(device)
+    q = torch.empty((r1 - r0, cols), device=device, dtype=dtype)
+    for i, row in enumerate(range(r0, r1)):
+        first = row * cols
+        base = first - first % 4
+        gen.set_offset(base)
+        draw = torch.empty(first - base + cols, device=device, dtype=dtype)
+        draw.normal_(0.0, 1.0, generator=gen)
+        q[i].copy_(draw[first - base:])
+    return q
 
 
 def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_of: int = 1,
@@ -70,7 +97,7 @@ def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_
     distrib_dion/parameter.py:424-466).  The rank r and the low-rank rule use the global shape
     (state.py:159-230); the orientation follows the shard dim (dim 0 -> transposed, dim 1 ->
     not, state.py:304-310) so the sharded dim is always the contraction side of P = X Q; Q is
-    the seeded global Q's rows [start, end) (state.py:50-109, the CPU stream).
+    the seeded global Q's rows [start, end), drawn on the parameter's device (init_q).
     `momentum_dtype` / `q_dtype` follow DionMixedPrecisionConfig (dion/state.py:502-514,
     544-547): None keeps the parameter's dtype; the speedrun sets both to bf16."""
     if param.dim() != 2:
@@ -92,12 +119,11 @@ def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_
     q_shape = (m if transposed else n, r)
     seed = q_seed_from_param_key(base_seed=base_seed, param_uid=param_uid, param_name=param_name,
                                  q_global_shape=q_shape, is_transposed=transposed)
-    q = init_q(q_shape, seed, "cpu", dtype=q_dtype or param.dtype)
-    if fs_shard is not None:
-        q = q[start:end]
+    q = init_q(q_shape, seed, param.device, dtype=q_dtype or param.dtype,
+               rows=None if fs_shard is None else (start, end))
     state = {
         "momentum": torch.zeros_like(param, dtype=momentum_dtype or param.dtype),
-        "Q": q.contiguous().to(param.device),
+        "Q": q,
         "r": r,
         "local_shape": (ml, nl),
         "global_shape": (m, n),

@@ -190,6 +190,7 @@ def _w2_worker(rank, world, port, out_dir):
     r, steps = 64, 3
     k = O.sketch_rows(r)
     res = {}
+    q0 = {}
     for backend in ("hip", "oracle"):
         on = dev if backend == "hip" else torch.device("cpu")
         named = [(n, torch.nn.Parameter((torch.randn(m, c, generator=torch.Generator().manual_seed(i)) * 0.02)
@@ -198,6 +199,13 @@ def _w2_worker(rank, world, port, out_dir):
         opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=r / 384,
                                coalesce_max_entries=6, local_streams=2, **kw)
         attach_dp_routing(opt, named, replicate_group=dist.group.WORLD)
+        # one Q0 for both backends: the device stream (HIP) and the CPU stream (oracle) of
+        # the seeded Q init differ (state.py init_q), the runs must start from the same Q
+        if backend == "hip":
+            q0 = {n: opt.state[p]["Q"].detach().cpu().clone() for n, p in named}
+        else:
+            for n, p in named:
+                opt.state[p]["Q"].copy_(q0[n])
         name_of = {id(p): n for n, p in named}
         cur = {"s": 0}
 

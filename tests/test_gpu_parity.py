@@ -301,6 +301,22 @@ def test_pass_b_fixed_scale_from_pass_a_max():
             assert maxrel(R[b], Rref) <= 1e-6, (b, maxrel(R[b], Rref))
 
 
+def test_device_q_init_stream_is_shard_consistent():
+    """dion/state.py:97-108's device stream (per-row Philox offsets): a shard's rows are the
+    full draw's rows (the property FS restores rely on), draws repeat, fp32 and bf16."""
+    from megatron_dion_amd.state import init_q
+
+    dev = _dev()
+    for shape, dtype in (((4096, 64), torch.float32), ((1000, 30), torch.float32), ((333, 16), torch.bfloat16)):
+        full = init_q(shape, 1234, dev, dtype=dtype)
+        assert full.device.type == "cuda" and full.dtype == dtype and tuple(full.shape) == shape
+        assert torch.equal(full, init_q(shape, 1234, dev, dtype=dtype))
+        a, b = shape[0] // 3, shape[0] // 3 + shape[0] // 2
+        assert torch.equal(init_q(shape, 1234, dev, dtype=dtype, rows=(a, b)), full[a:b])
+        assert abs(full.float().mean().item()) < 0.05 and abs(full.float().std().item() - 1.0) < 0.05
+        assert not torch.equal(full, init_q(shape, 1235, dev, dtype=dtype))
+
+
 def test_fixup_known_answer_on_device():
     """tests/unit_tests/optimizer/test_dion_optimizer_contracts.py:1314-1357 through the HIP fix-up."""
     from megatron_dion_amd.codec import HipDionCodec
