@@ -29,6 +29,7 @@ from .batches import build_dion_batches
 from .runtime import (AsyncRuntime, DionStateMap, coalesce_local_batches, coalesce_replicated_batches,
                       drop_pending_error_feedback, flush_pending_error_feedback, is_replicated,
                       run_dion_batch_async)
+from .split import child_uid, gather_rows, make_commit, split_plan, state_key
 from .state import init_dion_state
 from .types import DionDistMeta, DionMixedPrecisionConfig, DionStepParam, ElementwiseStepParam
 
@@ -438,6 +439,31 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
         mpc = optimizer._mixed_precision_config
         spec = (fs_shards or {}).get(name)
         fs_world = int(dist.get_world_size(fs_group)) if (spec is not None and fs_group is not None) else 1
+        plan = split_plan(p, optimizer.defaults)
+        if plan is not None:
+            if spec is not None:
+                raise RuntimeError(f"[DION_SPLIT_SHARDED_PARENT] {name}: split children of FS/TP shards are not built")
+            family, kinds, segs, flags = plan
+            pstate = optimizer.state[p]
+            pstate.update(flags)
+            pstate["momentum"] = torch.zeros_like(p, dtype=_as_dtype(getattr(mpc, "momentum_dtype", None)) or p.dtype)
+            for kind in kinds:
+                rows = sum(b - a for a, b in segs[kind])
+                cname = f"{name}::{kind}"
+                cstate, ccfg = init_dion_state(p.narrow(0, 0, rows), rank_fraction=rf, rank_multiple_of=mult,
+                                               base_seed=base_seed, param_uid=child_uid((name,), family, kind),
+                                               param_name=cname,
+                                               q_dtype=_as_dtype(getattr(mpc, "q_dtype", None)),
+                                               use_low_rank_sync=optimizer.use_low_rank_sync, with_momentum=False)
+                for field in ("Q", "r", "local_shape", "global_shape"):
+                    pstate[state_key(family, field, kind)] = cstate[field]
+                cmeta = DionDistMeta(shape=(rows, int(p.shape[1])), global_shape=tuple(cstate["global_shape"]),
+                                     rank_fraction=rf, is_transposed=ccfg.is_transposed,
+                                     param_uid=child_uid((name,), family, kind), is_dion_param=True,
+                                     param_name=cname, param_config=ccfg, local_shape=(rows, int(p.shape[1])))
+                metas[(name, kind)] = (ccfg, cmeta)
+            metas[name] = (None, plan)
+            continue
         state, cfg = init_dion_state(p, rank_fraction=rf, rank_multiple_of=mult, base_seed=base_seed,
                                      param_uid=(name,), param_name=name,
                                      momentum_dtype=_as_dtype(getattr(mpc, "momentum_dtype", None)),
@@ -466,6 +492,20 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
             if g is None:
                 continue
             cfg, meta = metas[name]
+            if cfg is None:  # a split parent: one step param per child (split.py)
+                family, kinds, segs, _ = meta
+                pstate = optimizer.state[p]
+                M = dict.__getitem__(pstate, "momentum")
+                for kind in kinds:
+                    ccfg, cmeta = metas[(name, kind)]
+                    cstate = {"momentum": gather_rows(M, segs[kind])}
+                    for field in ("Q", "r", "local_shape", "global_shape"):
+                        cstate[field] = pstate[state_key(family, field, kind)]
+                    steps.append(DionStepParam(param=gather_rows(p.data, segs[kind]), grad=gather_rows(g, segs[kind]),
+                                               optimizer_state=cstate, optim_group=group_of.get(id(p), group),
+                                               config=ccfg, dist_meta=cmeta,
+                                               commit_update=make_commit(p, M, segs[kind])))
+                continue
             steps.append(DionStepParam(param=p, grad=g, optimizer_state=optimizer.state[p],
                                        optim_group=group_of.get(id(p), group), config=cfg, dist_meta=meta))
         batches = build_dion_batches(

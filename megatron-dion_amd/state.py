@@ -89,7 +89,8 @@ def init_q(q_global_shape: Tuple[int, int], seed: int, device, dtype=torch.float
 def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_of: int = 1,
                     base_seed: int = 0, param_uid=None, param_name: str = "",
                     momentum_dtype: Optional[torch.dtype] = None, q_dtype: Optional[torch.dtype] = None,
-                    use_low_rank_sync: bool = True, fs_shard=None) -> Tuple[dict, DionParamConfig]:
+                    use_low_rank_sync: bool = True, fs_shard=None,
+                    with_momentum: bool = True) -> Tuple[dict, DionParamConfig]:
     """Fresh optimizer state + config for one 2D parameter (no TP sharding).
 
     `param` is the whole matrix, or with `fs_shard = (global_shape, fs_shard_dim, start, end,
@@ -122,12 +123,13 @@ def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_
     q = init_q(q_shape, seed, param.device, dtype=q_dtype or param.dtype,
                rows=None if fs_shard is None else (start, end))
     state = {
-        "momentum": torch.zeros_like(param, dtype=momentum_dtype or param.dtype),
         "Q": q,
         "r": r,
         "local_shape": (ml, nl),
         "global_shape": (m, n),
     }
+    if with_momentum:  # split children (split.py) read their rows of the parent's momentum
+        state = {"momentum": torch.zeros_like(param, dtype=momentum_dtype or param.dtype), **state}
     cfg = DionParamConfig(
         is_transposed=transposed,
         use_low_rank_sync=bool(use_low_rank_sync) and should_use_low_rank_sync(

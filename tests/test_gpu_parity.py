@@ -536,3 +536,55 @@ def test_pipelined_two_stream_schedule_is_bit_identical(deferred):
         for i, (a, b) in enumerate(zip(got, ref)):
             for k in range(3):
                 assert torch.equal(a[k], b[k]), (la, i, k)
+
+
+# ---------------------------------------------------------------------------------------------- split children
+def test_split_qkv_and_linear_children_on_device():
+    """split_qkv / split_linear children (split.py) through the HIP codec equal
+    the same split run through the CPU oracle codec (same Q0, same explicit sketches)."""
+    from megatron_dion_amd.split import state_key
+    from oracle.cpu_codec import OracleCodec
+
+    dev = _dev()
+    split, lin, cols = (64, 32, 32), (256, 256), 192
+
+    def build(on, codec):
+        g = torch.Generator().manual_seed(5)
+        qkv = torch.nn.Parameter((torch.randn(4 * sum(split), cols, generator=g) * 0.02).to(on))
+        qkv.is_qkv, qkv.qkv_split_shapes = True, split
+        fc1 = torch.nn.Parameter((torch.randn(sum(lin), cols, generator=g) * 0.02).to(on))
+        fc1.is_linear_fc1, fc1.linear_split_rows = True, lin
+        named = [("qkv", qkv), ("fc1", fc1)]
+        kw = {} if codec is None else dict(codec=codec)
+        opt = mda.MegatronDion([p for _, p in named], lr=0.02, mu=0.95, weight_decay=0.01, rank_fraction=0.25,
+                               split_qkv=True, split_linear=True, **kw)
+        attach_dp_routing(opt, named)
+
+        def override(batch):
+            out = {}
+            for i, bp in enumerate(batch.params[:batch.real_batch_size]):
+                m, n = bp.shape
+                mp_ = max(m, n)
+                k = O.sketch_rows(int(batch.q_tensors[i].shape[1]))
+                out[i] = (torch.randn(k, mp_, generator=torch.Generator().manual_seed(mp_ + 7 * i)) / k ** 0.5).to(on)
+            return out
+
+        opt._sketch_override = override
+        return opt, named
+
+    hip, hn = build(dev, None)
+    ora, on_ = build(torch.device("cpu"), OracleCodec())
+    for (fam, kinds, pn) in (("qkv", "qkv", 0), ("linear", ("gate", "up"), 1)):
+        for kind in kinds:
+            ora.state[on_[pn][1]][state_key(fam, "Q", kind)].copy_(hip.state[hn[pn][1]][state_key(fam, "Q", kind)].cpu())
+    for step in range(2):
+        g = torch.Generator().manual_seed(50 + step)
+        for (_, ph), (_, po) in zip(hn, on_):
+            gr = (torch.randn(ph.shape, generator=g) * 1e-3).to(torch.bfloat16)
+            ph.main_grad, po.main_grad = gr.to(dev), gr.float()
+        hip.step()
+        ora.step()
+        torch.cuda.synchronize()
+        for (n, ph), (_, po) in zip(hn, on_):
+            assert maxrel(ph, po) <= 1e-5, (step, n, maxrel(ph, po))
+            assert maxrel(hip.state[ph]["momentum"], ora.state[po]["momentum"]) <= 1e-5
