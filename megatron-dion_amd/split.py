@@ -7,11 +7,12 @@ and a fused SwiGLU linear_fc1 as two (gate, up) when `split_qkv` / `split_linear
     `qkv_split_shapes` = (q, k, v) rows per group; child `kind` is the concatenation of
     its block of every group (_child_segments, :237-280), its global shape
     (split[kind] * groups, cols) (:314-327);
+  * dion/qkvg.py: the gated-attention variant, groups of [q | gate | k | v] (four children);
   * dion/linear.py: rows [0, gate) are the gate child, [gate, gate + up) the up child
     (_direct_linear_rows, :140-155);
-  * child identities: name `parent::kind`, uid (*parent_uid, ("qkv_child" | "linear_child",
-    kind)) (qkv.py:104-127, linear.py:91-113), so each child has its own seeded Q, rank r
-    and low-rank rule from its own global shape;
+  * child identities: name `parent::kind`, uid (*parent_uid, ("qkv_child" | "qkvg_child" |
+    "linear_child", kind)) (qkv.py:104-127, qkvg.py:118-141, linear.py:91-113), so each
+    child has its own seeded Q, rank r and low-rank rule from its own global shape;
   * child state lives in the parent's state under `qkv_<kind>_<field>` /
     `linear_<kind>_<field>` (Q, r, local_shape, global_shape; qkv.py:98-101) beside
     `qkv_split_qkv` / `qkv_split_shapes` (`linear_split_linear` / `linear_split_rows`),
@@ -35,21 +36,31 @@ from typing import Callable, List, Sequence, Tuple
 import torch
 
 QKV_CHILD_KINDS = ("q", "k", "v")
+QKVG_CHILD_KINDS = ("q", "gate", "k", "v")
 LINEAR_CHILD_KINDS = ("gate", "up")
 
 
-def qkv_child_segments(rows: int, split_shapes: Sequence[int], kind: str) -> List[Tuple[int, int]]:
-    """Parent row ranges, in child-row order, of child `kind` (qkv.py:237-280 for the parent
-    range [0, rows))."""
+def grouped_child_segments(rows: int, split_shapes: Sequence[int], kind: str,
+                           kinds: Sequence[str] = QKV_CHILD_KINDS, tag: str = "QKV") -> List[Tuple[int, int]]:
+    """Parent row ranges, in child-row order, of child `kind` of a grouped fused weight
+    (qkv.py:237-280 / qkvg.py:267-300 for the parent range [0, rows))."""
     split = tuple(int(d) for d in split_shapes)
-    if len(split) != 3 or any(d <= 0 for d in split):
-        raise RuntimeError(f"[DION_INVALID_QKV_SPLIT_SHAPES] split_shapes={split}")
+    if len(split) != len(kinds) or any(d <= 0 for d in split):
+        raise RuntimeError(f"[DION_INVALID_{tag}_SPLIT_SHAPES] split_shapes={split}")
     total = sum(split)
     if rows <= 0 or rows % total:
-        raise RuntimeError(f"[DION_QKV_LOCAL_LAYOUT_MISMATCH] rows={rows} split_shapes={split}")
-    idx = QKV_CHILD_KINDS.index(kind)
+        raise RuntimeError(f"[DION_{tag}_LOCAL_LAYOUT_MISMATCH] rows={rows} split_shapes={split}")
+    idx = tuple(kinds).index(kind)
     off = sum(split[:idx])
     return [(g * total + off, g * total + off + split[idx]) for g in range(rows // total)]
+
+
+def qkv_child_segments(rows: int, split_shapes: Sequence[int], kind: str) -> List[Tuple[int, int]]:
+    return grouped_child_segments(rows, split_shapes, kind, QKV_CHILD_KINDS, "QKV")
+
+
+def qkvg_child_segments(rows: int, split_shapes: Sequence[int], kind: str) -> List[Tuple[int, int]]:
+    return grouped_child_segments(rows, split_shapes, kind, QKVG_CHILD_KINDS, "QKVG")
 
 
 def linear_child_segments(rows: int, split_rows: Sequence[int], kind: str) -> List[Tuple[int, int]]:
@@ -104,6 +115,11 @@ def state_key(family: str, field: str, kind: str) -> str:
 def split_plan(param: torch.Tensor, defaults: dict):
     """(family, kinds, segments_of(kind), parent state flags) when `param` is split, else None."""
     rows = int(param.shape[0])
+    # dion_distrib_optimizer.py:2020-2060: split_qkv covers QKVG (gated attention) first
+    if defaults.get("split_qkv") and (getattr(param, "is_qkvg", False) or hasattr(param, "qkvg_split_shapes")):
+        split = tuple(int(d) for d in getattr(param, "qkvg_split_shapes"))
+        seg = {k: qkvg_child_segments(rows, split, k) for k in QKVG_CHILD_KINDS}
+        return "qkvg", QKVG_CHILD_KINDS, seg, {"qkvg_split_qkvg": True, "qkvg_split_shapes": split}
     if defaults.get("split_qkv") and (getattr(param, "is_qkv", False) or hasattr(param, "qkv_split_shapes")):
         split = tuple(int(d) for d in getattr(param, "qkv_split_shapes"))
         seg = {k: qkv_child_segments(rows, split, k) for k in QKV_CHILD_KINDS}

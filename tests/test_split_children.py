@@ -12,7 +12,7 @@ import torch
 import megatron_dion_amd as mda
 from megatron_dion_amd.optimizer import attach_dp_routing
 from megatron_dion_amd.split import (child_uid, gather_rows, linear_child_segments, qkv_child_segments,
-                                     state_key)
+                                     qkvg_child_segments, state_key)
 from megatron_dion_amd.state import init_q, q_seed_from_param_key
 from tests._cpu_codec import OracleCodec
 
@@ -31,6 +31,7 @@ def test_qkv_segments_follow_the_grouped_layout():
     assert segs == [(8, 12), (24, 28), (40, 44), (56, 60)]
     assert qkv_child_segments(16, SPLIT, "q") == [(0, 8)]
     assert linear_child_segments(80, LIN, "up") == [(40, 80)]
+    assert qkvg_child_segments(2 * 20, (8, 4, 4, 4), "gate") == [(8, 12), (28, 32)]
     t = torch.arange(GROUPS * 16).float().view(-1, 1)
     assert gather_rows(t, segs).view(-1).tolist() == [8, 9, 10, 11, 24, 25, 26, 27, 40, 41, 42, 43, 56, 57, 58, 59]
     assert gather_rows(t, linear_child_segments(80, LIN, "gate")).data_ptr() == t.data_ptr()  # a view
