@@ -169,7 +169,34 @@ def cpu_baseline():
             "config1_gpt125m_2rank_gloo": c1, "llama_layer": c3}
 
 
-def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps, deferred, step_bpe=None):
+# MFMA work each kernel issues, in flops per gradient element per unit of rank r (2 r per
+# real product, times the split products): fp16x3 (h3) = 3, bf16x6 = 6, fp32 MFMA = 1.
+# Pass A carries two rank-r products (P = X Q, and the deferred EF P' R'^T); the
+# rank_stream update one (W -= s P Q^T, or the eager EF).  (family, flops / (elem r), peak)
+MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense BF16/FP16, MI355X_MICROARCH.md
+MFMA_F32_PEAK_TFLOPS = 157.3
+MFMA_WORK = (("rowproj_efh3_kernel", 2 * 2 * 3, MFMA_BF16_PEAK_TFLOPS),
+             ("rowproj_ef_kernel", 2 * 2 * 6, MFMA_BF16_PEAK_TFLOPS),
+             ("colproj_ef_kernel", 2 * 2 * 6, MFMA_BF16_PEAK_TFLOPS),
+             ("colproj_h3_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),
+             ("colproj_x6_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
+             ("rowproj_x6_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
+             ("rank_stream_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
+             ("rowproj_fast_kernel", 2, MFMA_F32_PEAK_TFLOPS),
+             ("colproj_fast_kernel", 2, MFMA_F32_PEAK_TFLOPS))
+
+
+def mfma_of(kernel, elems, r, ms):
+    """Issued MFMA TFLOP/s of one kernel over its probe time and the fraction of the dtype's
+    dense peak (the split products count as issued work: that is what the matrix cores do)."""
+    for fam, per, peak in MFMA_WORK:
+        if kernel.startswith(fam):
+            tf = per * elems * r / (ms * 1e-3) / 1e12
+            return {"issued_TFLOPs": round(tf, 1), "peak_TFLOPs": peak, "util": round(tf / peak, 4)}
+    return None
+
+
+def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps, deferred, step_bpe=None, r=64):
     """`roofline` of the dominant kernel (most probe time) + every kernel's rate + the step-level view."""
     dominant = max(per_kernel, key=lambda k: per_kernel[k]["ms"])
     d = per_kernel[dominant]
@@ -185,8 +212,10 @@ def kernel_roofline(per_kernel, elems, ms_per_step, probe_steps, deferred, step_
                 "traffic": None if traffic is None else round(traffic),
                 "kernel": dominant, "bytes_per_launch": round(bytes_per_launch),
                 "avg_launch_ms": round(avg_launch_ms, 4), "probe_steps": probe_steps,
+                "mfma": mfma_of(dominant, d["elems"], r, d["ms"]),
                 "kernels": {k: {"avg_launch_ms": round(v["ms"] / v["launches"], 4),
-                                "GB/s": round(v["bytes"] / v["launches"] / (v["ms"] / v["launches"] * 1e-3) / 1e9, 1)}
+                                "GB/s": round(v["bytes"] / v["launches"] / (v["ms"] / v["launches"] * 1e-3) / 1e9, 1),
+                                "mfma": mfma_of(k, v["elems"], r, v["ms"])}
                             for k, v in per_kernel.items()},
                 "step": {"algorithmic_bytes": step_bytes,
                          "achieved": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
@@ -344,7 +373,7 @@ def main():
                            mixed_precision_config=mpc, **kw)
     if args.simulate_world > 1:
         group = install_loopback(args.simulate_world)
-    attach_dp_routing(opt, named, replicate_group=group)
+    attach_dp_routing(opt, named, replicate_group=group, q_stream="cpu")
     assert all(opt.state[p]["r"] == rank_r for _, p in named), "rank rule gave another r"
     deferred = bool(opt._defer_ef) and codec.supports_deferred_ef(*shapes[0][1:], rank_r, shapes[0][1] < shapes[0][2])
     elems = sum(m * n for _, m, n in shapes)
@@ -387,14 +416,15 @@ def main():
         if key not in knames:
             continue
         kname, launches_per_call = knames[key]
-        agg = per_kernel.setdefault(kname, {"ms": 0.0, "bytes": 0.0, "launches": 0})
+        agg = per_kernel.setdefault(kname, {"ms": 0.0, "bytes": 0.0, "launches": 0, "elems": 0.0})
         agg["ms"] += v["total_ms"]
         agg["bytes"] += BYTES_PER_ELEM[key[0]] * v["elems"]
+        agg["elems"] += v["elems"] * launches_per_call
         agg["launches"] += v["calls"] * launches_per_call
     roofline = None
     if per_kernel:
         roofline = kernel_roofline(per_kernel, elems, ms_per_step, args.probe_steps, deferred,
-                                   step_bpe=20.0 if bf16_state else None)
+                                   step_bpe=20.0 if bf16_state else None, r=rank_r)
 
     wl = args.workload if (args.layers or default_layers) == default_layers else \
         f"{args.workload} ({args.layers} layers, debug)"

@@ -406,8 +406,14 @@ def is_dion_param(param: torch.Tensor, name: str = "") -> bool:
 
 def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str, torch.Tensor]],
                       replicate_group=None, base_seed: int = 0, dion_predicate=None, fs_group=None,
-                      fs_shards: Optional[Dict[str, tuple]] = None) -> Dict[str, torch.Tensor]:
+                      fs_shards: Optional[Dict[str, tuple]] = None,
+                      q_stream: str = "device") -> Dict[str, torch.Tensor]:
     """Stand-alone adapter: state init + `route_step_params` for plain data parallelism.
+
+    `q_stream`: "device" draws each Q0 on the parameter's device exactly as the reference
+    does there (per-row Philox offsets, state.init_q: two small launches per Q row); "cpu"
+    draws the reference's CPU stream and copies it over (the values a CPU run gets; the
+    benchmark uses it to keep its startup and profiler traces free of ~10^5 init launches).
 
     Plays the part of the reference's DionDistributedOptimizer routing
     (distrib_dion/bootstrap.py:519-606 -> batches.py:971 build_dion_batches) for
@@ -454,7 +460,8 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
                                                base_seed=base_seed, param_uid=child_uid((name,), family, kind),
                                                param_name=cname,
                                                q_dtype=_as_dtype(getattr(mpc, "q_dtype", None)),
-                                               use_low_rank_sync=optimizer.use_low_rank_sync, with_momentum=False)
+                                               use_low_rank_sync=optimizer.use_low_rank_sync, with_momentum=False,
+                                               q_stream=q_stream)
                 for field in ("Q", "r", "local_shape", "global_shape"):
                     pstate[state_key(family, field, kind)] = cstate[field]
                 cmeta = DionDistMeta(shape=(rows, int(p.shape[1])), global_shape=tuple(cstate["global_shape"]),
@@ -470,7 +477,7 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
                                      q_dtype=_as_dtype(getattr(mpc, "q_dtype", None)),
                                      use_low_rank_sync=optimizer.use_low_rank_sync,
                                      fs_shard=None if spec is None else (tuple(spec[0]), spec[1], spec[2], spec[3],
-                                                                         fs_world))
+                                                                         fs_world), q_stream=q_stream)
         optimizer.state[p].update(state)
         meta = DionDistMeta(shape=tuple(p.shape), global_shape=tuple(state["global_shape"]), rank_fraction=rf,
                             is_transposed=cfg.is_transposed, param_uid=(name,), is_dion_param=True,

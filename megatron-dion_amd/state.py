@@ -90,7 +90,7 @@ def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_
                     base_seed: int = 0, param_uid=None, param_name: str = "",
                     momentum_dtype: Optional[torch.dtype] = None, q_dtype: Optional[torch.dtype] = None,
                     use_low_rank_sync: bool = True, fs_shard=None,
-                    with_momentum: bool = True) -> Tuple[dict, DionParamConfig]:
+                    with_momentum: bool = True, q_stream: str = "device") -> Tuple[dict, DionParamConfig]:
     """Fresh optimizer state + config for one 2D parameter (no TP sharding).
 
     `param` is the whole matrix, or with `fs_shard = (global_shape, fs_shard_dim, start, end,
@@ -120,8 +120,10 @@ def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_
     q_shape = (m if transposed else n, r)
     seed = q_seed_from_param_key(base_seed=base_seed, param_uid=param_uid, param_name=param_name,
                                  q_global_shape=q_shape, is_transposed=transposed)
-    q = init_q(q_shape, seed, param.device, dtype=q_dtype or param.dtype,
-               rows=None if fs_shard is None else (start, end))
+    if q_stream not in ("device", "cpu"):
+        raise RuntimeError(f"[DION_INVALID_Q_STREAM] q_stream={q_stream!r}")
+    q = init_q(q_shape, seed, param.device if q_stream == "device" else "cpu", dtype=q_dtype or param.dtype,
+               rows=None if fs_shard is None else (start, end)).to(param.device)
     state = {
         "Q": q,
         "r": r,
