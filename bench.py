@@ -76,11 +76,11 @@ WORKLOADS = {
 KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("project_p", True): ("colproj_fast_kernel<4, 2>", 1),
              ("project_p_ef", False): ("rowproj_efh3_kernel<4, 2, 2>", 1),
-             ("project_p_ef", True): ("colproj_ef_kernel<4, 2>", 1),
+             ("project_p_ef", True): ("colproj_efh3_kernel<4, 2>", 1),
              ("ef_apply_w", False): ("rank_stream_kernel<4, false, 8, 2>", 1),
              ("ef_apply_w", True): ("rank_stream_kernel<4, false, 8, 2>", 1),
              ("project_r", False): ("colproj_h3_kernel<4, 4, 4>", 1),
-             ("project_r", True): ("rowproj_x6_kernel<4>", 1),
+             ("project_r", True): ("rowproj_h3_kernel<4>", 1),
              ("ef_apply", False): ("rank_stream_kernel<4, false, 8, 2>", 2),
              ("ef_apply", True): ("rank_stream_kernel<4, false, 8, 2>", 2)}
 
@@ -177,7 +177,9 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense BF16/FP16, MI355X_MICROARCH.md
 MFMA_F32_PEAK_TFLOPS = 157.3
 MFMA_WORK = (("rowproj_efh3_kernel", 2 * 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("rowproj_ef_kernel", 2 * 2 * 6, MFMA_BF16_PEAK_TFLOPS),
+             ("colproj_efh3_kernel", 2 * 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_ef_kernel", 2 * 2 * 6, MFMA_BF16_PEAK_TFLOPS),
+             ("rowproj_h3_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_h3_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_x6_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
              ("rowproj_x6_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),

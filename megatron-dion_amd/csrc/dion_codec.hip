@@ -4,7 +4,7 @@
 // /root/reference/megatron/core/optimizer/):
 //   rowproj_kernel / colproj_kernel  dion/runtime.py:1560-1616 (M += G, P = M Q),
 //                                     dion/runtime.py:1476-1477 (R = M^T P)
-//   sketch/gram colproj (panel mode), householder_qr_kernel, cholesky_kernel,
+//   sketch/gram colproj (panel mode), householder_qr_kernel,
 //   trsm_kernel                       dion/ortho.py:71-123 (randomised Cholesky QR)
 //   fixup_colnorm_kernel, pfix_kernel dion/kernels.py:157-210, 279-290
 //   ef_update_kernel                  dion/kernels.py:54-154, 229-276;
@@ -154,6 +154,7 @@ struct ProjArgs {
   uint32_t* nonzero;       // per-matrix nonzero flags (pass A) or null
   const float* sketch;     // explicit sketch (batch, k, m_P) or null
   uint64_t seed;
+  long sketch_row0;        // generated sketch: global index of P's first row (row-sharded P)
   float sketch_std;
   int rows, cols, r;       // X is rows x cols; thin is (rows or cols) x r
   long ld_m, ld_g;
@@ -335,7 +336,8 @@ __device__ __forceinline__ void load_col4(const ProjArgs& a, int b, float* __res
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int aa = col + e;
-      x[e] = (aa < a.cols) ? a.sketch_std * gauss(a.seed + 0x632BE59BD9B4E019ull * (b + 1), aa, i) : 0.f;
+      x[e] = (aa < a.cols) ? a.sketch_std * gauss(a.seed + 0x632BE59BD9B4E019ull * (b + 1), aa,
+                                                          static_cast<uint32_t>(i + a.sketch_row0)) : 0.f;
     }
     return;
   } else {
@@ -984,110 +986,6 @@ __global__ void __launch_bounds__(256) householder_qr_kernel(const float* __rest
     const int i = idx / r, c = idx - i * r;
     Q[idx] = As[c * ld + i];
   }
-}
-
-// ============================================================================
-// Upper Cholesky (LAPACK dpotf2 order: ajj = a_jj - u_j.u_j, u_jj = sqrt(ajj),
-// row j scaled by 1/u_jj) of one r x r Gram matrix per block.  A non-positive
-// or NaN pivot poisons the remaining diagonal with NaN (cholesky_ex does not
-// raise, ortho.py:112-115; the downstream nan_to_num fix-up handles it).
-// ============================================================================
-__global__ void __launch_bounds__(256) cholesky_kernel(const float* __restrict__ G_in,
-                                                       float* __restrict__ U_out, int r) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int b = blockIdx.x;
-  const int ld = r + 1;
-  float* U = sm;  // r x ld, row-major, upper triangle used
-  float* bc = U + r * ld;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const float* Gm = G_in + static_cast<long>(b) * r * r;
-  for (int idx = tid; idx < r * r; idx += nt) {
-    const int i = idx / r, c = idx - i * r;
-    U[i * ld + c] = Gm[idx];
-  }
-  __syncthreads();
-  int jf = r;  // first failed pivot (r = none)
-  int tpc = 64;
-  while (tpc > 1 && tpc * r > 2 * nt) tpc >>= 1;
-  const int lane = tid & 63;
-  for (int j = 0; j < r; ++j) {
-    if (tid < 64) {  // wave 0: ajj = a_jj - sum_k u_kj^2 (fixed lane order)
-      float v = 0.f;
-      for (int k = lane; k < j; k += 64) v += U[k * ld + j] * U[k * ld + j];
-      v = wave_sum(v);
-      if (lane == 0) bc[0] = U[j * ld + j] - v;
-    }
-    __syncthreads();
-    const float ajj = bc[0];
-    if (!(ajj > 0.f)) {  // uniform across the block
-      jf = j;
-      break;
-    }
-    const float ujj = sqrtf(ajj);
-    const float inv = 1.f / ujj;
-    for (int c0 = j + 1; c0 < r; c0 += nt / tpc) {
-      const int c = c0 + tid / tpc;
-      const int p = tid % tpc;
-      float v = 0.f;
-      if (c < r)
-        for (int k = p; k < j; k += tpc) v += U[k * ld + j] * U[k * ld + c];
-      for (int off = tpc >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      if (c < r && p == 0) U[j * ld + c] = (U[j * ld + c] - v) * inv;
-    }
-    __syncthreads();
-    if (tid == 0) U[j * ld + j] = ujj;
-    __syncthreads();
-  }
-  float* O = U_out + static_cast<long>(b) * r * r;
-  for (int idx = tid; idx < r * r; idx += nt) {
-    const int i = idx / r, c = idx - i * r;
-    float v = 0.f;
-    if (i < jf) v = (i <= c) ? U[i * ld + c] : 0.f;
-    else if (i == c) v = __builtin_nanf("");
-    O[idx] = v;
-  }
-}
-
-// ============================================================================
-// Inverse of an upper-triangular r x r matrix, one block per matrix.  The
-// reference applies U^-1 by a triangular solve (solve_triangular, ortho.py:105-121);
-// here U^-1 is formed once in fp64 (row-oriented back substitution, one thread
-// per column) and rounded to fp32, so that P U^-1 becomes an MFMA row
-// projection instead of an m_P-long serial solve.  A zero or NaN pivot gives
-// inf/NaN entries exactly as the solve would.
-// ============================================================================
-template <typename XT>
-__global__ void __launch_bounds__(256) triinv_kernel(const float* __restrict__ U_in, float* __restrict__ X_out,
-                                                     int r) {
-  extern __shared__ __attribute__((aligned(16))) char tri_sm[];
-  float* U = reinterpret_cast<float*>(tri_sm);                  // r x r
-  XT* X = reinterpret_cast<XT*>(tri_sm + sizeof(float) * ((r * r + 3) / 4 * 4));  // r x r
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const float* Ub = U_in + static_cast<long>(b) * r * r;
-  for (int idx = tid; idx < r * r; idx += nt) {
-    U[idx] = Ub[idx];
-    X[idx] = XT(0);
-  }
-  __syncthreads();
-  int tpc = 64;
-  while (tpc > 1 && tpc * r > 2 * nt) tpc >>= 1;
-  for (int i = r - 1; i >= 0; --i) {
-    const double uii = static_cast<double>(U[i * r + i]);
-    for (int c0 = i; c0 < r; c0 += nt / tpc) {
-      const int c = c0 + tid / tpc;
-      const int p = tid % tpc;
-      double acc = 0.0;
-      if (c < r)
-        for (int k = i + 1 + p; k <= c; k += tpc)
-          acc += static_cast<double>(U[i * r + k]) * static_cast<double>(X[k * r + c]);
-      for (int off = tpc >> 1; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      if (c < r && p == 0) X[i * r + c] = static_cast<XT>(((c == i) ? 1.0 : 0.0) - acc) / static_cast<XT>(uii);
-    }
-    __syncthreads();
-  }
-  float* Xo = X_out + static_cast<long>(b) * r * r;
-  for (int idx = tid; idx < r * r; idx += nt) Xo[idx] = static_cast<float>(X[idx]);
 }
 
 // ============================================================================
@@ -3007,6 +2905,10 @@ __device__ __forceinline__ float h3_scale(float amax, float& inv) {
 }
 
 __device__ __forceinline__ void split2h(const f32x4& a, const f32x4& b, float s, Split2h& o) {
+  // x s is rounded to fp32 ONCE and both limbs come from that value: with contraction the
+  // compiler fuses x s - hi into one mixed-precision FMA on the exact product, and where
+  // the rounded product is an fp16 tie, hi and lo then disagree by an ulp of hi
+#pragma clang fp contract(off)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float x = (j < 4 ? a[j] : b[j - 4]) * s;
@@ -3321,8 +3223,8 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
   const float invQ = e.inv[b];
   const float invR = e.inv[nb + b];
   float invF;
-  const float sF = h3_scale(fabsf(e.alpha) * __uint_as_float(e.amax[2 * nb + b]), invF);
-  const float efinv = invF * invR;
+  const float sF = h3_scale(__uint_as_float(e.amax[2 * nb + b]), invF);  // power of two: P' s is exact
+  const float efinv = e.alpha * invF * invR;
 
   Split2h F[kRBE][KK];
   if (has_ef) {
@@ -3331,8 +3233,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
         const float* src = e.efp[b] + static_cast<long>(row_base + 16 * rb + t) * R + 32 * kk + 8 * g;
-        split2h(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), e.alpha * sF,
-                F[rb][kk]);
+        split2h(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), sF, F[rb][kk]);
       }
   } else {
 #pragma unroll
@@ -3503,6 +3404,351 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
   }
 }
 
+// ---- pass A, transposed, h3 products: colproj_ef_kernel's geometry (block = 4 waves x
+// 32 columns, step = 32 rows; lane (t, g) holds columns 2t, 2t + 1 of rows 16 h + 4 g + q)
+// with rowproj_efh3_kernel's arithmetic.  The error feedback's fixed operand is P' of
+// the lane's two columns (per-matrix scale), the streamed one R' of the step's rows (the
+// A operand, as in the row kernel).  In the projection each column of the step is the B
+// operand (its 8 rows are the k-run, KMAP 1) with its own per-step scale (max over the
+// four lanes (t, g = 0..3)), Q the A operand: D[16 cb + 4 g + q][col 2t + c] is added as
+// acc += D / s_col.  The matrix's max |M| goes into the flag for a fixed-scale pass B.
+template <int RB, int GDT>
+__global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_efh3_kernel(const EfProjArgs e) {
+  constexpr int R = 16 * RB;
+  constexpr int KK = RB / 2;
+  constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;  // f16x8 units of one K-step's splits
+  __shared__ f16x8 tq[2][NQ];
+  __shared__ f16x8 rs[2][NR];
+  const ProjArgs& a = e.p;
+  const BlockXYZ blk = xcd_block_col();
+  const int b = blk.z;
+  const int nb = gridDim.z;
+  const int kc = blk.y;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int col_base = blk.x * 128 + wave * 32;
+  const int i_begin = kc * a.kchunk;
+  const int i_end = min(a.rows, i_begin + a.kchunk);
+  float* __restrict__ M = a.m[b] + static_cast<long>(4 * g) * a.ld_m + col_base + 2 * t;
+  const void* G = nullptr;
+  if constexpr (GDT == DION_DTYPE_BF16)
+    G = static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(4 * g) * a.ld_g + col_base + 2 * t;
+  else if constexpr (GDT == DION_DTYPE_F32)
+    G = static_cast<const float*>(a.g[b]) + static_cast<long>(4 * g) * a.ld_g + col_base + 2 * t;
+  const bool has_ef = e.efr[b] != nullptr;
+  const float invQ = e.inv[b];
+  const float invR = e.inv[nb + b];
+  float invF;
+  const float sF = h3_scale(__uint_as_float(e.amax[2 * nb + b]), invF);  // power of two: P' s is exact
+  const float efinv = e.alpha * invF * invR;
+
+  // fixed EF factor: P'[col_base + 2t + c][32 kk + 8 g ...] (B operand of tile c)
+  Split2h F[2][KK];
+  if (has_ef) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const float* src = e.efp[b] + static_cast<long>(col_base + 2 * t + c) * R + 32 * kk + 8 * g;
+        split2h(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), sF, F[c][kk]);
+      }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) F[c][kk] = Split2h{};
+  }
+
+  f32x4 acc[2][RB];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t nzb = 0;
+  float mx = 0.f;
+
+  auto compute = [&](ColStepE<GDT>& S, const f16x8* tqc, const f16x8* rsc, int i0) {
+    if (has_ef) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 ev[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          Split2h A;
+          A.hi = rsc[((h * KK + kk) * 2 + 0) * 64 + lane];
+          A.lo = rsc[((h * KK + kk) * 2 + 1) * 64 + lane];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) ev[c] = mfma3h(A, F[c][kk], ev[c]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          S.x[h][q][0] = fmaf(ev[0][q], efinv, S.x[h][q][0]);
+          S.x[h][q][1] = fmaf(ev[1][q], efinv, S.x[h][q][1]);
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (GDT == DION_DTYPE_BF16) {
+          S.x[h][q][0] += __uint_as_float(S.gb[h][q] << 16);
+          S.x[h][q][1] += __uint_as_float(S.gb[h][q] & 0xFFFF0000u);
+        } else if constexpr (GDT == DION_DTYPE_F32) {
+          S.x[h][q] += S.gf[h][q];
+        }
+        if (GDT != DION_DTYPE_NONE || has_ef)
+          st_stream(reinterpret_cast<f32x2*>(M + static_cast<long>(i0 + 16 * h + q) * a.ld_m), S.x[h][q]);
+        nzb |= __float_as_uint(S.x[h][q][0]) | __float_as_uint(S.x[h][q][1]);
+      }
+    Split2h Bx[2];
+    float invx[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const f32x4 lo4{S.x[0][0][c], S.x[0][1][c], S.x[0][2][c], S.x[0][3][c]};
+      const f32x4 hi4{S.x[1][0][c], S.x[1][1][c], S.x[1][2][c], S.x[1][3][c]};
+      float m8 = max8abs(lo4, hi4);
+      m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
+      m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
+      mx = fmaxf(mx, m8);
+      const float sx = h3_scale(m8, invx[c]);
+      split2h(lo4, hi4, sx, Bx[c]);
+    }
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      Split2h A;
+      A.hi = tqc[(cb * 2 + 0) * 64 + lane];
+      A.lo = tqc[(cb * 2 + 1) * 64 + lane];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const f32x4 d = mfma3h(A, Bx[c], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[c][cb][q] = fmaf(d[q], invx[c], acc[c][cb][q]);
+      }
+    }
+  };
+
+  const u32x4* qs = e.qsplit + b * e.split_stride;
+  const u32x4* rsp = e.rsplit + b * e.split_stride;
+  ColStepE<GDT> SA, SB;
+  SplitCopy<NQ> TA;
+  SplitCopy<NR> EA;
+  cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i_begin);
+  split_copy_load<NQ>(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
+  split_copy_store<NQ>(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
+  if (has_ef) {
+    split_copy_load<NR>(EA, rsp + static_cast<long>(i_begin / 32) * NR, tid);
+    split_copy_store<NR>(EA, reinterpret_cast<bf16x8*>(rs[0]), tid);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int i0 = i_begin; i0 < i_end; i0 += 64) {
+    const bool more = i0 + 32 < i_end;
+    if (more) {
+      cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
+      split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 1) * NQ, tid);
+      if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 1) * NR, tid);
+    }
+    compute(SA, tq[cur], rs[cur], i0);
+    if (!more) break;
+    split_copy_store<NQ>(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+    if (has_ef) split_copy_store<NR>(EA, reinterpret_cast<bf16x8*>(rs[cur ^ 1]), tid);
+    __syncthreads();
+    cur ^= 1;
+    const bool more2 = i0 + 64 < i_end;
+    if (more2) {
+      cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
+      split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 2) * NQ, tid);
+      if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 2) * NR, tid);
+    }
+    compute(SB, tq[cur], rs[cur], i0 + 32);
+    if (!more2) break;
+    split_copy_store<NQ>(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+    if (has_ef) split_copy_store<NR>(EA, reinterpret_cast<bf16x8*>(rs[cur ^ 1]), tid);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(col_base + 2 * t + c) * R + 16 * cb + 4 * g) =
+          acc[c][cb] * invQ;
+  if (a.nonzero != nullptr) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    const bool nz = __any((nzb & 0x7FFFFFFFu) != 0u);
+    const uint32_t mb = __float_as_uint(mx);
+    if (nz && lane == 0) atomicMax(&a.nonzero[b], mb > 1u ? mb : 1u);
+  }
+}
+
+// ---- pass B, transposed (R = M P), h3 products: rowproj_x6_kernel's geometry and whole-
+// line loads (lane (t, g) after the LDS transpose: row 16 rb + t, k-run KMAP 1 = columns
+// 16 c + 4 g .. + 3).  The streamed M is the B operand, the pre-split P the A operand
+// (one scale per matrix); with pass A's max |M| the step's products accumulate in place
+// under one scale for the matrix, else each row gets a per-step scale (as in pass A).
+template <int RB>
+__global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_h3_kernel(const ProjArgs a) {
+  constexpr int R = 16 * RB;
+  constexpr int NQ = RB * 2 * 64;
+  __shared__ f16x8 tq[2][NQ];
+  __shared__ f32x4 xt[4][32 * 8];
+  const BlockXYZ blk = xcd_block();
+  const int b = blk.z;
+  const int kc = blk.y;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int row_base = blk.x * (64 * kRBE) + wave * (16 * kRBE);
+  const int j_begin = kc * a.kchunk;
+  const int j_end = min(a.cols, j_begin + a.kchunk);
+  const int j_len = j_end - j_begin;
+  const int j_rot = walk_rotation(blk, j_len);
+  auto cj = [&](int j) { const int x = j - j_begin + j_rot; return j_begin + (x >= j_len ? x - j_len : x); };
+  const float* __restrict__ Mw = a.m[b] + static_cast<long>(row_base + (lane >> 3)) * a.ld_m + 4 * (lane & 7);
+  auto xload = [&](RowStepE<DION_DTYPE_NONE>& T, int j) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      T.x[q >> 1][q & 1] = ld_stream(reinterpret_cast<const f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j));
+  };
+  auto xpose = [&](RowStepE<DION_DTYPE_NONE>& T) {
+    f32x4* xw = xt[wave];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 8 * q + (lane >> 3), k = lane & 7;
+      xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[q >> 1][q & 1];
+    }
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int r = 16 * rb + t, k = 4 * c + g;
+        T.x[rb][c] = xw[r * 8 + (k ^ ((r >> 1) & 7))];
+      }
+  };
+
+  f32x4 acc[kRBE][RB];
+#pragma unroll
+  for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
+  const uint32_t mab = a.mabs != nullptr ? a.mabs[b] : kAbsUnknown;
+  float finv = 1.f;
+  const float fs = h3_scale(__uint_as_float(mab), finv);
+  auto run = [&](auto FIXc) {
+    constexpr bool FIX = decltype(FIXc)::value;
+    RowStepE<DION_DTYPE_NONE> SA, SB;
+    SplitCopy<NQ> TA;
+    auto compute = [&](RowStepE<DION_DTYPE_NONE>& X, const f16x8* tqc) {
+      Split2h Bx[kRBE];
+      float invx[kRBE];
+#pragma unroll
+      for (int rb = 0; rb < kRBE; ++rb) {
+        if constexpr (FIX) {
+          split2h(X.x[rb][0], X.x[rb][1], fs, Bx[rb]);
+        } else {
+          float m8 = max8abs(X.x[rb][0], X.x[rb][1]);
+          m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
+          m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
+          const float sx = h3_scale(m8, invx[rb]);
+          split2h(X.x[rb][0], X.x[rb][1], sx, Bx[rb]);
+        }
+      }
+      if constexpr (FIX) {
+        // the three products term by term: consecutive MFMAs are independent
+        Split2h A[RB];
+#pragma unroll
+        for (int cb = 0; cb < RB; ++cb) {
+          A[cb].hi = tqc[(cb * 2 + 0) * 64 + lane];
+          A[cb].lo = tqc[(cb * 2 + 1) * 64 + lane];
+        }
+#pragma unroll
+        for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < RB; ++cb)
+            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].lo, Bx[rb].hi, acc[rb][cb], 0, 0, 0);
+#pragma unroll
+        for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < RB; ++cb)
+            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].hi, Bx[rb].lo, acc[rb][cb], 0, 0, 0);
+#pragma unroll
+        for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < RB; ++cb)
+            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].hi, Bx[rb].hi, acc[rb][cb], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int cb = 0; cb < RB; ++cb) {
+          Split2h A;
+          A.hi = tqc[(cb * 2 + 0) * 64 + lane];
+          A.lo = tqc[(cb * 2 + 1) * 64 + lane];
+#pragma unroll
+          for (int rb = 0; rb < kRBE; ++rb) {
+            const f32x4 d = mfma3h(A, Bx[rb], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[rb][cb][q] = fmaf(d[q], invx[rb], acc[rb][cb][q]);
+          }
+        }
+      }
+    };
+    xload(SA, cj(j_begin));
+    split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j_begin) / 32) * NQ, tid);
+    split_copy_store<NQ>(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
+    __syncthreads();
+    int cur = 0;
+    for (int j0 = j_begin; j0 < j_end; j0 += 64) {
+      const bool more = j0 + 32 < j_end;
+      if (more) {
+        xload(SB, cj(j0 + 32));
+        split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j0 + 32) / 32) * NQ, tid);
+      }
+      xpose(SA);
+      compute(SA, tq[cur]);
+      if (!more) break;
+      split_copy_store<NQ>(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+      __syncthreads();
+      cur ^= 1;
+      const bool more2 = j0 + 64 < j_end;
+      if (more2) {
+        xload(SA, cj(j0 + 64));
+        split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j0 + 64) / 32) * NQ, tid);
+      }
+      xpose(SB);
+      compute(SB, tq[cur]);
+      if (!more2) break;
+      split_copy_store<NQ>(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+      __syncthreads();
+      cur ^= 1;
+    }
+  };
+  const bool fixed = mab < kAbsUnknown;
+  if (fixed)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
+
+  // lane (t, g): R row 16 rb + t, columns 16 cb + 4 g .. + 3
+  const float ps = a.tinv[b] * (fixed ? finv : 1.f);
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(row_base + 16 * rb + t) * R + 16 * cb + 4 * g) =
+          acc[rb][cb] * ps;
+}
+
 // ============================================================================
 // host side
 // ============================================================================
@@ -3527,6 +3773,16 @@ int validate(const DionBatchDesc* d) {
   if (d->w_dtype != DION_DTYPE_F32) return fail(DION_E_UNSUPPORTED, "weight dtype %d", d->w_dtype);
   if (d->g_dtype != DION_DTYPE_NONE && d->g_dtype != DION_DTYPE_F32 && d->g_dtype != DION_DTYPE_BF16)
     return fail(DION_E_UNSUPPORTED, "grad dtype %d", d->g_dtype);
+  if (d->transposed != 0 && d->transposed != 1) return fail(DION_E_INVALID, "transposed=%d", d->transposed);
+  return DION_OK;
+}
+
+// the distributed-RCQR pieces: P is a row shard (m_P local rows may be fewer than r)
+int validate_dortho(const DionBatchDesc* d) {
+  if (d == nullptr) return fail(DION_E_INVALID, "desc is null");
+  if (d->batch < 0) return fail(DION_E_INVALID, "batch=%d", d->batch);
+  if (d->m <= 0 || d->n <= 0) return fail(DION_E_INVALID, "bad shape m=%d n=%d", d->m, d->n);
+  if (d->r <= 0 || d->r > 128) return fail(DION_E_UNSUPPORTED, "rank r=%d outside 1..128", d->r);
   if (d->transposed != 0 && d->transposed != 1) return fail(DION_E_INVALID, "transposed=%d", d->transposed);
   return DION_OK;
 }
@@ -3614,9 +3870,17 @@ size_t thin_presplit_bytes(int rows, int r, int batch) { return static_cast<size
 #ifndef DION_PA_H3
 #define DION_PA_H3 1
 #endif
+// pass A, transposed, through the fp16x3 column kernel (colproj_efh3_kernel; tuning knob)
+#ifndef DION_PA_H3T
+#define DION_PA_H3T 1
+#endif
 // pass B through the fp16x3 column kernel (colproj_h3_kernel) instead of bf16x6 (tuning knob)
 #ifndef DION_PB_H3
 #define DION_PB_H3 1
+#endif
+// pass B, transposed, through the fp16x3 row kernel (rowproj_h3_kernel) instead of bf16x6 (tuning knob)
+#ifndef DION_PB_H3R
+#define DION_PB_H3R 1
 #endif
 // columns per lane of colproj_h3_kernel (2: 8-byte loads, 4: 16-byte loads; tuning knob)
 #ifndef DION_COLH3_CT
@@ -3650,8 +3914,8 @@ size_t presplit_bytes(int nq, int r, int batch) { return 2 * 16 * presplit_strid
 
 // deferred-EF pass A (rowproj_ef_kernel / colproj_ef_kernel)
 bool proj_ef_ok(int m, int n, int r, bool transposed) {
-  // r = 128 (the Mixtral config) only through the h3 row kernel
-  if (r != 32 && r != 64 && !(r == 128 && !transposed && DION_PA_H3)) return false;
+  // r = 128 (the Mixtral config) only through the h3 kernels
+  if (r != 32 && r != 64 && !(r == 128 && (transposed ? DION_PA_H3T : DION_PA_H3))) return false;
   return transposed ? (n % 128 == 0 && m % 32 == 0) : (m % (16 * kRBE * kPaNW) == 0 && n % 32 == 0);
 }
 
@@ -3781,8 +4045,9 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
   const bool x6 = fast && gdt == DION_DTYPE_NONE &&
                   (row_mode ? rows % (64 * kRBE) == 0
                             : (rows % 32 == 0 && cols % ((r >= 64 ? 32 : 64) * kColX6NW) == 0));
-  const bool h3 = fast && gdt == DION_DTYPE_NONE && !row_mode && colh3_ok(rows, cols, r);
-  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, x6 ? 64 * kRBE : (fast ? 64 * kRB : 128))
+  const bool h3 = fast && gdt == DION_DTYPE_NONE &&
+                  (row_mode ? (DION_PB_H3R && rows % (64 * kRBE) == 0) : colh3_ok(rows, cols, r));
+  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, (x6 || h3) ? 64 * kRBE : (fast ? 64 * kRB : 128))
                  : h3      ? colh3_geo(rows, cols, batch, r)
                  : x6      ? colx6_geo(rows, cols, batch, r)
                            : colproj_geo(rows, cols, batch, false);
@@ -3818,7 +4083,7 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     pa.stride = per / 8 * 2;
     pa.rows = thin_rows;
     pa.r = r;
-    pa.kmap = 0;
+    pa.kmap = row_mode ? 1 : 0;  // rowproj_h3 steps columns 16c + 4g (KMAP 1), colproj_h3 rows 8g + e
     pa.layout = 0;
     const dim3 pgrid(static_cast<unsigned>(ceil_div(per / 8, 256)), batch);
     hipLaunchKernelGGL(presplit16_kernel, pgrid, dim3(256), 0, st, pa);
@@ -3871,7 +4136,9 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     constexpr int RB = decltype(RBc)::value;
     return dispatch_gdt(gdt, [&](auto Gc) {
       constexpr int GD = decltype(Gc)::value;
-      if (x6 && row_mode)
+      if (h3 && row_mode)
+        hipLaunchKernelGGL((rowproj_h3_kernel<RB>), grid, dim3(256), 0, st, a);
+      else if (x6 && row_mode)
         hipLaunchKernelGGL((rowproj_x6_kernel<RB>), grid, dim3(256), 0, st, a);
       else if (h3)
         hipLaunchKernelGGL((colproj_h3_kernel<RB, kColX6NW, colh3_ct(16 * RB)>), grid, dim3(64 * kColX6NW), 0, st, a);
@@ -3896,9 +4163,10 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
 
 // panel reduction over the rows of P: out[b] (cols x r) = X_b^T P_b
 int run_panel(int xmode, int mp, int cols, int r, int batch, const float* P, const float* sketch, uint64_t seed,
-              float std_, float* out, void* slab, const Geo& geo, hipStream_t st) {
+              float std_, float* out, void* slab, const Geo& geo, hipStream_t st, long sketch_row0 = 0) {
   ProjArgs a;
   memset(&a, 0, sizeof(a));
+  a.sketch_row0 = sketch_row0;
   for (int b = 0; b < batch; ++b) {
     a.thin[b] = P + static_cast<long>(b) * mp * r;
     a.m[b] = const_cast<float*>(P + static_cast<long>(b) * mp * r);
@@ -3942,22 +4210,6 @@ int allow_lds(K kernel, size_t bytes) {
                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
   if (e != hipSuccess) return fail(DION_E_LAUNCH, "hipFuncSetAttribute(%zu): %s", bytes, hipGetErrorString(e));
   return DION_OK;
-}
-
-int launch_triinv(const float* U, float* Uinv, int r, int batch, hipStream_t st) {
-  const size_t ubytes = sizeof(float) * static_cast<size_t>((r * r + 3) / 4 * 4);
-  if (r <= 96) {
-    const size_t lds = ubytes + sizeof(double) * r * r;
-    int rc = allow_lds(triinv_kernel<double>, lds);
-    if (rc != DION_OK) return rc;
-    hipLaunchKernelGGL((triinv_kernel<double>), dim3(batch), dim3(256), lds, st, U, Uinv, r);
-  } else {
-    const size_t lds = ubytes + sizeof(float) * r * r;
-    int rc = allow_lds(triinv_kernel<float>, lds);
-    if (rc != DION_OK) return rc;
-    hipLaunchKernelGGL((triinv_kernel<float>), dim3(batch), dim3(256), lds, st, U, Uinv, r);
-  }
-  return check_launch("triinv");
 }
 
 int launch_sketch_qr_inv(const float* SP, float* Rinv, int K, int r, int batch, hipStream_t st) {
@@ -4062,6 +4314,23 @@ int dion_abi_version(void) { return DION_ABI_VERSION; }
 const char* dion_last_error(void) { return g_err; }
 
 int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
+  if (op == DION_OP_DORTHO) {
+    const int rcd = validate_dortho(d);
+    if (rcd != DION_OK) return rcd;
+    if (bytes == nullptr) return fail(DION_E_INVALID, "bytes is null");
+    const int mp = d->transposed ? d->n : d->m;
+    const int nb = d->batch < MAXB ? d->batch : MAXB;
+    const size_t a = slab_bytes(colproj_geo(mp, sketch_k(d->r, 2.0f), nb, true), nb, d->r);
+    const size_t g = slab_bytes(colproj_geo(mp, d->r, nb, true), nb, d->r);
+    size_t need = a > g ? a : g;
+    // the sketch slab grows with k; any oversample up to 2 fits (k <= 256 for r <= 128)
+    for (int k = 128; k <= 256; k += 128) {
+      const size_t x = slab_bytes(colproj_geo(mp, k, nb, true), nb, d->r);
+      need = x > need ? x : need;
+    }
+    *bytes = need;
+    return DION_OK;
+  }
   if (op == DION_OP_GRAD_SUM_SQ) {
     const int rcg = validate_grads(d);
     if (rcg != DION_OK) return rcg;
@@ -4213,7 +4482,7 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
     const size_t need = slab + presplit_bytes(nq, d->r, nb);
     if (need > ws_bytes || ws == nullptr)
       return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
-    const bool h3 = !tr && DION_PA_H3;
+    const bool h3 = tr ? DION_PA_H3T != 0 : DION_PA_H3 != 0;
     const long sstride = h3 ? static_cast<long>(nq) * d->r / 4 : static_cast<long>(presplit_stride(nq, d->r));
     u32x4* qsplit = reinterpret_cast<u32x4*>(static_cast<char*>(ws) + slab);
     u32x4* rsplit = qsplit + sstride * nb;
@@ -4313,10 +4582,15 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
       constexpr int RB = decltype(RBc)::value;
       return dispatch_gdt(d->g_dtype, [&](auto Gc) {
         constexpr int GD = decltype(Gc)::value;
-        if constexpr (RB == 8) {  // r = 128: the h3 row kernel only (proj_ef_ok)
-          hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, 1>), grid, dim3(64 * kPaNW), 0, st, e);
-        } else {
+        if constexpr (RB == 8) {  // r = 128: the h3 kernels only (proj_ef_ok)
           if (tr)
+            hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
+          else
+            hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, 1>), grid, dim3(64 * kPaNW), 0, st, e);
+        } else {
+          if (tr && h3)
+            hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
+          else if (tr)
             hipLaunchKernelGGL((colproj_ef_kernel<RB, GD>), grid, dim3(256), 0, st, e);
           else if (h3)
             hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, 2>), grid, dim3(64 * kPaNW), 0, st, e);
@@ -4440,6 +4714,100 @@ int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, u
   }
   // ortho.py:123: the fp32 result is cast back to P's dtype
   if (d->m_dtype == DION_DTYPE_BF16) return b16::round_buffer(P, static_cast<long>(d->batch) * mp * r, st);
+  return DION_OK;
+}
+
+// ---- distributed (row-sharded) randomised Cholesky QR: the per-rank pieces of
+// dion/ortho.py:682-834 distributed_orthogonalize, between the caller's collectives
+int dion_dortho_sketch(const DionBatchDesc* d, const float* P, const float* sketch, uint64_t seed,
+                       int64_t row_offset, float oversample, float* SP, void* ws, size_t ws_bytes,
+                       dion_stream_t stream) {
+  int rc = validate_dortho(d);
+  if (rc != DION_OK) return rc;
+  if (P == nullptr || SP == nullptr) return fail(DION_E_INVALID, "null argument");
+  if (!(oversample > 0.f)) return fail(DION_E_INVALID, "oversample=%f", oversample);
+  if (row_offset < 0) return fail(DION_E_INVALID, "row_offset=%lld", static_cast<long long>(row_offset));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int mp = d->transposed ? d->n : d->m;
+  const int r = d->r;
+  const int K = sketch_k(r, oversample);
+  const float std_ = sqrtf(1.0f / static_cast<float>(K));
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    const Geo geo = colproj_geo(mp, K, nb, true);
+    if (slab_bytes(geo, nb, r) > ws_bytes || (slab_bytes(geo, nb, r) > 0 && ws == nullptr))
+      return fail(DION_E_WORKSPACE, "sketch product needs %zu workspace bytes", slab_bytes(geo, nb, r));
+    rc = run_panel(sketch ? 1 : 2, mp, K, r, nb, P + static_cast<long>(b0) * mp * r,
+                   sketch ? sketch + static_cast<long>(b0) * K * mp : nullptr,
+                   seed + 0x9E3779B97F4A7C15ull * static_cast<uint64_t>(b0), std_,
+                   SP + static_cast<long>(b0) * K * r, ws, geo, st, static_cast<long>(row_offset));
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_dortho_qr_inv(int32_t k, int32_t r, int32_t batch, const float* SP, float* R1inv, dion_stream_t stream) {
+  if (SP == nullptr || R1inv == nullptr) return fail(DION_E_INVALID, "null argument");
+  if (batch < 0 || r <= 0 || r > 128 || k < r || k > 256) return fail(DION_E_UNSUPPORTED, "sketch QR %dx%d", k, r);
+  if (batch == 0) return DION_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int b0 = 0; b0 < batch; b0 += 65535) {
+    const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    int rc = launch_sketch_qr_inv(SP + static_cast<long>(b0) * k * r, R1inv + static_cast<long>(b0) * r * r, k, r,
+                                  nb, st);
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_dortho_gram(const DionBatchDesc* d, const float* P, float* gram, void* ws, size_t ws_bytes,
+                     dion_stream_t stream) {
+  int rc = validate_dortho(d);
+  if (rc != DION_OK) return rc;
+  if (P == nullptr || gram == nullptr) return fail(DION_E_INVALID, "null argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int mp = d->transposed ? d->n : d->m;
+  const int r = d->r;
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    const Geo geo = colproj_geo(mp, r, nb, true);
+    if (slab_bytes(geo, nb, r) > ws_bytes || (slab_bytes(geo, nb, r) > 0 && ws == nullptr))
+      return fail(DION_E_WORKSPACE, "Gram product needs %zu workspace bytes", slab_bytes(geo, nb, r));
+    rc = run_panel(0, mp, r, r, nb, P + static_cast<long>(b0) * mp * r, nullptr, 0, 0.f,
+                   gram + static_cast<long>(b0) * r * r, ws, geo, st);
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_dortho_chol_inv(int32_t r, int32_t batch, const float* gram, float* R2inv, dion_stream_t stream) {
+  if (gram == nullptr || R2inv == nullptr) return fail(DION_E_INVALID, "null argument");
+  if (batch < 0 || r <= 0 || r > 128) return fail(DION_E_UNSUPPORTED, "Cholesky of %dx%d", r, r);
+  if (batch == 0) return DION_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int b0 = 0; b0 < batch; b0 += 65535) {
+    const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    int rc = launch_chol_inv(gram + static_cast<long>(b0) * r * r, R2inv + static_cast<long>(b0) * r * r, r, nb, st);
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_dortho_apply(const DionBatchDesc* d, const float* P_in, const float* Uinv, float* P_out,
+                      dion_stream_t stream) {
+  int rc = validate_dortho(d);
+  if (rc != DION_OK) return rc;
+  if (P_in == nullptr || Uinv == nullptr || P_out == nullptr) return fail(DION_E_INVALID, "null argument");
+  if (P_in == P_out) return fail(DION_E_INVALID, "P_in and P_out must not alias");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int mp = d->transposed ? d->n : d->m;
+  const int r = d->r;
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    rc = apply_right(P_in + static_cast<long>(b0) * mp * r, P_out + static_cast<long>(b0) * mp * r,
+                     Uinv + static_cast<long>(b0) * r * r, mp, r, nb, st);
+    if (rc != DION_OK) return rc;
+  }
   return DION_OK;
 }
 

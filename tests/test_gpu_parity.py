@@ -255,40 +255,45 @@ def test_project_kernels_against_fp64():
         assert all(v != 0 for v in nz.tolist())
 
 
-def test_pass_b_fixed_scale_from_pass_a_max():
-    """Pass A (the fused deferred-EF row kernel) leaves max |M_b| in its nonzero flag;
-    pass B given those flags runs the fp16x3 column kernel on one scale per matrix.
+@pytest.mark.parametrize("transposed,r", [(False, 64), (True, 64), (True, 128)])
+def test_pass_b_fixed_scale_from_pass_a_max(transposed, r):
+    """Pass A (the fused deferred-EF kernels, row or column) leaves max |M_b| in its nonzero
+    flag; pass B given those flags runs the fp16x3 kernel (column kernel not transposed, row
+    kernel transposed) on one scale per matrix.
     Element error of the fixed scale: <= 2^-22 |x| + 2^-39 max|M| (two fp16 limbs of x s,
-    s = 2^(14 - e(max|M|))), so with columns spanning 12 decades every row of R (= column
-    of M) of magnitude >= 1e-6 max stays within 1e-5 of its own size, and the matrix-level
-    error (SURVEY 8(c)'s max|a - b| / max|b|) within 1e-6.  An all-zero matrix must report
-    0 and come out as R = 0."""
+    s = 2^(14 - e(max|M|))), so with the contraction-side slices of M spanning 12 decades
+    every row of R of magnitude >= 1e-6 max stays within 1e-5 of its own size, and the
+    matrix-level error (SURVEY 8(c)'s max|a - b| / max|b|) within 1e-6.  An all-zero matrix
+    must report 0 and come out as R = 0."""
     from megatron_dion_amd.codec import HipDionCodec
 
     dev = _dev()
     codec = HipDionCodec(dev)
-    m, n, r = 2048, 1024, 64
-    assert codec.supports_deferred_ef(m, n, r, False)
+    m, n = (1024, 2048) if transposed else (2048, 1024)
+    mp, nq = (n, m) if transposed else (m, n)
+    assert codec.supports_deferred_ef(m, n, r, transposed)
     g = torch.Generator().manual_seed(17)
-    colscale = torch.logspace(-12, 0, n, dtype=torch.float64).float()
-    Ms = [(torch.randn(m, n, generator=g) * colscale).to(dev), torch.zeros(m, n, device=dev),
+    scale = torch.logspace(-12, 0, nq, dtype=torch.float64).float()
+    scale = scale[:, None] if transposed else scale[None, :]   # R's rows: rows (T) or columns of M
+    Ms = [(torch.randn(m, n, generator=g) * scale).to(dev), torch.zeros(m, n, device=dev),
           (torch.randn(m, n, generator=g) * 3e4).to(dev)]
     Gs = [torch.zeros(m, n, dtype=torch.bfloat16, device=dev) for _ in Ms]
     Gs[2] = (torch.randn(m, n, generator=g) * 1e-3).to(torch.bfloat16).to(dev)
-    Qs = [torch.randn(n, r, generator=g).to(dev) for _ in Ms]
-    P = torch.zeros(len(Ms), m, r, device=dev)
+    Qs = [torch.randn(nq, r, generator=g).to(dev) for _ in Ms]
+    P = torch.zeros(len(Ms), mp, r, device=dev)
     nz = torch.zeros(len(Ms), dtype=torch.int32, device=dev)
-    codec.project_p_ef(Gs, Ms, Qs, P, nz, False, [None] * len(Ms), [None] * len(Ms), -0.05)
-    R_fix = torch.zeros(len(Ms), n, r, device=dev)
-    R_step = torch.zeros(len(Ms), n, r, device=dev)
-    codec.project_r(Ms, P, R_fix, False, nonzero=nz)
-    codec.project_r(Ms, P, R_step, False)
+    codec.project_p_ef(Gs, Ms, Qs, P, nz, transposed, [None] * len(Ms), [None] * len(Ms), -0.05)
+    R_fix = torch.zeros(len(Ms), nq, r, device=dev)
+    R_step = torch.zeros(len(Ms), nq, r, device=dev)
+    codec.project_r(Ms, P, R_fix, transposed, nonzero=nz)
+    codec.project_r(Ms, P, R_step, transposed)
     torch.cuda.synchronize()
     flags = nz.cpu().view(torch.float32)
     for b, M in enumerate(Ms):
         amax = M.abs().max().item()
         assert flags[b].item() == amax, (b, flags[b].item(), amax)  # exact: a max of fp32 values
-        Rref = M.double().t() @ P[b].double()
+        Xo = M.double().t() if transposed else M.double()
+        Rref = Xo.t() @ P[b].double()
         if amax == 0:
             assert torch.count_nonzero(R_fix[b]).item() == 0
             continue
@@ -392,7 +397,8 @@ def test_llama_shape_properties(m, n):
 
 # ---------------------------------------------------------------------------------------------- deferred EF
 @pytest.mark.parametrize("m,n,r,gdt", [(512, 384, 64, torch.bfloat16), (384, 1024, 64, torch.bfloat16),
-                                       (1024, 512, 32, torch.float32), (256, 2048, 32, torch.bfloat16)])
+                                       (1024, 512, 32, torch.float32), (256, 2048, 32, torch.bfloat16),
+                                       (256, 1024, 128, torch.bfloat16), (512, 256, 128, torch.float32)])
 def test_deferred_ef_pass_a_matches_eager_and_fp64(m, n, r, gdt):
     """dion_project_p_ef == (dion_ef_apply on M, then dion_project_p), and both == fp64 math."""
     from megatron_dion_amd.codec import HipDionCodec
