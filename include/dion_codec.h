@@ -41,7 +41,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 9
+#define DION_ABI_VERSION 10
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -61,6 +61,7 @@ typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 #define DION_OP_PROJECT_P_EF 5 /* DION_E_UNSUPPORTED: no fused kernel for this shape */
 #define DION_OP_EF_APPLY 6     /* optional: pre-split P for the rank-update kernels   */
 #define DION_OP_GRAD_SUM_SQ 7  /* dion_grad_sum_sq (only batch, m, n, g_dtype, ld_g used) */
+#define DION_OP_DORTHO 8       /* dion_dortho_sketch / dion_dortho_gram (row-sharded P)   */
 
 typedef struct DionBatchDesc {
   int32_t batch;      /* matrices in this call (all the same shape)            */
@@ -133,6 +134,37 @@ int dion_project_p_ef(const DionBatchDesc* desc, const void* const* G, float* co
 int dion_orthonormalize(const DionBatchDesc* desc, float* P, const float* sketch,
                         uint64_t seed, float oversample, void* ws, size_t ws_bytes,
                         dion_stream_t stream);
+
+/*
+ * Distributed randomised Cholesky QR of a row-sharded P (the "fsdp_tp" kernel kind: P's
+ * rows are split over the TP group, dion/ortho.py:682-834 distributed_orthogonalize).
+ * The collectives stay with the caller; these are the per-rank pieces between them:
+ *
+ *   dion_dortho_sketch:   SP_b = S_b[:, rows] P_b  (k x r per entry, fp32), the local
+ *                         rows' share of the sketch product (ortho.py:777-787), to be
+ *                         reduced (sum) over the group.  `desc` describes the LOCAL shard
+ *                         (m_P local rows, which may be fewer than r); `row_offset` is the
+ *                         global index of this rank's first P row, so a generated sketch is
+ *                         the same global S on every rank (ortho.py:575-640 slices one
+ *                         seeded draw the same way); `sketch` (batch x k x m_P local) may
+ *                         be given instead.  Scratch: DION_OP_DORTHO.
+ *   dion_dortho_qr_inv:   R1inv_b = qr(SP_b).R ^ -1  (r x r; ortho.py:791-792, the solve of
+ *                         :799-806 becomes a product with the inverse).
+ *   dion_dortho_apply:    P_out_b = P_in_b Uinv_b  (ortho.py:799-806, 821-828).
+ *   dion_dortho_gram:     gram_b = P_b^T P_b  (r x r), the local rows' share (ortho.py:808-812).
+ *   dion_dortho_chol_inv: R2inv_b = chol_upper(gram_b) ^ -1 (ortho.py:813-814; a failed
+ *                         pivot poisons the columns from it on with NaN, as cholesky_ex).
+ */
+int dion_dortho_sketch(const DionBatchDesc* desc, const float* P, const float* sketch, uint64_t seed,
+                       int64_t row_offset, float oversample, float* SP, void* ws, size_t ws_bytes,
+                       dion_stream_t stream);
+int dion_dortho_qr_inv(int32_t k, int32_t r, int32_t batch, const float* SP, float* R1inv,
+                       dion_stream_t stream);
+int dion_dortho_apply(const DionBatchDesc* desc, const float* P_in, const float* Uinv, float* P_out,
+                      dion_stream_t stream);
+int dion_dortho_gram(const DionBatchDesc* desc, const float* P, float* gram, void* ws, size_t ws_bytes,
+                     dion_stream_t stream);
+int dion_dortho_chol_inv(int32_t r, int32_t batch, const float* gram, float* R2inv, dion_stream_t stream);
 
 /*
  * Pass B.  R_b = X_b^T P_b  (n_Q x r), fp32.  runtime.py:1476-1477.

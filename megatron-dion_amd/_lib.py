@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # DION_LIB_PATH: load another build of the same ABI (kernel-variant A/B runs during tuning)
 LIB_PATH = os.environ.get("DION_LIB_PATH") or os.path.join(HERE, "csrc", "libdion_codec.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -31,6 +31,7 @@ OP_FIXUP_COLNORM = 4
 OP_PROJECT_P_EF = 5
 OP_EF_APPLY = 6
 OP_GRAD_SUM_SQ = 7
+OP_DORTHO = 8
 
 # every symbol include/dion_codec.h declares
 EXPORTED = (
@@ -40,6 +41,11 @@ EXPORTED = (
     "dion_project_p",
     "dion_project_p_ef",
     "dion_orthonormalize",
+    "dion_dortho_sketch",
+    "dion_dortho_qr_inv",
+    "dion_dortho_apply",
+    "dion_dortho_gram",
+    "dion_dortho_chol_inv",
     "dion_project_r",
     "dion_fixup_colnorm",
     "dion_fixup_colsum",
@@ -96,6 +102,12 @@ _SIGNATURES = {
     "dion_colnorm_apply": ([_DESC, _P, _PP, _P, ctypes.c_float, _P], ctypes.c_int),
     "dion_ef_apply": ([_DESC, _PP, _PP, _P, _P, _PP, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                        ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "dion_dortho_sketch": ([_DESC, _P, _P, ctypes.c_uint64, ctypes.c_int64, ctypes.c_float, _P, _P, ctypes.c_size_t,
+                            _P], ctypes.c_int),
+    "dion_dortho_qr_inv": ([ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P], ctypes.c_int),
+    "dion_dortho_apply": ([_DESC, _P, _P, _P, _P], ctypes.c_int),
+    "dion_dortho_gram": ([_DESC, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "dion_dortho_chol_inv": ([ctypes.c_int32, ctypes.c_int32, _P, _P, _P], ctypes.c_int),
     "dion_round_bf16": ([_P, ctypes.c_int64, _P], ctypes.c_int),
     "dion_grad_sum_sq": ([_DESC, _PP, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_elementwise_adamw": ([ctypes.c_int32, _P, _PP, _PP, ctypes.c_int32, ctypes.c_int32, _PP, _PP, ctypes.c_double,

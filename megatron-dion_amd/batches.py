@@ -77,16 +77,28 @@ def _group_key(bg: DionBatchGroup) -> tuple:
             tuple(_ranks(g) for g in bg.sync_groups))
 
 
-def resolve_dp_batch_group(config, *, replicate_group, group_size: Callable, fs_group=None) -> DionBatchGroup:
-    """resolve_batch_group (batches.py:496-603) for the DP/RP and FS axes (no TP).
+def resolve_dp_batch_group(config, *, replicate_group, group_size: Callable, fs_group=None,
+                           tp_group=None) -> DionBatchGroup:
+    """resolve_batch_group (batches.py:496-603) for the DP/RP, FS and TP axes.
 
-    An FS-sharded entry with an FS group of size > 1 gets the "fsdp" kind: batch size = FS
+    A TP-sharded entry (P-row side, state.py:407-416) with a TP group of size > 1 gets the
+    "fsdp_tp" kind: batch size = TP world, ortho group = TP group (sharding.py:194-209).  An
+    FS-sharded entry with an FS group of size > 1 gets the "fsdp" kind: batch size = FS
     world, q_norm group = FS group, and with low-rank sync over replicas the
     low_rank_replicate_group (:571-603).  Everything else is "ddp" over the replicate group."""
-    if getattr(config, "use_tp_shard", False):
-        raise RuntimeError("[DION_UNSUPPORTED_SHARDING] TP-sharded Dion params are outside this codec's path")
     world = group_size(replicate_group) if replicate_group is not None else 1
     sync = [replicate_group] if (config.use_low_rank_sync and replicate_group is not None and world > 1) else []
+    if getattr(config, "use_tp_shard", False):
+        if tp_group is None:
+            raise RuntimeError("[DION_MISSING_BATCH_TP_GROUP] a TP-sharded Dion param needs its TP group")
+        tp_world = group_size(tp_group)
+        dim, tr = int(getattr(config, "tp_shard_dim", -1)), bool(config.is_transposed)
+        if not ((not tr and dim == 0) or (tr and dim == 1)):
+            raise RuntimeError("[DION_UNSUPPORTED_SHARDING] TP on the contraction side of P is not built")
+        if tp_world > 1:
+            sync.append(tp_group)
+            return DionBatchGroup(kernel_kind="fsdp_tp", replicate_group=replicate_group, ortho_group=tp_group,
+                                  batch_world_size=int(tp_world), sync_groups=tuple(sync))
     if bool(getattr(config, "use_fs_shard", False)):
         if fs_group is None:
             raise RuntimeError("[DION_MISSING_BATCH_FS_GROUP] an FS-sharded Dion param needs its FS group")
@@ -103,7 +115,8 @@ def resolve_dp_batch_group(config, *, replicate_group, group_size: Callable, fs_
 
 def build_dion_batches(*, dion_params: Sequence, get_replicate_group: Callable,
                        group_size: Callable = None, batch_key_cache: Optional[dict] = None,
-                       resolve_fs_group_from_meta: Optional[Callable] = None, **_unused) -> List[DionBatch]:
+                       resolve_fs_group_from_meta: Optional[Callable] = None,
+                       resolve_tp_group: Optional[Callable] = None, **_unused) -> List[DionBatch]:
     """Group, order, chunk and pad routed Dion params into DionBatch objects.
 
     FS-sharded params (config.use_fs_shard) take their FS group from
@@ -125,7 +138,12 @@ def build_dion_batches(*, dion_params: Sequence, get_replicate_group: Callable,
         if bool(getattr(cfg, "use_fs_shard", False)):
             fs_group = resolve_fs_group_from_meta(meta, expect_group=True) if resolve_fs_group_from_meta \
                 else getattr(meta, "fs_group", None)
-        bg = resolve_dp_batch_group(cfg, replicate_group=replicate_group, group_size=group_size, fs_group=fs_group)
+        tp_group = None
+        if bool(getattr(cfg, "use_tp_shard", False)):
+            tp_group = resolve_tp_group(meta, expect_group=True) if resolve_tp_group \
+                else getattr(meta, "tp_group", None)
+        bg = resolve_dp_batch_group(cfg, replicate_group=replicate_group, group_size=group_size, fs_group=fs_group,
+                                    tp_group=tp_group)
         key = (build_batch_key(local_shape, cfg, sp.grad.dtype, global_shape=global_shape,
                                per_expert_global_shape=per_expert,
                                tensor_row_shard_sizes=getattr(meta, "tensor_row_shard_sizes", None),
@@ -159,7 +177,13 @@ def build_dion_batches(*, dion_params: Sequence, get_replicate_group: Callable,
                     momentum=torch.zeros_like(tmpl.momentum), q_tensor=torch.zeros_like(tmpl.q_tensor),
                     param_shape=tmpl.param_shape))
             coll = DionBatchCollectives()
-            if bg.kernel_kind == "fsdp":
+            if bg.kernel_kind == "fsdp_tp":
+                # build_batch_collectives (batches.py:659-771): Q gather, R sum and Q reshard over TP
+                tp = bg.ortho_group
+                ax = DionAxisCollective(indices=tuple(range(size)), process_group=tp, world_size=int(group_size(tp)),
+                                        rank=int(dist.get_rank(tp)))
+                coll = DionBatchCollectives(tp_q_gathers=(ax,), tp_r_collectives=(ax,), tp_q_reshards=(ax,))
+            elif bg.kernel_kind == "fsdp":
                 fs = bg.q_norm_group
                 coll = DionBatchCollectives(fs_collective=DionAxisCollective(
                     indices=tuple(range(size)), process_group=fs, world_size=int(group_size(fs)),

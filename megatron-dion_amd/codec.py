@@ -189,6 +189,59 @@ class HipDionCodec:
                                           ws.data_ptr(), ws.numel(), self._stream())
         _lib.check(rc, "dion_orthonormalize")
 
+    # ------------------------------------------------------------ distributed RCQR
+    # the per-rank pieces of dion/ortho.py:682-834 (P row-sharded over the TP group); the
+    # caller runs the collectives between them (runtime.distributed_orthonormalize)
+    def dortho_sketch(self, P: torch.Tensor, m: int, n: int, transposed: bool, seed: int, row_offset: int,
+                      oversample: float, SP: torch.Tensor, sketch: Optional[torch.Tensor] = None) -> None:
+        """SP_b = S_b[:, rows] P_b (k x r): this rank's share of the sketch product.  `m, n`: the
+        local shard's shape; `row_offset`: global index of the first local P row."""
+        B, _, r = P.shape
+        if B == 0:
+            return
+        d = self._desc(B, m, n, r, transposed)
+        ws = self.workspace(d, _lib.OP_DORTHO)
+        rc = self.lib.dion_dortho_sketch(ctypes.byref(d), P.data_ptr(), None if sketch is None else sketch.data_ptr(),
+                                         int(seed) & ((1 << 64) - 1), int(row_offset), float(oversample),
+                                         SP.data_ptr(), ws.data_ptr(), ws.numel(), self._stream())
+        _lib.check(rc, "dion_dortho_sketch")
+
+    def dortho_qr_inv(self, SP: torch.Tensor, R1inv: torch.Tensor) -> None:
+        """R1inv_b = qr(SP_b).R^-1 (ortho.py:791-806)."""
+        B, k, r = SP.shape
+        if B == 0:
+            return
+        _lib.check(self.lib.dion_dortho_qr_inv(int(k), int(r), int(B), SP.data_ptr(), R1inv.data_ptr(),
+                                               self._stream()), "dion_dortho_qr_inv")
+
+    def dortho_apply(self, P_in: torch.Tensor, Uinv: torch.Tensor, P_out: torch.Tensor, m: int, n: int,
+                     transposed: bool) -> None:
+        """P_out_b = P_in_b Uinv_b (ortho.py:799-806, 821-828)."""
+        B, _, r = P_in.shape
+        if B == 0:
+            return
+        d = self._desc(B, m, n, r, transposed)
+        _lib.check(self.lib.dion_dortho_apply(ctypes.byref(d), P_in.data_ptr(), Uinv.data_ptr(), P_out.data_ptr(),
+                                              self._stream()), "dion_dortho_apply")
+
+    def dortho_gram(self, P: torch.Tensor, gram: torch.Tensor, m: int, n: int, transposed: bool) -> None:
+        """gram_b = P_b^T P_b, this rank's rows' share (ortho.py:808-812)."""
+        B, _, r = P.shape
+        if B == 0:
+            return
+        d = self._desc(B, m, n, r, transposed)
+        ws = self.workspace(d, _lib.OP_DORTHO)
+        _lib.check(self.lib.dion_dortho_gram(ctypes.byref(d), P.data_ptr(), gram.data_ptr(), ws.data_ptr(),
+                                             ws.numel(), self._stream()), "dion_dortho_gram")
+
+    def dortho_chol_inv(self, gram: torch.Tensor, R2inv: torch.Tensor) -> None:
+        """R2inv_b = chol_upper(gram_b)^-1 (ortho.py:813-828)."""
+        B, r, _ = gram.shape
+        if B == 0:
+            return
+        _lib.check(self.lib.dion_dortho_chol_inv(int(r), int(B), gram.data_ptr(), R2inv.data_ptr(), self._stream()),
+                   "dion_dortho_chol_inv")
+
     def project_r(self, momentums: List[torch.Tensor], P: torch.Tensor, R: torch.Tensor,
                   transposed: bool, nonzero: Optional[torch.Tensor] = None) -> None:
         """R = M^T P (or M P).  runtime.py:1476-1477.  `nonzero`: the flags project_p /

@@ -406,7 +406,8 @@ def is_dion_param(param: torch.Tensor, name: str = "") -> bool:
 
 def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str, torch.Tensor]],
                       replicate_group=None, base_seed: int = 0, dion_predicate=None, fs_group=None,
-                      fs_shards: Optional[Dict[str, tuple]] = None,
+                      fs_shards: Optional[Dict[str, tuple]] = None, tp_group=None,
+                      tp_shards: Optional[Dict[str, tuple]] = None,
                       q_stream: str = "device") -> Dict[str, torch.Tensor]:
     """Stand-alone adapter: state init + `route_step_params` for plain data parallelism.
 
@@ -429,6 +430,10 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
     (global_shape, fs_shard_dim, start, end)` marks `param` as this rank's shard of a matrix
     sharded over `fs_group` (distrib_dion/parameter.py:424-466); those params form "fsdp"
     batches of FS-world entries.
+
+    TP sharding: `tp_shards[name] = (global_shape, tp_shard_dim, start, end)` marks `param` as
+    this rank's TP shard over `tp_group` (rows for dim 0, columns for dim 1); Q then holds this
+    rank's columns of r and those params form "fsdp_tp" batches of TP-world entries.
     """
     group = optimizer.param_groups[0]
     rf = float(group.get("rank_fraction", optimizer.defaults["rank_fraction"]))
@@ -445,9 +450,12 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
         mpc = optimizer._mixed_precision_config
         spec = (fs_shards or {}).get(name)
         fs_world = int(dist.get_world_size(fs_group)) if (spec is not None and fs_group is not None) else 1
+        tspec = (tp_shards or {}).get(name)
+        if tspec is not None and tp_group is None:
+            raise RuntimeError(f"[DION_MISSING_BATCH_TP_GROUP] {name}: tp_shards given without tp_group")
         plan = split_plan(p, optimizer.defaults)
         if plan is not None:
-            if spec is not None:
+            if spec is not None or tspec is not None:
                 raise RuntimeError(f"[DION_SPLIT_SHARDED_PARENT] {name}: split children of FS/TP shards are not built")
             family, kinds, segs, flags = plan
             pstate = optimizer.state[p]
@@ -477,7 +485,11 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
                                      q_dtype=_as_dtype(getattr(mpc, "q_dtype", None)),
                                      use_low_rank_sync=optimizer.use_low_rank_sync,
                                      fs_shard=None if spec is None else (tuple(spec[0]), spec[1], spec[2], spec[3],
-                                                                         fs_world), q_stream=q_stream)
+                                                                         fs_world),
+                                     tp_shard=None if tspec is None else (tuple(tspec[0]), tspec[1], tspec[2], tspec[3],
+                                                                          int(dist.get_world_size(tp_group)),
+                                                                          int(dist.get_rank(tp_group))),
+                                     q_stream=q_stream)
         optimizer.state[p].update(state)
         meta = DionDistMeta(shape=tuple(p.shape), global_shape=tuple(state["global_shape"]), rank_fraction=rf,
                             is_transposed=cfg.is_transposed, param_uid=(name,), is_dion_param=True,
@@ -485,6 +497,9 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
         if spec is not None:
             meta.extra.update(fs_group=fs_group, fs_shard_dim=int(spec[1]), fs_start_idx=int(spec[2]),
                               fs_end_idx=int(spec[3]), fs_world_size=fs_world)
+        if tspec is not None:
+            meta.extra.update(tp_group=tp_group, tp_shard_dim=int(tspec[1]), tp_start_idx=int(tspec[2]),
+                              tp_end_idx=int(tspec[3]), tp_world_size=int(dist.get_world_size(tp_group)))
         metas[name] = (cfg, meta)
     ordered = sorted(dion_named, key=lambda kv: kv[0])
 
@@ -518,7 +533,8 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
         batches = build_dion_batches(
             dion_params=steps, get_replicate_group=lambda: replicate_group,
             group_size=lambda g: dist.get_world_size(g),
-            resolve_fs_group_from_meta=lambda meta, expect_group=True: meta.extra.get("fs_group"))
+            resolve_fs_group_from_meta=lambda meta, expect_group=True: meta.extra.get("fs_group"),
+            resolve_tp_group=lambda meta, expect_group=True: meta.extra.get("tp_group"))
         elementwise = []
         for _, p in ew_named:
             g = grad_of(p)

@@ -15,6 +15,7 @@ concurrent same-shape batches read each other's P).
 from __future__ import annotations
 
 import collections
+import math
 import weakref
 from typing import Callable, Generator, Iterable, List, Optional
 
@@ -79,9 +80,10 @@ def _group_world(group) -> int:
 
 def is_replicated(batch) -> bool:
     """True when the batch exchanges factors with other ranks: replicas (replicate group size > 1)
-    or FS shards (the "fsdp" kind)."""
+    or FS / TP shards (the "fsdp" and "fsdp_tp" kinds)."""
     bg = getattr(batch, "batch_group", None)
-    return _group_world(getattr(bg, "replicate_group", None)) > 1 or str(getattr(bg, "kernel_kind", "ddp")) == "fsdp"
+    return (_group_world(getattr(bg, "replicate_group", None)) > 1
+            or str(getattr(bg, "kernel_kind", "ddp")) in ("fsdp", "fsdp_tp"))
 
 
 def validate_update_contract(optimizer, *, optim_groups, optimizer_states, dist_metas, param_shapes,
@@ -140,8 +142,31 @@ def check_supported_batch(optimizer, *, batch_group, batch_collectives, configs,
     tp_colls = batch_collectives is not None and any(
         len(tuple(getattr(batch_collectives, f, None) or ())) for f in ("tp_q_gathers", "tp_r_collectives",
                                                                          "tp_q_reshards"))
-    if kind not in ("ddp", "fsdp"):
+    reals = configs[:int(real_batch_size)]
+    if kind not in ("ddp", "fsdp", "fsdp_tp"):
         why = f"kernel_kind={kind!r}"
+    elif kind == "fsdp_tp":
+        og = getattr(batch_group, "ortho_group", None)
+        gathers = tuple(getattr(batch_collectives, "tp_q_gathers", None) or ()) if batch_collectives else ()
+        rsums = tuple(getattr(batch_collectives, "tp_r_collectives", None) or ()) if batch_collectives else ()
+        every = set(range(len(param_shapes)))
+        if og is None or world(og) <= 1:
+            why = "an fsdp_tp batch without its TP ortho group"
+        elif not all(is_p_tp_sharded(c) for c in reals):
+            why = "an fsdp_tp batch whose entries are not TP-sharded on the P-row side"
+        elif len(gathers) != 1 or set(int(i) for i in gathers[0].indices) != every:
+            why = "an fsdp_tp batch without one Q all-gather over all its entries"
+        elif len(rsums) != 1 or set(int(i) for i in rsums[0].indices) != every:
+            why = "an fsdp_tp batch without one R all-reduce over all its entries"
+        elif any(bool(getattr(c, "use_fs_shard", False)) and not reduces_p_over_fs(c) for c in reals):
+            why = "FS shards on the P-row side together with TP (P sharded on both axes)"
+        elif any(bool(getattr(c, "use_fs_shard", False)) for c in reals) and (
+                not len(tuple(getattr(batch_collectives, "fs_p_collectives", None) or ()))
+                or getattr(batch_group, "q_norm_group", None) is None):
+            why = "an FS-sharded fsdp_tp batch without its FS P reduction and q_norm group"
+        elif any(optimizer_states[i] is not None and getattr(optimizer_states[i].get("momentum"), "dtype", None)
+                 == torch.bfloat16 for i in range(int(real_batch_size))):
+            why = "bf16 momentum with the fsdp_tp kind (not built)"
     elif getattr(batch_group, "ortho_group", None) is not None and world(batch_group.ortho_group) > 1:
         why = "a distributed ortho_group (TP-sharded P)"
     elif tp_colls or any(bool(getattr(c, "use_tp_shard", False)) for c in configs[:int(real_batch_size)]):
@@ -174,7 +199,31 @@ def check_supported_batch(optimizer, *, batch_group, batch_collectives, configs,
     if why is not None:
         raise RuntimeError(
             f"[DION_UNSUPPORTED_KERNEL_KIND] step={optimizer._step_count}: {why}; this codec computes "
-            "whole-matrix data-parallel ('ddp') batches and FS-sharded ('fsdp') batches without TP")
+            "whole-matrix data-parallel ('ddp') batches, FS-sharded ('fsdp') batches, and TP-sharded "
+            "('fsdp_tp') batches with TP on the P-row side (FS, if any, on the contraction side)")
+
+
+def is_p_tp_sharded(config) -> bool:
+    """dion/state.py:407-416: TP shards the P-row side (tp_shard_dim 0 not transposed, 1 transposed)."""
+    if not (bool(getattr(config, "use_tp_shard", False)) and bool(getattr(config, "has_tp_shard", True))):
+        return False
+    dim, tr = int(getattr(config, "tp_shard_dim", -1)), bool(config.is_transposed)
+    return (not tr and dim == 0) or (tr and dim == 1)
+
+
+def reduces_p_over_fs(config) -> bool:
+    """dion/state.py:399-404: FS shards the contraction side, so P = X Q is a partial sum over FS."""
+    if not bool(getattr(config, "use_fs_shard", False)):
+        return False
+    dim, tr = int(getattr(config, "fs_shard_dim", -1)), bool(config.is_transposed)
+    return (not tr and dim == 1) or (tr and dim == 0)
+
+
+def split_range(size: int, world: int, rank: int):
+    """dion/ortho.py:247-259: contiguous shard [start, end) of `rank`, remainder on the first ranks."""
+    base, rem = size // world, size % world
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
 
 
 def _sketch_seed(optimizer, batch_cache_key: int, entry: int) -> int:
@@ -217,6 +266,11 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     use_low_rank = bool(optimizer.use_low_rank_sync) and W > 1 and any(
         bool(c.use_low_rank_sync) for c in configs)
     real_grads = [g for g in (grads or [])[:real]] if grads is not None else []
+    if str(getattr(batch_group, "kernel_kind", "ddp")) == "fsdp_tp":
+        yield from _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, optim_groups, real_grads,
+                                    optimizer_states, param_shapes, real, batch_cache_key, batch_group,
+                                    batch_collectives, commit_updates, use_low_rank, sketches)
+        return
     if str(getattr(batch_group, "kernel_kind", "ddp")) == "fsdp":
         yield from _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, optim_groups, real_grads,
                                     optimizer_states, param_shapes, real, batch_cache_key, batch_group,
@@ -492,6 +546,224 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     codec.colnorm_apply(R, list(Qs[:real]), colsum, float(optimizer.defaults["epsilon"]), m, n, transposed)
     _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim_groups, optimizer_states,
                    dist_metas, real, m, n, transposed, defer, commit_updates)
+
+
+def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, optim_groups, real_grads,
+                     optimizer_states, param_shapes, real, batch_cache_key, batch_group, batch_collectives,
+                     commit_updates, use_low_rank, sketches):
+    """One TP ("fsdp_tp") batch: every entry is this rank's TP shard of a matrix, sharded on the
+    P-row side (dion/state.py:304-310, 407-416), and its Q holds this rank's columns of Q
+    (resolve_q_state_layout, state.py:159-217).  The reference's order:
+
+      dense all-reduce of G across replicas without low-rank sync     runtime.py:1553-1558
+      Q all-gathered over TP (columns in rank order)                  runtime.py:680-873
+      M += G; P = X Q_full (this rank's rows of P)                    pass A, local
+      FS on the contraction side: all-reduce(sum) of P over FS        runtime.py:876-920
+      with low-rank sync over replicas: all-reduce(avg) of P          runtime.py:1339-1345
+      row-sharded randomised Cholesky QR over the TP group            ortho.py:682-834
+      R = X^T P, all-reduce(sum) over TP (+ avg over replicas)        runtime.py:923-962, 1361-1376
+      fix-up with the local zero test and the gathered Q; column norm (summed over the FS
+        q_norm group when FS shards the rows of R); error feedback on the shard; weight
+        update with the GLOBAL shape's LR                              runtime.py:1838-1901
+      Q <- this rank's columns of the new Q                           ortho.py:837-871, runtime.py:1101-1132
+    `sketches` (tests): entry -> this rank's (k, local rows) slice of the sketch."""
+    codec = optimizer.codec
+    group = getattr(batch_group, "replicate_group", None)
+    W = _group_world(group)
+    if W > 1 and not use_low_rank and real_grads:
+        op = dist.ReduceOp.AVG if optimizer.defaults.get("rp_average_in_collective", True) else dist.ReduceOp.SUM
+        works = [dist.all_reduce(g, op=op, group=group, async_op=True) for g in real_grads]
+        yield
+        for w in works:
+            w.wait()
+    B = len(params)
+    m, n = (int(d) for d in param_shapes[0])
+    transposed = bool(configs[0].is_transposed)
+    mp, nq = factor_rows(m, n, transposed)
+    dev = momentums[0].device
+    # Q unshard: all-gather this rank's columns (padded to the widest rank) over TP
+    gath = batch_collectives.tp_q_gathers[0]
+    tp_group, T, tp_rank = gath.process_group, int(gath.world_size), int(gath.rank)
+    r = int((optimizer_states[0] or {}).get("r", -1))
+    if r <= 0:
+        raise RuntimeError(f"[DION_INVALID_Q_UNSHARD_RANK] step={optimizer._step_count} r={r}")
+    cols = [split_range(r, T, k) for k in range(T)]
+    widest = max(c1 - c0 for c0, c1 in cols)
+    c0, c1 = cols[tp_rank]
+    for i in range(B):
+        if tuple(Qs[i].shape) != (nq, c1 - c0):
+            raise RuntimeError(f"[DION_Q_UNSHARD_LOCAL_RANK_MISMATCH] step={optimizer._step_count} entry={i} "
+                               f"local_shape={tuple(Qs[i].shape)} expected={(nq, c1 - c0)} r={r} tp={T}")
+    local = torch.zeros((B, nq, widest), dtype=torch.float32, device=dev)
+    for i in range(B):
+        local[i, :, :c1 - c0].copy_(Qs[i])
+    gathered = torch.empty((T * B, nq, widest), dtype=torch.float32, device=dev)
+    work = dist.all_gather_into_tensor(gathered, local, group=tp_group, async_op=True)
+    yield
+    work.wait()
+    gathered = gathered.view(T, B, nq, widest)
+    Qfull = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
+    for k, (a, b) in enumerate(cols):
+        Qfull[:, :, a:b].copy_(gathered[k, :, :, :b - a])
+    del local, gathered
+    qviews = [Qfull[i] for i in range(B)]
+    P = torch.zeros((B, mp, r), dtype=torch.float32, device=dev)
+    nonzero = torch.zeros((B,), dtype=torch.int32, device=dev)
+    defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
+             and (commit_updates is None or all(c is None for c in commit_updates[:real]))
+             and codec.supports_deferred_ef(m, n, r, transposed))
+    _project_with_pending(codec, real_grads, momentums, qviews, P, nonzero, optimizer_states, real, m, n, transposed,
+                          defer)
+    for coll in tuple(getattr(batch_collectives, "fs_p_collectives", None) or ()):
+        if coll.process_group is not None and int(coll.world_size) > 1:
+            idx = [int(i) for i in coll.indices]
+            work = (dist.all_reduce(P, op=dist.ReduceOp.SUM, group=coll.process_group, async_op=True)
+                    if idx == list(range(B)) else
+                    dist.all_reduce_coalesced([P[i] for i in idx], op=dist.ReduceOp.SUM, group=coll.process_group,
+                                              async_op=True))
+            yield
+            work.wait()
+    if use_low_rank and W > 1:
+        work = dist.all_reduce(P, op=dist.ReduceOp.AVG, group=group, async_op=True)
+        yield
+        work.wait()
+    yield from distributed_orthonormalize(optimizer, P, real, m, n, transposed, batch_group.ortho_group, dist_metas,
+                                          batch_cache_key, sketches)
+    R = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
+    codec.project_r(list(momentums[:real]), P[:real], R[:real], transposed, nonzero=nonzero)
+    if real < B:
+        R[real:].zero_()
+    rsum = batch_collectives.tp_r_collectives[0]
+    work = dist.all_reduce(R, op=dist.ReduceOp.SUM, group=rsum.process_group, async_op=True)
+    yield
+    work.wait()
+    if use_low_rank and W > 1:
+        work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
+        yield
+        work.wait()
+    eps = float(optimizer.defaults["epsilon"])
+    qgroup = getattr(batch_group, "q_norm_group", None)
+    if qgroup is not None and _group_world(qgroup) > 1:
+        colsum = torch.empty((real, r), dtype=torch.float32, device=dev)
+        codec.fixup_colsum(P, R, qviews[:real], nonzero, colsum, m, n, transposed)
+        work = dist.all_reduce(colsum, op=dist.ReduceOp.SUM, group=qgroup, async_op=True)
+        yield
+        work.wait()
+        codec.colnorm_apply(R, qviews[:real], colsum, eps, m, n, transposed)
+    else:
+        codec.fixup_colnorm(P, R, qviews[:real], nonzero, eps, m, n, transposed)
+    _apply_updates(optimizer, codec, params, momentums, qviews, P, R, nonzero, optim_groups, optimizer_states,
+                   dist_metas, real, m, n, transposed, defer, commit_updates)
+    for i in range(real):  # reshard_q_along_tp: keep this rank's columns
+        Qs[i].copy_(Qfull[i][:, c0:c1])
+
+
+def _tp_row_sizes(dist_metas, real, T, global_rows):
+    """ortho.py:270-380: explicit row_shard_sizes from the metadata, else the canonical split."""
+    meta = next((d for d in dist_metas[:real] if d is not None), None)
+    explicit = getattr(meta, "row_shard_sizes", None) if meta is not None else None
+    if explicit is not None:
+        sizes = [int(x) for x in explicit]
+        if len(sizes) != T or sum(sizes) != global_rows:
+            raise RuntimeError(f"[DION_ORTHO_ROW_SIZES_MISMATCH] row_shard_sizes={tuple(sizes)} ortho_world={T} "
+                               f"global_rows={global_rows}")
+        return sizes
+    return [b - a for a, b in (split_range(global_rows, T, k) for k in range(T))]
+
+
+def distributed_orthonormalize(optimizer, P, real, m, n, transposed, ortho_group, dist_metas, batch_cache_key,
+                               sketches=None):
+    """Randomised Cholesky QR of the first `real` entries of a row-sharded P (this rank's rows,
+    in place), dion/ortho.py:682-834.  The small products run on the device (dion_dortho_*);
+    the reductions over the ortho group follow the reference's partition: reduce-scatter
+    (sum) over batch shards, the owner factors its entries, all-gather of the factors."""
+    codec = optimizer.codec
+    T, rank = _group_world(ortho_group), int(dist.get_rank(ortho_group))
+    B, rows, r = (int(x) for x in P.shape)
+    dev = P.device
+    meta0 = next((d for d in dist_metas[:real] if d is not None), None)
+    gshape = getattr(meta0, "global_shape", None) if meta0 is not None else None
+    if gshape is None:
+        raise RuntimeError("[DION_MISSING_ORTHO_GLOBAL_SHAPE] distributed orthonormalisation needs global_shape")
+    global_rows = int(gshape[1]) if transposed else int(gshape[0])
+    sizes = _tp_row_sizes(dist_metas, real, T, global_rows)
+    if sizes[rank] != rows:
+        raise RuntimeError(f"[DION_ORTHO_ROW_LAYOUT_MISMATCH] local rows {rows} != {sizes[rank]} "
+                           f"(row sizes {tuple(sizes)}, rank {rank})")
+    offset = sum(sizes[:rank])
+    Pa = P[:real]
+    if global_rows <= r:
+        # ortho.py:752-775: the whole P is a short matrix; every rank gathers the rows and
+        # takes the Q factor of the same Householder QR (the reference gives each rank a share
+        # of the batch instead: the same numbers)
+        widest = max(sizes)
+        buf = torch.zeros((real, widest, r), dtype=torch.float32, device=dev)
+        buf[:, :rows].copy_(Pa)
+        allrows = torch.empty((T * real, widest, r), dtype=torch.float32, device=dev)
+        work = dist.all_gather_into_tensor(allrows, buf, group=ortho_group, async_op=True)
+        yield
+        work.wait()
+        allrows = allrows.view(T, real, widest, r)
+        full = torch.cat([allrows[k, :, :sizes[k]] for k in range(T)], dim=1).contiguous()
+        codec.orthonormalize(full, global_rows, max(r, 1), False, 0, float(optimizer.defaults["rcqr_oversample"]))
+        Pa.copy_(full[:, offset:offset + rows])
+        return
+    oversample = float(optimizer.defaults["rcqr_oversample"])
+    k = int(math.ceil(oversample * r / 128.0) * 128)  # ortho.py:595
+    shares = [b - a for a, b in (split_range(real, T, q) for q in range(T))]
+    most = max(shares)
+    starts = [sum(shares[:q]) for q in range(T)]
+
+    def exchange(local_full, width):
+        """Reduce-scatter (sum) the (real, width, r) products by batch shards; return this rank's
+        (most, width, r) sums (ortho.py:529-572)."""
+        padded = torch.zeros((T * most, width, r), dtype=torch.float32, device=dev)
+        for q in range(T):
+            if shares[q]:
+                padded[q * most:q * most + shares[q]].copy_(local_full[starts[q]:starts[q] + shares[q]])
+        mine = torch.empty((most, width, r), dtype=torch.float32, device=dev)
+        work = dist.reduce_scatter_tensor(mine, padded, op=dist.ReduceOp.SUM, group=ortho_group, async_op=True)
+        return mine, work
+
+    def gather(mine_inv):
+        """All-gather the owners' (most, r, r) factors back to (real, r, r) (ortho.py:383-419)."""
+        allf = torch.empty((T * most, r, r), dtype=torch.float32, device=dev)
+        work = dist.all_gather_into_tensor(allf, mine_inv, group=ortho_group, async_op=True)
+        return allf, work
+
+    def unpack(allf):
+        return torch.cat([allf[q * most:q * most + shares[q]] for q in range(T) if shares[q]], dim=0).contiguous()
+
+    SP = torch.empty((real, k, r), dtype=torch.float32, device=dev)
+    if sketches is not None:
+        S = torch.stack([sketches[i].to(device=dev, dtype=torch.float32) for i in range(real)], dim=0).contiguous()
+    else:
+        S = None
+    seed = _sketch_seed(optimizer, batch_cache_key, 0)
+    codec.dortho_sketch(Pa, m, n, transposed, seed, offset, oversample, SP, sketch=S)
+    mine, work = exchange(SP, k)
+    yield
+    work.wait()
+    inv = torch.zeros((most, r, r), dtype=torch.float32, device=dev)
+    if shares[rank]:
+        codec.dortho_qr_inv(mine[:shares[rank]].contiguous(), inv[:shares[rank]])
+    allf, work = gather(inv)
+    yield
+    work.wait()
+    P1 = torch.empty_like(Pa)
+    codec.dortho_apply(Pa, unpack(allf), P1, m, n, transposed)
+    gram = torch.empty((real, r, r), dtype=torch.float32, device=dev)
+    codec.dortho_gram(P1, gram, m, n, transposed)
+    mine, work = exchange(gram, r)
+    yield
+    work.wait()
+    inv.zero_()
+    if shares[rank]:
+        codec.dortho_chol_inv(mine[:shares[rank]].contiguous(), inv[:shares[rank]])
+    allf, work = gather(inv)
+    yield
+    work.wait()
+    codec.dortho_apply(P1, unpack(allf), Pa, m, n, transposed)
 
 
 def _project_with_pending(codec, real_grads, momentums, Qs, P, nonzero, optimizer_states, real, m, n, transposed,

@@ -53,8 +53,9 @@ def q_seed_from_param_key(*, base_seed: int, param_uid, param_name: str,
 
 
 def init_q(q_global_shape: Tuple[int, int], seed: int, device, dtype=torch.float32,
-           rows: Optional[Tuple[int, int]] = None) -> torch.Tensor:
-    """Rows [rows[0], rows[1]) (default: all) of the seeded Q0 ~ N(0, 1) of the global shape,
+           rows: Optional[Tuple[int, int]] = None, cols: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+    """Rows [rows[0], rows[1]) and columns [cols[0], cols[1]) (default: all; columns are a TP
+    rank's share of r) of the seeded Q0 ~ N(0, 1) of the global shape,
     drawn the way the reference draws on that device (dion/state.py:50-109,
     _normal_q_submatrix):
       * CPU: one torch.randn of the full global shape on a CPU generator, then the rows
@@ -65,22 +66,23 @@ def init_q(q_global_shape: Tuple[int, int], seed: int, device, dtype=torch.float
     Draws are made in `dtype` itself, as the reference does.  Pinned by the reference's
     CPU captures (tests/test_host.py); the device stream is the same torch calls on the
     same torch build, checked for shard consistency on the GPU (tests/test_gpu_parity.py)."""
-    q_rows, cols = (int(d) for d in q_global_shape)
+    q_rows, ncols = (int(d) for d in q_global_shape)
     r0, r1 = (0, q_rows) if rows is None else (int(rows[0]), int(rows[1]))
+    c0, c1 = (0, ncols) if cols is None else (int(cols[0]), int(cols[1]))
     device = torch.device(device)
     if device.type == "cpu":
         gen = torch.Generator(device="cpu")
         gen.manual_seed(int(seed))
-        q = torch.randn((q_rows, cols), generator=gen, dtype=dtype)
-        return q[r0:r1].contiguous()
+        q = torch.randn((q_rows, ncols), generator=gen, dtype=dtype)
+        return q[r0:r1, c0:c1].contiguous()
     gen = torch.Generator(device=device)
     gen.manual_seed(int(seed))
-    q = torch.empty((r1 - r0, cols), device=device, dtype=dtype)
+    q = torch.empty((r1 - r0, c1 - c0), device=device, dtype=dtype)
     for i, row in enumerate(range(r0, r1)):
-        first = row * cols
+        first = row * ncols + c0
         base = first - first % 4
         gen.set_offset(base)
-        draw = torch.empty(first - base + cols, device=device, dtype=dtype)
+        draw = torch.empty(first - base + (c1 - c0), device=device, dtype=dtype)
         draw.normal_(0.0, 1.0, generator=gen)
         q[i].copy_(draw[first - base:])
     return q
@@ -89,7 +91,7 @@ def init_q(q_global_shape: Tuple[int, int], seed: int, device, dtype=torch.float
 def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_of: int = 1,
                     base_seed: int = 0, param_uid=None, param_name: str = "",
                     momentum_dtype: Optional[torch.dtype] = None, q_dtype: Optional[torch.dtype] = None,
-                    use_low_rank_sync: bool = True, fs_shard=None,
+                    use_low_rank_sync: bool = True, fs_shard=None, tp_shard=None,
                     with_momentum: bool = True, q_stream: str = "device") -> Tuple[dict, DionParamConfig]:
     """Fresh optimizer state + config for one 2D parameter (no TP sharding).
 
@@ -100,10 +102,47 @@ def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_
     not, state.py:304-310) so the sharded dim is always the contraction side of P = X Q; Q is
     the seeded global Q's rows [start, end), drawn on the parameter's device (init_q).
     `momentum_dtype` / `q_dtype` follow DionMixedPrecisionConfig (dion/state.py:502-514,
-    544-547): None keeps the parameter's dtype; the speedrun sets both to bf16."""
+    544-547): None keeps the parameter's dtype; the speedrun sets both to bf16.
+
+    `tp_shard = (global_shape, tp_shard_dim, start, end, tp_world, tp_rank)`: this rank's TP
+    shard (rows for dim 0, columns for dim 1).  TP takes the P-row side (dim 0 -> not
+    transposed, dim 1 -> transposed, state.py:304-310), Q keeps all its rows and this rank's
+    columns of r (resolve_q_state_layout, state.py:159-217: split_range(r, tp, rank))."""
     if param.dim() != 2:
         raise RuntimeError(f"[DION_NOT_2D] shape={tuple(param.shape)}")
     ml, nl = (int(d) for d in param.shape)
+    if tp_shard is not None:
+        if fs_shard is not None:
+            raise RuntimeError("[DION_UNSUPPORTED_SHARDING] FS and TP shards of one param are not built "
+                               "in the stand-alone adapter")
+        (m, n), dim, start, end, tp_world, tp_rank = tp_shard
+        m, n, dim, tp_world, tp_rank = int(m), int(n), int(dim), int(tp_world), int(tp_rank)
+        if dim not in (0, 1):
+            raise RuntimeError(f"[DION_BAD_TP_SHARD_DIM] tp_shard_dim={dim}")
+        if (ml, nl) != ((end - start, n) if dim == 0 else (m, end - start)):
+            raise RuntimeError(f"[DION_BAD_TP_SHARD] local {(ml, nl)} vs global {(m, n)} dim {dim} [{start}, {end})")
+        transposed = dim == 1
+        r = rank_for_shape(m, n, rank_fraction, rank_multiple_of)
+        base = r // tp_world
+        rem = r % tp_world
+        c0 = tp_rank * base + min(tp_rank, rem)
+        c1 = c0 + base + (1 if tp_rank < rem else 0)
+        if c1 <= c0:
+            raise RuntimeError(f"[DION_EMPTY_Q_SHARD] r_global={r} tp_world_size={tp_world} tp_rank={tp_rank}")
+        q_shape = (m if transposed else n, r)
+        seed = q_seed_from_param_key(base_seed=base_seed, param_uid=param_uid, param_name=param_name,
+                                     q_global_shape=q_shape, is_transposed=transposed)
+        if q_stream not in ("device", "cpu"):
+            raise RuntimeError(f"[DION_INVALID_Q_STREAM] q_stream={q_stream!r}")
+        q = init_q(q_shape, seed, param.device if q_stream == "device" else "cpu", dtype=q_dtype or param.dtype,
+                   cols=(c0, c1)).to(param.device)
+        state = {"Q": q, "r": r, "local_shape": (ml, nl), "global_shape": (m, n)}
+        if with_momentum:
+            state = {"momentum": torch.zeros_like(param, dtype=momentum_dtype or param.dtype), **state}
+        cfg = DionParamConfig(is_transposed=transposed, use_low_rank_sync=bool(use_low_rank_sync) and
+                              should_use_low_rank_sync(global_shape=(m, n), r_global=r, rank_fraction=rank_fraction))
+        cfg.has_tp_shard, cfg.use_tp_shard, cfg.tp_shard_dim = True, tp_world > 1, dim
+        return state, cfg
     if fs_shard is None:
         m, n = ml, nl
         transposed = is_transposed_shape(m, n)

@@ -45,6 +45,29 @@ class OracleCodec:
             out = O.orthogonalize(P[b:b + 1], oversample, sketch=S, generator=gen)
             P[b:b + 1] = out.to(state_dtype)      # ortho.py:123 casts back to P's dtype
 
+    # distributed RCQR pieces (dion/ortho.py:682-834): the reference's arithmetic, with the
+    # triangular solves as products with the explicit inverses the codec interface passes on
+    def dortho_sketch(self, P, m, n, transposed, seed, row_offset, oversample, SP, sketch=None):
+        if sketch is None:
+            raise RuntimeError("[ORACLE_CODEC] the distributed sketch needs an explicit slice on CPU")
+        SP.copy_(sketch.to(torch.float32) @ P)
+
+    def dortho_qr_inv(self, SP, R1inv):
+        R1 = torch.linalg.qr(SP.to(torch.float32), mode="r")[1]
+        eye = torch.eye(R1.shape[-1], dtype=torch.float32).expand_as(R1)
+        R1inv.copy_(torch.linalg.solve_triangular(R1, eye, upper=True))
+
+    def dortho_apply(self, P_in, Uinv, P_out, m, n, transposed):
+        P_out.copy_(P_in @ Uinv)
+
+    def dortho_gram(self, P, gram, m, n, transposed):
+        gram.copy_(P.mT @ P)
+
+    def dortho_chol_inv(self, gram, R2inv):
+        R2 = torch.linalg.cholesky_ex(gram.to(torch.float32), upper=True)[0]
+        eye = torch.eye(R2.shape[-1], dtype=torch.float32).expand_as(R2)
+        R2inv.copy_(torch.linalg.solve_triangular(R2, eye, upper=True))
+
     def round_bf16(self, X):
         X.copy_(X.to(torch.bfloat16).float())
 

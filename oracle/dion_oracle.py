@@ -26,6 +26,8 @@ Reference files (all under `/root/reference/megatron/core/optimizer/`):
   dion/state.py:179-188      rank rule;  state.py:220-230 low-rank-sync rule
   dion/runtime.py:1729-1795, :965-1013  the FS ("fsdp") kind: RS(sum)/ortho/AG of the
                              partial P, shard-local R / fix-up / EF, column norm over shards
+  dion/runtime.py:1328-1377, :680-873, :923-962; ortho.py:575-640, 682-871  the TP ("fsdp_tp")
+                             kind: Q unshard, row-sharded RCQR, R sum over TP, Q reshard
 """
 
 from __future__ import annotations
@@ -48,6 +50,10 @@ __all__ = [
     "DionHyper",
     "dion_batch_step_local",
     "dion_batch_step_replicated",
+    "dion_batch_step_tp",
+    "split_range",
+    "distributed_sketch_seed",
+    "reference_sharded_sketch",
     "grad_sum_sq_fp64",
     "elementwise_adamw",
     "elementwise_lion",
@@ -194,11 +200,13 @@ def _project(mats: Sequence[DionMatrix]):
 
 
 def _finish(mats: Sequence[DionMatrix], X, Qb, P, R, real: int, hyper: DionHyper,
-            m_global: int, n_global: int, colsum_reduce=None):
+            m_global: int, n_global: int, colsum_reduce=None, q_cols=None):
     """runtime.py:1838-1901: fix-up, error feedback, column norm, weight update, Q commit.
 
     `colsum_reduce(col_sum_sq)` (FS kind) returns the column sums of squares summed over
-    the q_norm group (runtime.py:994-1001); the local sums are used otherwise."""
+    the q_norm group (runtime.py:994-1001); the local sums are used otherwise.  `q_cols`
+    (TP kind) = (c0, c1): the rank keeps only those columns of the new Q
+    (reshard_q_along_tp, ortho.py:837-871)."""
     P, R = fix_all_zero_or_nan(P, R, Qb, X, real)
     transposed = mats[0].transposed
     alpha = -(1.0 - hyper.mu)
@@ -225,7 +233,7 @@ def _finish(mats: Sequence[DionMatrix], X, Qb, P, R, real: int, hyper: DionHyper
         if hyper.weight_decay > 0:
             mats[i].W.mul_(1 - hyper.lr * hyper.weight_decay)
         mats[i].W.add_(delta[i].to(mats[i].W.dtype), alpha=-s)
-        mats[i].Q.copy_(Qn[i])
+        mats[i].Q.copy_(Qn[i] if q_cols is None else Qn[i][:, q_cols[0]:q_cols[1]])
         mats[i].trace.update(P=P[i].clone(), R=R[i].clone(), Qn=Qn[i].clone())
 
 
@@ -363,6 +371,99 @@ def dion_step_fs(batches, hyper: DionHyper, sketch_fn=None, max_concurrent: int 
     `batches` is a list of (per_rank, real, (m_global, n_global)) as _fs_batch_gen takes them."""
     gens = (_fs_batch_gen(per_rank, real, hyper, sketch_fn, mg, ng) for per_rank, real, (mg, ng) in batches)
     run_async_runtime(gens, max_concurrent=max_concurrent)
+
+
+def split_range(size: int, world: int, rank: int):
+    """dion/ortho.py:247-259 (_split_range): contiguous shards, remainder on the first ranks."""
+    base, rem = size // world, size % world
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def distributed_sketch_seed(step_count: int, param_uid, param_name: str) -> int:
+    """dion/ortho.py:126-131 + 154-177: the seed of one matrix's distributed sketch,
+    blake2b(repr(("distributed", step, param_uid, param_name)))."""
+    import hashlib
+    key = ("distributed", int(step_count), param_uid, param_name)
+    return int.from_bytes(hashlib.blake2b(repr(key).encode("utf-8"), digest_size=8).digest(),
+                          "little") & ((1 << 63) - 1)
+
+
+def reference_sharded_sketch(seed: int, k: int, global_rows: int, row_start: int, rows: int) -> torch.Tensor:
+    """dion/ortho.py:575-640 on CPU: one seeded N(0, 1/k) draw of the (k, global_rows) sketch,
+    of which the rank keeps its columns [row_start, row_start + rows)."""
+    gen = torch.Generator(device="cpu")
+    gen.manual_seed(int(seed))
+    full = torch.empty((k, global_rows), dtype=torch.float32)
+    full.normal_(mean=0.0, std=math.sqrt(1.0 / k), generator=gen)
+    return full[:, row_start:row_start + rows].clone()
+
+
+def dion_batch_step_tp(per_rank: List[List[DionMatrix]], hyper: DionHyper, m_global: int, n_global: int,
+                       sketch_fn=None) -> None:
+    """One "fsdp_tp" batch, every TP rank simulated (TP world T; no FS, no replicas).
+
+    per_rank[k][i]: rank k's shard of matrix i -- W/M/G its rows of the P side (tp_shard_dim on
+    m_P, dion/state.py:304-310 and :407-416) and Q its columns of the rank (resolve_q_state_layout,
+    state.py:159-217).  Reference order:
+      M += G (local); Q all-gathered over TP, columns in rank order       runtime.py:1560-1566, :680-873
+      P_k = X_k Q (this rank's rows of P)                                  runtime.py:1602-1616
+      distributed RCQR over the row shards (ortho.py:682-834):
+        global rows <= r: QR of the whole P (rows exchanged, :752-775)
+        else SP = sum_k S[:, rows_k] P_k (reduce-scatter over batch shards), R1 = qr(SP).R,
+             P_k = P_k R1^-1; G = sum_k P_k^T P_k, R2 = chol_upper(G), P_k = P_k R2^-1
+      R = sum_k X_k^T P_k (all-reduce sum over TP, runtime.py:923-962)
+      per rank: fix-up with ITS shard's zero test and the gathered Q, error feedback on its shard,
+        column norm of the full R (no q_norm group), weight update with the GLOBAL shape's LR,
+        Q <- its columns of the new Q (ortho.py:837-871)
+    `sketch_fn(k, i, rows)` returns rank k's (k_s, rows) slice of entry i's sketch."""
+    T = len(per_rank)
+    real = len(per_rank[0])
+    Qfull = [torch.cat([per_rank[k][i].Q for k in range(T)], dim=1) for i in range(real)]
+    r = int(Qfull[0].shape[1])
+    cols, start = [], 0
+    for k in range(T):
+        w = int(per_rank[k][0].Q.shape[1])
+        cols.append((start, start + w))
+        start += w
+    Xs, Ps = [], []
+    for k in range(T):
+        for mt in per_rank[k]:
+            if mt.G is not None:
+                mt.M.add_(mt.G if mt.M.dtype == mt.G.dtype else mt.G.to(mt.M.dtype))
+        X = torch.stack([mt.M.mT if mt.transposed else mt.M for mt in per_rank[k]], dim=0)
+        Xs.append(X)
+        Ps.append(X @ torch.stack([q.to(X.dtype) for q in Qfull], dim=0))
+    rows = [int(P.shape[1]) for P in Ps]
+    P_raw = [P.clone() for P in Ps]
+    if sum(rows) <= r:
+        full = torch.linalg.qr(torch.cat(Ps, dim=1), mode="reduced")[0].to(torch.float32)
+        offs = [sum(rows[:k]) for k in range(T)]
+        Ps = [full[:, offs[k]:offs[k] + rows[k]].contiguous() for k in range(T)]
+    else:
+        SP = None
+        for k in range(T):
+            S = torch.stack([sketch_fn(k, i, rows[k]) for i in range(real)], dim=0).to(torch.float32)
+            part = S @ Ps[k]
+            SP = part if SP is None else SP + part
+        R1 = torch.linalg.qr(SP.to(torch.float32), mode="r")[1].to(torch.float32)
+        Ps = [torch.linalg.solve_triangular(R1, P, upper=True, left=False).to(torch.float32) for P in Ps]
+        Gm = None
+        for P in Ps:
+            part = P.mT @ P
+            Gm = part if Gm is None else Gm + part
+        R2 = torch.linalg.cholesky_ex(Gm.to(torch.float32), upper=True)[0].to(torch.float32)
+        Ps = [torch.linalg.solve_triangular(R2, P, upper=True, left=False).to(torch.float32) for P in Ps]
+    R = None
+    for k in range(T):
+        part = Xs[k].mT @ Ps[k]
+        R = part if R is None else R + part
+    Qb = torch.stack(Qfull, dim=0)
+    for k in range(T):
+        for i in range(real):
+            per_rank[k][i].trace["P_raw"] = P_raw[k][i].clone()
+        _finish(per_rank[k], Xs[k], Qb, Ps[k].contiguous(), R.clone(), real, hyper, m_global, n_global,
+                q_cols=cols[k])
 
 
 def run_async_runtime(generators, max_concurrent: int = 3) -> None:

@@ -90,3 +90,21 @@ class FsCase(Case):
 
     def fs_dim(self, name):
         return next(int(d) for n, _, _, d in self.entry["mats"] if n == name)
+
+
+def tp_case_names():
+    return [c["name"] for c in manifest("manifest_tp.json")["cases"]]
+
+
+class TpCase(FsCase):
+    """A TP ("fsdp_tp") capture (make_golden_tp.py): per-rank row shards of the P side and
+    column shards of Q; shard() also carries the rank's Q columns (c0, c1)."""
+    MANIFEST = "manifest_tp.json"
+
+    def tp_dim(self, name):
+        return self.fs_dim(name)
+
+    def global_rows(self, name):
+        """m_P of the global matrix: rows (tp_shard_dim 0) or columns (1) -- the sharded side."""
+        _, m, n, dim = next(e for e in self.entry["mats"] if e[0] == name)
+        return int(m) if int(dim) == 0 else int(n)
