@@ -3766,8 +3766,6 @@ int validate(const DionBatchDesc* d) {
   if (d->m <= 0 || d->n <= 0) return fail(DION_E_INVALID, "bad shape m=%d n=%d", d->m, d->n);
   if (d->r <= 0 || d->r > 128)
     return fail(DION_E_UNSUPPORTED, "rank r=%d outside 1..128", d->r);
-  if (d->r > d->m || d->r > d->n)
-    return fail(DION_E_INVALID, "rank r=%d exceeds min(m=%d, n=%d)", d->r, d->m, d->n);
   if (d->m_dtype != DION_DTYPE_F32 && d->m_dtype != DION_DTYPE_BF16)
     return fail(DION_E_UNSUPPORTED, "momentum dtype %d", d->m_dtype);
   if (d->w_dtype != DION_DTYPE_F32) return fail(DION_E_UNSUPPORTED, "weight dtype %d", d->w_dtype);
@@ -4399,6 +4397,8 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
         n = ef_presplit_bytes(mp, d->r, chunk);
         break;
       case DION_OP_ORTHONORMALIZE: {
+        if (d->r > d->m || d->r > d->n)
+          return fail(DION_E_INVALID, "rank r=%d exceeds min(m=%d, n=%d) of a whole matrix", d->r, d->m, d->n);
         // k = ceil(oversample r / 128) * 128 is bounded by the value at oversample 2
         n = ortho_plan(mp, d->r, chunk, 2.0f).total;
         break;
@@ -4652,6 +4652,8 @@ int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, u
                         void* ws, size_t ws_bytes, dion_stream_t stream) {
   int rc = validate(d);
   if (rc != DION_OK) return rc;
+  if (d->r > d->m || d->r > d->n)
+    return fail(DION_E_INVALID, "rank r=%d exceeds min(m=%d, n=%d) of a whole matrix", d->r, d->m, d->n);
   if (P == nullptr) return fail(DION_E_INVALID, "P is null");
   if (!(oversample > 0.f)) return fail(DION_E_INVALID, "oversample=%f", oversample);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

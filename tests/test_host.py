@@ -70,8 +70,11 @@ def test_abi_rejects_bad_descriptors_without_gpu():
     assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P, ctypes.byref(nbytes)) == \
         _lib.DION_E_UNSUPPORTED
     d.m_dtype = _lib.DTYPE_F32
-    d.r = 100
-    assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P, ctypes.byref(nbytes)) == _lib.DION_E_INVALID
+    d.r = 100   # r > min(m, n): a TP row shard may have fewer rows than r, a whole matrix may not
+    assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P, ctypes.byref(nbytes)) == _lib.DION_OK
+    assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_ORTHONORMALIZE, ctypes.byref(nbytes)) == \
+        _lib.DION_E_INVALID
+    assert b"whole matrix" in lib.dion_last_error()
     d.r = 8
     assert lib.dion_workspace_bytes(ctypes.byref(d), 99, ctypes.byref(nbytes)) == _lib.DION_E_INVALID
     # null pointers are rejected before any device work
