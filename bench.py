@@ -80,7 +80,7 @@ KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("ef_apply_w", False): ("rank_stream_kernel<4, false, 8, 2>", 1),
              ("ef_apply_w", True): ("rank_stream_kernel<4, false, 8, 2>", 1),
              ("project_r", False): ("colproj_h3_kernel<4, 4, 4>", 1),
-             ("project_r", True): ("rowproj_h3_kernel<4>", 1),
+             ("project_r", True): ("rowproj_h3_kernel<4, 4>", 1),
              ("ef_apply", False): ("rank_stream_kernel<4, false, 8, 2>", 2),
              ("ef_apply", True): ("rank_stream_kernel<4, false, 8, 2>", 2)}
 

@@ -2199,6 +2199,15 @@ __device__ __forceinline__ void thin_x6_store(const ThinX6<RB>& T, bf16x8* tq, i
   }
 }
 
+// swizzle of the 32 x 8 (16-byte unit) LDS transpose tile: chunk k of row r is stored at
+// k ^ xt_swz(r).  0: (r >> 1) & 7 (conflict-free for 16 consecutive lanes on 64 banks);
+// 1: 5 (r >> 1) & 7, which also separates the two same-parity rows of every 4-row group
+// (tuning knob)
+#ifndef DION_XT_SWZ
+#define DION_XT_SWZ 0
+#endif
+__device__ __forceinline__ int xt_swz(int r) { return DION_XT_SWZ ? ((5 * (r >> 1)) & 7) : ((r >> 1) & 7); }
+
 #ifndef DION_KRBE
 #define DION_KRBE 2
 #endif
@@ -2378,14 +2387,14 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_ef_kernel(const
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = 8 * q + (lane >> 3), k = lane & 7;
-      xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[q >> 1][q & 1];
+      xw[r * 8 + (k ^ xt_swz(r))] = T.x[q >> 1][q & 1];
     }
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int r = 16 * rb + t, k = 4 * c + g;
-        T.x[rb][c] = xw[r * 8 + (k ^ ((r >> 1) & 7))];
+        T.x[rb][c] = xw[r * 8 + (k ^ xt_swz(r))];
       }
   };
   // the inverse: MFMA layout -> LDS -> whole-line non-temporal stores
@@ -2396,12 +2405,12 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_ef_kernel(const
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int r = 16 * rb + t, k = 4 * c + g;
-        xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[rb][c];
+        xw[r * 8 + (k ^ xt_swz(r))] = T.x[rb][c];
       }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = 8 * q + (lane >> 3), k = lane & 7;
-      st_stream(reinterpret_cast<f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j), xw[r * 8 + (k ^ ((r >> 1) & 7))]);
+      st_stream(reinterpret_cast<f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j), xw[r * 8 + (k ^ xt_swz(r))]);
     }
   };
   SplitCopyN<NQ, 64 * kPaNW> TA;
@@ -2708,14 +2717,14 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const 
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int r = 8 * q + (lane >> 3), k = lane & 7;
-        xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[q >> 1][q & 1];
+        xw[r * 8 + (k ^ xt_swz(r))] = T.x[q >> 1][q & 1];
       }
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
           const int r = 16 * rb + t, k = 4 * c + g;
-          T.x[rb][c] = xw[r * 8 + (k ^ ((r >> 1) & 7))];
+          T.x[rb][c] = xw[r * 8 + (k ^ xt_swz(r))];
         }
     }
   };
@@ -3264,14 +3273,14 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = 8 * q + (lane >> 3), k = lane & 7;
-      xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[q >> 1][q & 1];
+      xw[r * 8 + (k ^ xt_swz(r))] = T.x[q >> 1][q & 1];
     }
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int r = 16 * rb + t, k = 4 * c + g;
-        T.x[rb][c] = xw[r * 8 + (k ^ ((r >> 1) & 7))];
+        T.x[rb][c] = xw[r * 8 + (k ^ xt_swz(r))];
       }
   };
   auto xstore = [&](const RowStepE<GDT>& T, int j) {
@@ -3281,12 +3290,12 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int r = 16 * rb + t, k = 4 * c + g;
-        xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[rb][c];
+        xw[r * 8 + (k ^ xt_swz(r))] = T.x[rb][c];
       }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = 8 * q + (lane >> 3), k = lane & 7;
-      st_stream(reinterpret_cast<f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j), xw[r * 8 + (k ^ ((r >> 1) & 7))]);
+      st_stream(reinterpret_cast<f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j), xw[r * 8 + (k ^ xt_swz(r))]);
     }
   };
   auto compute = [&](RowStepE<GDT>& X, const f16x8* tqc, const f16x8* rsc) {
@@ -3593,12 +3602,12 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_efh3_kernel(cons
 // 16 c + 4 g .. + 3).  The streamed M is the B operand, the pre-split P the A operand
 // (one scale per matrix); with pass A's max |M| the step's products accumulate in place
 // under one scale for the matrix, else each row gets a per-step scale (as in pass A).
-template <int RB>
-__global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_h3_kernel(const ProjArgs a) {
+template <int RB, int NW>
+__global__ void __launch_bounds__(64 * NW, (RB >= 8 || NW >= 8) ? 1 : 2) rowproj_h3_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int NQ = RB * 2 * 64;
   __shared__ f16x8 tq[2][NQ];
-  __shared__ f32x4 xt[4][32 * 8];
+  __shared__ f32x4 xt[NW][32 * 8];
   const BlockXYZ blk = xcd_block();
   const int b = blk.z;
   const int kc = blk.y;
@@ -3607,7 +3616,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_h3_kernel(const 
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
-  const int row_base = blk.x * (64 * kRBE) + wave * (16 * kRBE);
+  const int row_base = blk.x * (16 * kRBE * NW) + wave * (16 * kRBE);
   const int j_begin = kc * a.kchunk;
   const int j_end = min(a.cols, j_begin + a.kchunk);
   const int j_len = j_end - j_begin;
@@ -3624,14 +3633,14 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_h3_kernel(const 
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = 8 * q + (lane >> 3), k = lane & 7;
-      xw[r * 8 + (k ^ ((r >> 1) & 7))] = T.x[q >> 1][q & 1];
+      xw[r * 8 + (k ^ xt_swz(r))] = T.x[q >> 1][q & 1];
     }
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int r = 16 * rb + t, k = 4 * c + g;
-        T.x[rb][c] = xw[r * 8 + (k ^ ((r >> 1) & 7))];
+        T.x[rb][c] = xw[r * 8 + (k ^ xt_swz(r))];
       }
   };
 
@@ -3648,7 +3657,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_h3_kernel(const 
   auto run = [&](auto FIXc) {
     constexpr bool FIX = decltype(FIXc)::value;
     RowStepE<DION_DTYPE_NONE> SA, SB;
-    SplitCopy<NQ> TA;
+    SplitCopyN<NQ, 64 * NW> TA;
     auto compute = [&](RowStepE<DION_DTYPE_NONE>& X, const f16x8* tqc) {
       Split2h Bx[kRBE];
       float invx[kRBE];
@@ -3703,31 +3712,31 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_h3_kernel(const 
       }
     };
     xload(SA, cj(j_begin));
-    split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j_begin) / 32) * NQ, tid);
-    split_copy_store<NQ>(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
+    split_copy_load_n(TA, qs + static_cast<long>(cj(j_begin) / 32) * NQ, tid);
+    split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
     __syncthreads();
     int cur = 0;
     for (int j0 = j_begin; j0 < j_end; j0 += 64) {
       const bool more = j0 + 32 < j_end;
       if (more) {
         xload(SB, cj(j0 + 32));
-        split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j0 + 32) / 32) * NQ, tid);
+        split_copy_load_n(TA, qs + static_cast<long>(cj(j0 + 32) / 32) * NQ, tid);
       }
       xpose(SA);
       compute(SA, tq[cur]);
       if (!more) break;
-      split_copy_store<NQ>(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+      split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
       __syncthreads();
       cur ^= 1;
       const bool more2 = j0 + 64 < j_end;
       if (more2) {
         xload(SA, cj(j0 + 64));
-        split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j0 + 64) / 32) * NQ, tid);
+        split_copy_load_n(TA, qs + static_cast<long>(cj(j0 + 64) / 32) * NQ, tid);
       }
       xpose(SB);
       compute(SB, tq[cur]);
       if (!more2) break;
-      split_copy_store<NQ>(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+      split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
       __syncthreads();
       cur ^= 1;
     }
@@ -3880,6 +3889,12 @@ size_t thin_presplit_bytes(int rows, int r, int batch) { return static_cast<size
 #ifndef DION_PB_H3R
 #define DION_PB_H3R 1
 #endif
+// waves per block of rowproj_h3_kernel: one LDS copy of the step's P split serves 32 NW rows
+// of M (tuning knob)
+#ifndef DION_PBR_NW
+#define DION_PBR_NW 4
+#endif
+constexpr int kPbRNW = DION_PBR_NW;
 // columns per lane of colproj_h3_kernel (2: 8-byte loads, 4: 16-byte loads; tuning knob)
 #ifndef DION_COLH3_CT
 #define DION_COLH3_CT 4
@@ -4044,8 +4059,9 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
                   (row_mode ? rows % (64 * kRBE) == 0
                             : (rows % 32 == 0 && cols % ((r >= 64 ? 32 : 64) * kColX6NW) == 0));
   const bool h3 = fast && gdt == DION_DTYPE_NONE &&
-                  (row_mode ? (DION_PB_H3R && rows % (64 * kRBE) == 0) : colh3_ok(rows, cols, r));
-  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch, (x6 || h3) ? 64 * kRBE : (fast ? 64 * kRB : 128))
+                  (row_mode ? (DION_PB_H3R && rows % (16 * kRBE * kPbRNW) == 0) : colh3_ok(rows, cols, r));
+  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch,
+                                         h3 ? 16 * kRBE * kPbRNW : x6 ? 64 * kRBE : (fast ? 64 * kRB : 128))
                  : h3      ? colh3_geo(rows, cols, batch, r)
                  : x6      ? colx6_geo(rows, cols, batch, r)
                            : colproj_geo(rows, cols, batch, false);
@@ -4135,7 +4151,7 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     return dispatch_gdt(gdt, [&](auto Gc) {
       constexpr int GD = decltype(Gc)::value;
       if (h3 && row_mode)
-        hipLaunchKernelGGL((rowproj_h3_kernel<RB>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((rowproj_h3_kernel<RB, kPbRNW>), grid, dim3(64 * kPbRNW), 0, st, a);
       else if (x6 && row_mode)
         hipLaunchKernelGGL((rowproj_x6_kernel<RB>), grid, dim3(256), 0, st, a);
       else if (h3)
