@@ -3048,11 +3048,15 @@ __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a)
 // pre-split P is the A operand (A[row j = 16 cb + t'][k]), one scale per matrix.  Each
 // step's product lands in a fresh accumulator D[j][col] (lane (t, g): R rows CT t + c,
 // r columns 16 cb + 4 g + q) and is added as acc += D / s_col.
+// r > 64 pass-B h3 kernels: the split P two cb at a time, two waves per SIMD (tuning knob)
+#ifndef DION_H3_PAIRS
+#define DION_H3_PAIRS 1
+#endif
 #ifndef DION_PBX
 #define DION_PBX 0  // dev experiments on colproj_h3_kernel's fixed-scale loop (0 = product)
 #endif
 template <int RB, int NW, int CT>
-__global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : 2) colproj_h3_kernel(const ProjArgs a) {
+__global__ void __launch_bounds__(64 * NW, (RB >= 8 && !DION_H3_PAIRS) ? 1 : 2) colproj_h3_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int NQ = RB * 2 * 64;  // f16x8 units of one K-step's P split
   __shared__ f16x8 tq[2][NQ];
@@ -3124,7 +3128,33 @@ __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : 2) colproj_h3_kernel(co
               split2h(lo4, hi4, sc, B[c]);
             }
           }
-          if constexpr (FIX) {
+          if constexpr (FIX && RB >= 8 && DION_H3_PAIRS) {
+            // r > 64: the split P of two cb at a time (all RB of them would need 64 VGPRs
+            // and push the kernel to one wave per SIMD); term by term over (c, cb pair)
+#pragma unroll
+            for (int cp = 0; cp < RB; cp += 2) {
+              Split2h A0, A1;
+              A0.hi = tq[cur][(cp * 2 + 0) * 64 + lane];
+              A0.lo = tq[cur][(cp * 2 + 1) * 64 + lane];
+              A1.hi = tq[cur][(cp * 2 + 2) * 64 + lane];
+              A1.lo = tq[cur][(cp * 2 + 3) * 64 + lane];
+#pragma unroll
+              for (int c = 0; c < CT; ++c) {
+                acc[c][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.lo, B[c].hi, acc[c][cp], 0, 0, 0);
+                acc[c][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.lo, B[c].hi, acc[c][cp + 1], 0, 0, 0);
+              }
+#pragma unroll
+              for (int c = 0; c < CT; ++c) {
+                acc[c][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.hi, B[c].lo, acc[c][cp], 0, 0, 0);
+                acc[c][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.hi, B[c].lo, acc[c][cp + 1], 0, 0, 0);
+              }
+#pragma unroll
+              for (int c = 0; c < CT; ++c) {
+                acc[c][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.hi, B[c].hi, acc[c][cp], 0, 0, 0);
+                acc[c][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.hi, B[c].hi, acc[c][cp + 1], 0, 0, 0);
+              }
+            }
+          } else if constexpr (FIX) {
             // the three products term by term over all (c, cb): consecutive MFMAs are
             // independent (a back-to-back dependent MFMA waits for its predecessor)
             Split2h A[RB];
@@ -3603,7 +3633,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_efh3_kernel(cons
 // (one scale per matrix); with pass A's max |M| the step's products accumulate in place
 // under one scale for the matrix, else each row gets a per-step scale (as in pass A).
 template <int RB, int NW>
-__global__ void __launch_bounds__(64 * NW, (RB >= 8 || NW >= 8) ? 1 : 2) rowproj_h3_kernel(const ProjArgs a) {
+__global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >= 8) ? 1 : 2) rowproj_h3_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int NQ = RB * 2 * 64;
   __shared__ f16x8 tq[2][NQ];
@@ -3673,7 +3703,32 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 || NW >= 8) ? 1 : 2) rowproj
           split2h(X.x[rb][0], X.x[rb][1], sx, Bx[rb]);
         }
       }
-      if constexpr (FIX) {
+      if constexpr (FIX && RB >= 8 && DION_H3_PAIRS) {
+        // r > 64: two cb of the split P at a time (see colproj_h3_kernel)
+#pragma unroll
+        for (int cp = 0; cp < RB; cp += 2) {
+          Split2h A0, A1;
+          A0.hi = tqc[(cp * 2 + 0) * 64 + lane];
+          A0.lo = tqc[(cp * 2 + 1) * 64 + lane];
+          A1.hi = tqc[(cp * 2 + 2) * 64 + lane];
+          A1.lo = tqc[(cp * 2 + 3) * 64 + lane];
+#pragma unroll
+          for (int rb = 0; rb < kRBE; ++rb) {
+            acc[rb][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.lo, Bx[rb].hi, acc[rb][cp], 0, 0, 0);
+            acc[rb][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.lo, Bx[rb].hi, acc[rb][cp + 1], 0, 0, 0);
+          }
+#pragma unroll
+          for (int rb = 0; rb < kRBE; ++rb) {
+            acc[rb][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.hi, Bx[rb].lo, acc[rb][cp], 0, 0, 0);
+            acc[rb][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.hi, Bx[rb].lo, acc[rb][cp + 1], 0, 0, 0);
+          }
+#pragma unroll
+          for (int rb = 0; rb < kRBE; ++rb) {
+            acc[rb][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.hi, Bx[rb].hi, acc[rb][cp], 0, 0, 0);
+            acc[rb][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.hi, Bx[rb].hi, acc[rb][cp + 1], 0, 0, 0);
+          }
+        }
+      } else if constexpr (FIX) {
         // the three products term by term: consecutive MFMAs are independent
         Split2h A[RB];
 #pragma unroll
@@ -4392,6 +4447,8 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
           if (nf > n) n = nf;
           const size_t ne = slab_bytes(rowproj_geo(d->m, d->n, chunk, 64 * kRBE), chunk, d->r);
           if (ne > n) n = ne;
+          const size_t nh = slab_bytes(rowproj_geo(d->m, d->n, chunk, 16 * kRBE * kPbRNW), chunk, d->r);
+          if (nh > n) n = nh;
         } else {
           const size_t nx = slab_bytes(colx6_geo(d->m, d->n, chunk, d->r), chunk, d->r);
           if (nx > n) n = nx;

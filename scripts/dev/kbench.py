@@ -7,7 +7,7 @@ op = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 m, n = (4096, 14336) if op.endswith("_T") else (28672, 4096)
 T = m < n
-B, r = 16 if not T else 16, 64
+B, r = 16 if not T else 16, int(os.environ.get("KB_R", "64"))  # KB_R=128: Mixtral's rank
 mp, nq = (n, m) if T else (m, n)
 dev = torch.device("cuda", 0)
 codec = HipDionCodec(dev)
