@@ -77,8 +77,8 @@ KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("project_p", True): ("colproj_fast_kernel<4, 2>", 1),
              ("project_p_ef", False): ("rowproj_efh3_kernel<4, 2, 2>", 1),
              ("project_p_ef", True): ("colproj_efh3_kernel<4, 2>", 1),
-             ("ef_apply_w", False): ("rank_stream_kernel<4, false, 8, 2>", 1),
-             ("ef_apply_w", True): ("rank_stream_kernel<4, false, 8, 2>", 1),
+             ("ef_apply_w", False): ("rank_stream_kernel<4, false, 8, 2, true>", 1),
+             ("ef_apply_w", True): ("rank_stream_kernel<4, false, 8, 2, true>", 1),
              ("project_r", False): ("colproj_h3_kernel<4, 4, 4>", 1),
              ("project_r", True): ("rowproj_h3_kernel<4, 4>", 1),
              ("ef_apply", False): ("rank_stream_kernel<4, false, 8, 2>", 2),
@@ -183,6 +183,7 @@ MFMA_WORK = (("rowproj_efh3_kernel", 2 * 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_h3_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_x6_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
              ("rowproj_x6_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
+             ("rank_stream_kernel@h3", 2 * 3, MFMA_BF16_PEAK_TFLOPS),  # <..., true>: the weight update
              ("rank_stream_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
              ("rowproj_fast_kernel", 2, MFMA_F32_PEAK_TFLOPS),
              ("colproj_fast_kernel", 2, MFMA_F32_PEAK_TFLOPS))
@@ -192,7 +193,8 @@ def mfma_of(kernel, elems, r, ms):
     """Issued MFMA TFLOP/s of one kernel over its probe time and the fraction of the dtype's
     dense peak (the split products count as issued work: that is what the matrix cores do)."""
     for fam, per, peak in MFMA_WORK:
-        if kernel.startswith(fam):
+        base, _, tag = fam.partition("@")
+        if kernel.startswith(base) and (not tag or kernel.endswith(", true>")):
             tf = per * elems * r / (ms * 1e-3) / 1e12
             return {"issued_TFLOPs": round(tf, 1), "peak_TFLOPs": peak, "util": round(tf / peak, 4)}
     return None

@@ -1678,7 +1678,43 @@ struct RankArgs {
   float scale;               // applied to the fixed factor
   float decay;               // X multiplier (1 for M)
   int skip_zero;             // 1: entries with an all-zero momentum are left untouched
+  // rank_stream_kernel<..., H3 = true> (the weight update: both factors bounded by 1 in
+  // magnitude, P orthonormal, Qn column-normalised): power-of-two h3 scales fixed by that
+  // bound instead of measured
+  float h3_fixed_mul;        // scale * s_fixed
+  float h3_stream_scale;     // s_streamed
+  float h3_inv;              // 1 / (s_fixed s_streamed)
 };
+
+// fp16x3 ("h3") split types and helpers: see the h3 section below
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+struct Split2h {
+  f16x8 hi, lo;
+};
+
+// power-of-two scale s (and 1/s) with amax * s in [2^14, 2^15); clamped to normal floats
+__device__ __forceinline__ float h3_scale(float amax, float& inv) {
+  const int be = static_cast<int>((__float_as_uint(amax) >> 23) & 0xFFu);  // biased exponent
+  int es = 127 + 14 - (be - 127);                                           // 2^(14 - e)
+  es = es < 1 ? 1 : (es > 253 ? 253 : es);  // s and inv both normal: inv == 1 / s exactly
+  inv = __uint_as_float(static_cast<uint32_t>(254 - es) << 23);
+  return __uint_as_float(static_cast<uint32_t>(es) << 23);
+}
+
+__device__ __forceinline__ void split2h(const f32x4& a, const f32x4& b, float s, Split2h& o) {
+  // x s is rounded to fp32 ONCE and both limbs come from that value: with contraction the
+  // compiler fuses x s - hi into one mixed-precision FMA on the exact product, and where
+  // the rounded product is an fp16 tie, hi and lo then disagree by an ulp of hi
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = (j < 4 ? a[j] : b[j - 4]) * s;
+    const _Float16 h = static_cast<_Float16>(x);
+    o.hi[j] = h;
+    o.lo[j] = static_cast<_Float16>(x - static_cast<float>(h));
+  }
+}
 
 struct Split3 {
   bf16x8 hi, mid, lo;
@@ -1706,6 +1742,15 @@ __device__ __forceinline__ f32x16 mfma6(const Split3& A, const Split3& B, f32x16
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.mid, B.hi, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.hi, B.mid, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.hi, B.hi, acc, 0, 0, 0);
+  return acc;
+}
+
+// D += A B on 32x32x16 fp16 with both operands h3-split (fp32 accumulate): the two small
+// cross terms first
+__device__ __forceinline__ f32x16 mfma3h32(const Split2h& A, const Split2h& B, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A.lo, B.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A.hi, B.lo, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A.hi, B.hi, acc, 0, 0, 0);
   return acc;
 }
 
@@ -1847,13 +1892,14 @@ __global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const
 // LDS layout of a step: [u][part][lane] bf16x8 (the 32x32x16 operand run of lane
 // (t, h): factor row t, columns 16 u + 8 h .. +7), conflict-free ds_read_b128.
 // ============================================================================
-template <int RU, bool ROWFIX, int NW, int D>
+template <int RU, bool ROWFIX, int NW, int D, bool H3 = false>
 __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_stream_kernel(const RankArgs a) {
   constexpr int R = 16 * RU;
   constexpr int NT = 64 * NW;
   constexpr int kGroups = RU * 64;                   // 8-value groups of one 32-row step
   constexpr int kPer = (kGroups + NT - 1) / NT;      // groups per thread
-  __shared__ bf16x8 sp[2][RU * 3 * 64];
+  constexpr int NP = H3 ? 2 : 3;                     // limbs per staged value
+  __shared__ bf16x8 sp[2][RU * NP * 64];
   const int b = blockIdx.z;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(tid >> 6));
@@ -1875,13 +1921,19 @@ __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_st
 #pragma unroll
   for (int q = 0; q < 16; ++q) voff[q] = (((q & 3) + 8 * (q >> 2) + 4 * h) * ld + t) * 4;
 
-  Split3 F[RU];
+  Split3 F[H3 ? 1 : RU];
+  Split2h FH[H3 ? RU : 1];
   if (active) {
     const float* fp = a.fixed[b] + static_cast<long>(fbase + t) * R + 8 * h;
 #pragma unroll
-    for (int u = 0; u < RU; ++u)
-      split3(*reinterpret_cast<const f32x4*>(fp + 16 * u), *reinterpret_cast<const f32x4*>(fp + 16 * u + 4),
-             a.scale, F[u]);
+    for (int u = 0; u < RU; ++u) {
+      const f32x4 lo4 = *reinterpret_cast<const f32x4*>(fp + 16 * u);
+      const f32x4 hi4 = *reinterpret_cast<const f32x4*>(fp + 16 * u + 4);
+      if constexpr (H3)
+        split2h(lo4, hi4, a.h3_fixed_mul, FH[u]);
+      else
+        split3(lo4, hi4, a.scale, F[u]);
+    }
   }
 
   // staging of one step's streamed rows: thread item g = tid + NT * it -> (u, lane') =
@@ -1905,11 +1957,18 @@ __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_st
       const int g = tid + NT * it;
       if (g < kGroups) {
         const int u = g >> 6, l = g & 63;
-        Split3 o;
-        split3(pv[it][0], pv[it][1], 1.f, o);
-        dst[(u * 3 + 0) * 64 + l] = o.hi;
-        dst[(u * 3 + 1) * 64 + l] = o.mid;
-        dst[(u * 3 + 2) * 64 + l] = o.lo;
+        if constexpr (H3) {
+          Split2h o;
+          split2h(pv[it][0], pv[it][1], a.h3_stream_scale, o);
+          dst[(u * 2 + 0) * 64 + l] = __builtin_bit_cast(bf16x8, o.hi);
+          dst[(u * 2 + 1) * 64 + l] = __builtin_bit_cast(bf16x8, o.lo);
+        } else {
+          Split3 o;
+          split3(pv[it][0], pv[it][1], 1.f, o);
+          dst[(u * 3 + 0) * 64 + l] = o.hi;
+          dst[(u * 3 + 1) * 64 + l] = o.mid;
+          dst[(u * 3 + 2) * 64 + l] = o.lo;
+        }
       }
     }
   };
@@ -1928,18 +1987,26 @@ __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_st
     for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
-      Split3 Sp;
-      Sp.hi = src[(u * 3 + 0) * 64 + lane];
-      Sp.mid = src[(u * 3 + 1) * 64 + lane];
-      Sp.lo = src[(u * 3 + 2) * 64 + lane];
-      acc = ROWFIX ? mfma6(F[u], Sp, acc) : mfma6(Sp, F[u], acc);
+      if constexpr (H3) {
+        Split2h Sp;
+        Sp.hi = __builtin_bit_cast(f16x8, src[(u * 2 + 0) * 64 + lane]);
+        Sp.lo = __builtin_bit_cast(f16x8, src[(u * 2 + 1) * 64 + lane]);
+        acc = ROWFIX ? mfma3h32(FH[u], Sp, acc) : mfma3h32(Sp, FH[u], acc);
+      } else {
+        Split3 Sp;
+        Sp.hi = src[(u * 3 + 0) * 64 + lane];
+        Sp.mid = src[(u * 3 + 1) * 64 + lane];
+        Sp.lo = src[(u * 3 + 2) * 64 + lane];
+        acc = ROWFIX ? mfma6(F[u], Sp, acc) : mfma6(Sp, F[u], acc);
+      }
     }
     const int row0 = ROWFIX ? fbase : s0;
     const int col0 = ROWFIX ? s0 : fbase;
     const int so = (row0 * ld + col0) * 4;
+    const float ainv = H3 ? a.h3_inv : 1.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const float v = T[q] * a.decay + acc[q];
+      const float v = H3 ? fmaf(acc[q], ainv, T[q] * a.decay) : T[q] * a.decay + acc[q];
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[q], so, kStreamAux);
     }
   };
@@ -2898,34 +2965,7 @@ __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : (NW >= 8 ? DION_COLX6_M
 // err by at most 2^-40 of the maximum in absolute terms.  Zero / NaN / inf maxima keep
 // s = 1 or shrink it, so NaN and inf propagate as in fp32.
 // ============================================================================
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-
-struct Split2h {
-  f16x8 hi, lo;
-};
-
-// power-of-two scale s (and 1/s) with amax * s in [2^14, 2^15); clamped to normal floats
-__device__ __forceinline__ float h3_scale(float amax, float& inv) {
-  const int be = static_cast<int>((__float_as_uint(amax) >> 23) & 0xFFu);  // biased exponent
-  int es = 127 + 14 - (be - 127);                                           // 2^(14 - e)
-  es = es < 1 ? 1 : (es > 253 ? 253 : es);  // s and inv both normal: inv == 1 / s exactly
-  inv = __uint_as_float(static_cast<uint32_t>(254 - es) << 23);
-  return __uint_as_float(static_cast<uint32_t>(es) << 23);
-}
-
-__device__ __forceinline__ void split2h(const f32x4& a, const f32x4& b, float s, Split2h& o) {
-  // x s is rounded to fp32 ONCE and both limbs come from that value: with contraction the
-  // compiler fuses x s - hi into one mixed-precision FMA on the exact product, and where
-  // the rounded product is an fp16 tie, hi and lo then disagree by an ulp of hi
-#pragma clang fp contract(off)
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float x = (j < 4 ? a[j] : b[j - 4]) * s;
-    const _Float16 h = static_cast<_Float16>(x);
-    o.hi[j] = h;
-    o.lo[j] = static_cast<_Float16>(x - static_cast<float>(h));
-  }
-}
+// (f16x8, Split2h, h3_scale and split2h are defined with the bf16x6 types above)
 
 // D += A B with both operands h3-split: the two small cross terms first
 __device__ __forceinline__ f32x4 mfma3h(const Split2h& A, const Split2h& B, f32x4 acc) {
@@ -3974,6 +4014,24 @@ Geo colh3_geo(int rows, int cols, int batch, int r) {
 }
 
 // pre-split streamed factor P (m_P x r per matrix) of the rank-update kernels
+// host twin of h3_scale: the power of two s with amax s in [2^14, 2^15) (1 for amax 0 or
+// not finite)
+float h3_scale_host(float amax) {
+  if (!(amax > 0.f) || !isfinite(amax)) return 1.f;
+  int e = 0;
+  frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1)
+  int k = 15 - e;
+  k = k < -126 ? -126 : (k > 126 ? 126 : k);
+  return ldexpf(1.f, k);
+}
+
+// the weight update's rank_stream_kernel on h3 products (3 fp16 MFMAs per product instead
+// of bf16x6's 6; tuning knob)
+#ifndef DION_RANK_H3
+#define DION_RANK_H3 1
+#endif
+constexpr bool kRankH3 = DION_RANK_H3 != 0;
+
 size_t ef_presplit_bytes(int mp, int r, int batch) { return static_cast<size_t>(mp) * r * 6 * batch; }
 
 // two pre-split operand buffers (Q and R', n_Q x r each) of dion_project_p_ef, after the slabs
@@ -5114,6 +5172,14 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
         ra.scale = pass == 0 ? a.alpha : a.beta;
         ra.decay = pass == 0 ? 1.0f : a.decay;
         ra.skip_zero = pass == 0 ? 1 : 0;
+        if (pass == 1) {
+          // h3 scales from the factors' bound |P|, |Qn| <= 1 (2 leaves headroom for rounding)
+          const float sf = h3_scale_host(2.f * fabsf(ra.scale));
+          const float ss = h3_scale_host(2.f);
+          ra.h3_fixed_mul = ra.scale * sf;
+          ra.h3_stream_scale = ss;
+          ra.h3_inv = 1.f / (sf * ss);
+        }
         auto launch = [&](auto RUc) {
           constexpr int RUv = decltype(RUc)::value;
           const int variant = pre ? 0 : rank_stream_variant();
@@ -5135,7 +5201,10 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
               constexpr int NWv = decltype(NWc)::value, Dv = decltype(Dc)::value;
               const dim3 g2(static_cast<unsigned>(ceil_div(d->n, 32 * NWv)),
                             static_cast<unsigned>(ceil_div(d->m, s_len)), grid.z);
-              hipLaunchKernelGGL((rank_stream_kernel<RUv, false, NWv, Dv>), g2, dim3(64 * NWv), 0, st, ra);
+              if (pass == 1 && kRankH3)
+                hipLaunchKernelGGL((rank_stream_kernel<RUv, false, NWv, Dv, true>), g2, dim3(64 * NWv), 0, st, ra);
+              else
+                hipLaunchKernelGGL((rank_stream_kernel<RUv, false, NWv, Dv>), g2, dim3(64 * NWv), 0, st, ra);
             };
             using I4 = std::integral_constant<int, 4>;
             using I8 = std::integral_constant<int, 8>;
