@@ -3088,6 +3088,14 @@ __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a)
 // pre-split P is the A operand (A[row j = 16 cb + t'][k]), one scale per matrix.  Each
 // step's product lands in a fresh accumulator D[j][col] (lane (t, g): R rows CT t + c,
 // r columns 16 cb + 4 g + q) and is added as acc += D / s_col.
+// pipeline depth of the r <= 64 fused pass A row kernel (tuning knob)
+#ifndef DION_PA_PD
+#define DION_PA_PD 2
+#endif
+// blocks per CU the r <= 64 pass-B row kernel is compiled for (tuning knob)
+#ifndef DION_PBR_MINB
+#define DION_PBR_MINB 2
+#endif
 // r > 64 pass-B h3 kernels: the split P two cb at a time, two waves per SIMD (tuning knob)
 #ifndef DION_H3_PAIRS
 #define DION_H3_PAIRS 1
@@ -3673,7 +3681,8 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_efh3_kernel(cons
 // (one scale per matrix); with pass A's max |M| the step's products accumulate in place
 // under one scale for the matrix, else each row gets a per-step scale (as in pass A).
 template <int RB, int NW>
-__global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >= 8) ? 1 : 2) rowproj_h3_kernel(const ProjArgs a) {
+__global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >= 8) ? 1 : (RB <= 4 ? DION_PBR_MINB : 2))
+    rowproj_h3_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int NQ = RB * 2 * 64;
   __shared__ f16x8 tq[2][NQ];
@@ -4724,7 +4733,7 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
           else if (tr)
             hipLaunchKernelGGL((colproj_ef_kernel<RB, GD>), grid, dim3(256), 0, st, e);
           else if (h3)
-            hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, 2>), grid, dim3(64 * kPaNW), 0, st, e);
+            hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, DION_PA_PD>), grid, dim3(64 * kPaNW), 0, st, e);
           else if (pa_lines())
             hipLaunchKernelGGL((rowproj_ef_kernel<RB, GD, 2, true>), grid, dim3(64 * kPaNW), 0, st, e);
           else
