@@ -41,7 +41,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 10
+#define DION_ABI_VERSION 11
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -245,10 +245,12 @@ int dion_grad_sum_sq(const DionBatchDesc* desc, const void* const* G, double* ou
 
 /*
  * The elementwise branch of MegatronDion.step (algorithm.py:247-429) for one bucket of
- * n_tensors same-hyper-parameter tensors: W fp32; exp_avg (first_moment) and exp_avg_sq
- * (second_moment) in m_dtype (DION_DTYPE_F32, or _BF16 for the speedrun's bf16 moments,
- * every foreach result then rounded to bf16 as torch does); G fp32 or bf16 (g_dtype);
- * numels[i] elements each, contiguous.
+ * n_tensors same-hyper-parameter tensors: W fp32; exp_avg (first_moment) in m1_dtype and
+ * exp_avg_sq (second_moment) in m2_dtype (Lion: exp_avg in m_dtype), each DION_DTYPE_F32 or
+ * _BF16 (the reference's independent momentum_dtype / variance_dtype, algorithm.py:308-332:
+ * every foreach result rounded to its tensor's dtype as torch does, g*g in the first
+ * moment's dtype then cast to the second's, m / denom in the promoted dtype); G fp32 or
+ * bf16 (g_dtype); numels[i] elements each, contiguous.  ABI 11 split m_dtype in two.
  * One read and one write of every tensor replaces the reference's chain of
  * torch._foreach_* passes:
  *   AdamW  elementwise_opts.py:45-80:  m = lerp(m, g, 1-b1); v = lerp(v, g*g, 1-b2);
@@ -259,9 +261,9 @@ int dion_grad_sum_sq(const DionBatchDesc* desc, const void* const* G, double* ou
  * Python doubles; step > 0 for AdamW ([DION_INVALID_ELEMENTWISE_ADAMW_STEP]).
  */
 int dion_elementwise_adamw(int32_t n_tensors, const int64_t* numels, float* const* W, const void* const* G,
-                           int32_t g_dtype, int32_t m_dtype, void* const* exp_avg, void* const* exp_avg_sq,
-                           double lr, double beta1, double beta2, double weight_decay, double eps, int32_t step,
-                           dion_stream_t stream);
+                           int32_t g_dtype, int32_t m1_dtype, int32_t m2_dtype, void* const* exp_avg,
+                           void* const* exp_avg_sq, double lr, double beta1, double beta2, double weight_decay,
+                           double eps, int32_t step, dion_stream_t stream);
 int dion_elementwise_lion(int32_t n_tensors, const int64_t* numels, float* const* W, const void* const* G,
                           int32_t g_dtype, int32_t m_dtype, void* const* exp_avg, double lr, double beta1,
                           double beta2, double weight_decay, dion_stream_t stream);

@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # DION_LIB_PATH: load another build of the same ABI (kernel-variant A/B runs during tuning)
 LIB_PATH = os.environ.get("DION_LIB_PATH") or os.path.join(HERE, "csrc", "libdion_codec.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -110,7 +110,8 @@ _SIGNATURES = {
     "dion_dortho_chol_inv": ([ctypes.c_int32, ctypes.c_int32, _P, _P, _P], ctypes.c_int),
     "dion_round_bf16": ([_P, ctypes.c_int64, _P], ctypes.c_int),
     "dion_grad_sum_sq": ([_DESC, _PP, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
-    "dion_elementwise_adamw": ([ctypes.c_int32, _P, _PP, _PP, ctypes.c_int32, ctypes.c_int32, _PP, _PP, ctypes.c_double,
+    "dion_elementwise_adamw": ([ctypes.c_int32, _P, _PP, _PP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _PP, _PP,
+                                ctypes.c_double,
                                 ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int32,
                                 _P], ctypes.c_int),
     "dion_elementwise_lion": ([ctypes.c_int32, _P, _PP, _PP, ctypes.c_int32, ctypes.c_int32, _PP, ctypes.c_double, ctypes.c_double,

@@ -361,16 +361,17 @@ class HipDionCodec:
 
     # ------------------------------------------------------------------ elementwise branch
     def _ew_lists(self, params, grads, moments):
-        mdt = moments[0][0].dtype if moments and moments[0] else torch.float32
         for t in params:
             if t.dtype != torch.float32 or not t.is_contiguous() or t.device != self.device:
                 raise RuntimeError(f"[DION_ELEMENTWISE_STATE_DTYPE_UNSUPPORTED] param {t.dtype} {tuple(t.shape)} "
                                    f"{t.device}; the elementwise kernel takes contiguous fp32 params")
-        for t in [m for ms in moments for m in ms]:
-            if t.dtype != mdt or mdt not in (torch.float32, torch.bfloat16) or not t.is_contiguous() \
-                    or t.device != self.device:
-                raise RuntimeError(f"[DION_ELEMENTWISE_STATE_DTYPE_UNSUPPORTED] moment {t.dtype} {tuple(t.shape)}; "
-                                   "moments are contiguous fp32 or bf16, one dtype per bucket")
+        for ms in moments:  # each moment list has its own dtype (momentum_dtype / variance_dtype)
+            mdt = ms[0].dtype if ms else torch.float32
+            for t in ms:
+                if t.dtype != mdt or mdt not in (torch.float32, torch.bfloat16) or not t.is_contiguous() \
+                        or t.device != self.device:
+                    raise RuntimeError(f"[DION_ELEMENTWISE_STATE_DTYPE_UNSUPPORTED] moment {t.dtype} "
+                                       f"{tuple(t.shape)}; each moment list is contiguous fp32 or bf16 of one dtype")
         by_gdt = {}
         for i, g in enumerate(grads):
             if not g.is_contiguous() or g.numel() != params[i].numel():
@@ -385,7 +386,7 @@ class HipDionCodec:
             numels = (ctypes.c_int64 * len(idx))(*[int(params[i].numel()) for i in idx])
             rc = self.lib.dion_elementwise_adamw(
                 len(idx), numels, _ptrs([params[i] for i in idx]), _ptrs([grads[i] for i in idx]), gdt,
-                _dtype_code_state(first_moments[0].dtype),
+                _dtype_code_state(first_moments[0].dtype), _dtype_code_state(second_moments[0].dtype),
                 _ptrs([first_moments[i] for i in idx]), _ptrs([second_moments[i] for i in idx]), float(lr),
                 float(beta1), float(beta2), float(weight_decay), float(epsilon), int(step), self._stream())
             _lib.check(rc, "dion_elementwise_adamw")

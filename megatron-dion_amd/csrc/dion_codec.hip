@@ -60,6 +60,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define DION_COLX6_MINB 1
 #endif
 constexpr int kStreamAux = DION_NT ? 2 : 0;  // buffer-op cache-policy bits (nt)
+// streaming projection kernels: issue the next step's split-operand staging loads before the big
+// operand's prefetch, so the wait before the LDS store retires only the split and the
+// prefetch stays in flight across the barrier (tuning knob)
+#ifndef DION_SPLIT_FIRST
+#define DION_SPLIT_FIRST 0
+#endif
 
 template <typename T>
 __device__ __forceinline__ T ld_stream(const T* p) {
@@ -2687,9 +2693,10 @@ __global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) 
   for (int i0 = i_begin; i0 < i_end; i0 += 64) {
     const bool more = i0 + 32 < i_end;
     if (more) {
-      cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
+      if (!DION_SPLIT_FIRST) cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
       split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 1) * NQ, tid);
       if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 1) * NR, tid);
+      if (DION_SPLIT_FIRST) cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
     }
     cpe_compute<RB, GDT>(SA, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, i0, lane, nzb);
     if (!more) break;
@@ -2699,9 +2706,10 @@ __global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) 
     cur ^= 1;
     const bool more2 = i0 + 64 < i_end;
     if (more2) {
-      cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
+      if (!DION_SPLIT_FIRST) cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
       split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 2) * NQ, tid);
       if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 2) * NR, tid);
+      if (DION_SPLIT_FIRST) cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
     }
     cpe_compute<RB, GDT>(SB, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, i0 + 32, lane, nzb);
     if (!more2) break;
@@ -3151,8 +3159,9 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !DION_H3_PAIRS) ? 1 : 2) 
         const int i = i0 + 32 * k;
         if (i >= i_end) break;
         const bool more = i + 32 < i_end;
+        if (DION_SPLIT_FIRST && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
         if (i + 32 * (PD - 1) < i_end) cpx_load<CT>(S[(k + PD - 1) % PD], M, a.ld_m, i + 32 * (PD - 1));
-        if (more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
+        if (!DION_SPLIT_FIRST && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
         {
           const ColStepX6<CT>& X = S[k];
           Split2h B[CT];
@@ -3457,11 +3466,12 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
       const int j = j0 + 32 * k;
       if (j >= j_end) break;
       const bool more = j + 32 < j_end;
-      if (j + 32 * (PD - 1) < j_end) xload(S[(k + PD - 1) % PD], j + 32 * (PD - 1));
+      if (!DION_SPLIT_FIRST && j + 32 * (PD - 1) < j_end) xload(S[(k + PD - 1) % PD], j + 32 * (PD - 1));
       if (more) {
         split_copy_load_n(TA, qs + static_cast<long>((j + 32) / 32) * NQ, tid);
         if (has_ef) split_copy_load_n(EA, rsp + static_cast<long>((j + 32) / 32) * NR, tid);
       }
+      if (DION_SPLIT_FIRST && j + 32 * (PD - 1) < j_end) xload(S[(k + PD - 1) % PD], j + 32 * (PD - 1));
       xpose(S[k]);
       compute(S[k], tq[cur], rs[cur]);
       xstore(S[k], j);
@@ -3635,9 +3645,10 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_efh3_kernel(cons
   for (int i0 = i_begin; i0 < i_end; i0 += 64) {
     const bool more = i0 + 32 < i_end;
     if (more) {
-      cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
+      if (!DION_SPLIT_FIRST) cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
       split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 1) * NQ, tid);
       if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 1) * NR, tid);
+      if (DION_SPLIT_FIRST) cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
     }
     compute(SA, tq[cur], rs[cur], i0);
     if (!more) break;
@@ -3647,9 +3658,10 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_efh3_kernel(cons
     cur ^= 1;
     const bool more2 = i0 + 64 < i_end;
     if (more2) {
-      cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
+      if (!DION_SPLIT_FIRST) cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
       split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 2) * NQ, tid);
       if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 2) * NR, tid);
+      if (DION_SPLIT_FIRST) cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
     }
     compute(SB, tq[cur], rs[cur], i0 + 32);
     if (!more2) break;
@@ -3823,8 +3835,9 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >=
     for (int j0 = j_begin; j0 < j_end; j0 += 64) {
       const bool more = j0 + 32 < j_end;
       if (more) {
-        xload(SB, cj(j0 + 32));
+        if (!DION_SPLIT_FIRST) xload(SB, cj(j0 + 32));
         split_copy_load_n(TA, qs + static_cast<long>(cj(j0 + 32) / 32) * NQ, tid);
+        if (DION_SPLIT_FIRST) xload(SB, cj(j0 + 32));
       }
       xpose(SA);
       compute(SA, tq[cur]);
@@ -3834,8 +3847,9 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >=
       cur ^= 1;
       const bool more2 = j0 + 64 < j_end;
       if (more2) {
-        xload(SA, cj(j0 + 64));
+        if (!DION_SPLIT_FIRST) xload(SA, cj(j0 + 64));
         split_copy_load_n(TA, qs + static_cast<long>(cj(j0 + 64) / 32) * NQ, tid);
+        if (DION_SPLIT_FIRST) xload(SA, cj(j0 + 64));
       }
       xpose(SB);
       compute(SB, tq[cur]);
@@ -5302,13 +5316,14 @@ int dion_grad_sum_sq(const DionBatchDesc* d, const void* const* G, double* out, 
 // the host-side scalars follow the reference's Python doubles (elementwise_opts.py:64-78,
 // 98-104): bias corrections and 1 - lr wd in double, cast to fp32 once
 int dion_elementwise_adamw(int32_t n_tensors, const int64_t* numels, float* const* W, const void* const* G,
-                           int32_t g_dtype, int32_t m_dtype, void* const* exp_avg, void* const* exp_avg_sq, double lr,
-                           double beta1, double beta2, double weight_decay, double eps, int32_t step,
-                           dion_stream_t stream) {
+                           int32_t g_dtype, int32_t m1_dtype, int32_t m2_dtype, void* const* exp_avg,
+                           void* const* exp_avg_sq, double lr, double beta1, double beta2, double weight_decay,
+                           double eps, int32_t step, dion_stream_t stream) {
   if (step <= 0) return fail(DION_E_INVALID, "[DION_INVALID_ELEMENTWISE_ADAMW_STEP] step=%d", step);
   const double bc1 = 1.0 - pow(beta1, step);
   const double bc2 = 1.0 - pow(beta2, step);
-  return ew::run(n_tensors, numels, W, G, g_dtype, m_dtype, exp_avg, exp_avg_sq, false, static_cast<float>(1.0 - beta1),
+  return ew::run(n_tensors, numels, W, G, g_dtype, m1_dtype, m2_dtype, exp_avg, exp_avg_sq, false,
+                 static_cast<float>(1.0 - beta1),
                  static_cast<float>(1.0 - beta2), static_cast<float>(sqrt(bc2)), static_cast<float>(eps),
                  static_cast<float>(lr / bc1), static_cast<float>(1.0 - lr * weight_decay), weight_decay != 0.0,
                  reinterpret_cast<hipStream_t>(stream));
@@ -5317,7 +5332,7 @@ int dion_elementwise_adamw(int32_t n_tensors, const int64_t* numels, float* cons
 int dion_elementwise_lion(int32_t n_tensors, const int64_t* numels, float* const* W, const void* const* G,
                           int32_t g_dtype, int32_t m_dtype, void* const* exp_avg, double lr, double beta1, double beta2,
                           double weight_decay, dion_stream_t stream) {
-  return ew::run(n_tensors, numels, W, G, g_dtype, m_dtype, exp_avg, nullptr, true, static_cast<float>(1.0 - beta1),
+  return ew::run(n_tensors, numels, W, G, g_dtype, m_dtype, m_dtype, exp_avg, nullptr, true, static_cast<float>(1.0 - beta1),
                  static_cast<float>(1.0 - beta2), 1.0f, 0.0f, static_cast<float>(lr),
                  static_cast<float>(1.0 - lr * weight_decay), weight_decay != 0.0, reinterpret_cast<hipStream_t>(stream));
 }

@@ -56,8 +56,10 @@ __device__ __forceinline__ void st_moment(void* p, long i, float v) {
   else static_cast<float*>(p)[i] = v;
 }
 
-template <int GDT, int MDT, bool LION>
+template <int GDT, int M1, int M2, bool LION>
 __global__ void __launch_bounds__(256) elementwise_kernel(const EwArgs a) {
+  // torch's type promotion of first_moments / denom: bf16 only when both moments are bf16
+  constexpr int UDT = (M1 == DION_DTYPE_BF16 && M2 == DION_DTYPE_BF16) ? DION_DTYPE_BF16 : DION_DTYPE_F32;
   const int b = blockIdx.y;
   const long n = a.numel[b];
   float* __restrict__ W = a.w[b];
@@ -65,28 +67,29 @@ __global__ void __launch_bounds__(256) elementwise_kernel(const EwArgs a) {
     float g;
     if constexpr (GDT == DION_DTYPE_BF16) g = bf16_to_f32(static_cast<const uint16_t*>(a.g[b])[i]);
     else g = static_cast<const float*>(a.g[b])[i];
-    g = rnd<MDT>(g);  // grad.to(first_moment.dtype)
+    g = rnd<M1>(g);  // grad.to(first_moment.dtype)
     float w = W[i];
-    const float m = ld_moment<MDT>(a.m1[b], i);
+    const float m = ld_moment<M1>(a.m1[b], i);
     if constexpr (LION) {
       // elementwise_opts.py:88-105
-      float u = torch_sign(rnd<MDT>(torch_lerp(m, g, a.lerp1)));
-      st_moment<MDT>(a.m1[b], i, torch_lerp(m, g, a.lerp2));
-      u = rnd<MDT>(u * a.step_size);
+      float u = torch_sign(rnd<M1>(torch_lerp(m, g, a.lerp1)));
+      st_moment<M1>(a.m1[b], i, torch_lerp(m, g, a.lerp2));
+      u = rnd<M1>(u * a.step_size);
       if (a.has_decay) w = w * a.decay;
       W[i] = w - u;
     } else {
-      // elementwise_opts.py:45-80
-      const float m_new = rnd<MDT>(torch_lerp(m, g, a.lerp1));
-      const float gsq = rnd<MDT>(g * g);
-      const float v_new = rnd<MDT>(torch_lerp(ld_moment<MDT>(a.m2[b], i), gsq, a.lerp2));
-      st_moment<MDT>(a.m1[b], i, m_new);
-      st_moment<MDT>(a.m2[b], i, v_new);
-      float denom = rnd<MDT>(sqrtf(v_new));
-      denom = rnd<MDT>(denom / a.bc2_sqrt);
-      denom = rnd<MDT>(denom + a.eps);
-      float u = rnd<MDT>(m_new / denom);
-      u = rnd<MDT>(u * a.step_size);
+      // elementwise_opts.py:45-80: the first moment's ops in its dtype, the squared
+      // gradient cast to the second moment's dtype, the denominator in that dtype
+      const float m_new = rnd<M1>(torch_lerp(m, g, a.lerp1));
+      const float gsq = rnd<M2>(rnd<M1>(g * g));
+      const float v_new = rnd<M2>(torch_lerp(ld_moment<M2>(a.m2[b], i), gsq, a.lerp2));
+      st_moment<M1>(a.m1[b], i, m_new);
+      st_moment<M2>(a.m2[b], i, v_new);
+      float denom = rnd<M2>(sqrtf(v_new));
+      denom = rnd<M2>(denom / a.bc2_sqrt);
+      denom = rnd<M2>(denom + a.eps);
+      float u = rnd<UDT>(m_new / denom);
+      u = rnd<UDT>(u * a.step_size);
       if (a.has_decay) w = w * a.decay;
       W[i] = w - u;
     }
@@ -97,14 +100,16 @@ __global__ void __launch_bounds__(256) elementwise_kernel(const EwArgs a) {
 
 namespace ew {
 
-int run(int n_tensors, const int64_t* numels, float* const* W, const void* const* G, int g_dtype, int m_dtype,
-        void* const* m1, void* const* m2, bool lion, float lerp1, float lerp2, float bc2_sqrt, float eps, float step_size,
+int run(int n_tensors, const int64_t* numels, float* const* W, const void* const* G, int g_dtype, int m1_dtype,
+        int m2_dtype, void* const* m1, void* const* m2, bool lion, float lerp1, float lerp2, float bc2_sqrt, float eps, float step_size,
         float decay, int has_decay, hipStream_t st) {
   if (n_tensors < 0) return fail(DION_E_INVALID, "n_tensors=%d", n_tensors);
   if (n_tensors > 0 && (numels == nullptr || W == nullptr || G == nullptr || m1 == nullptr || (!lion && m2 == nullptr)))
     return fail(DION_E_INVALID, "null argument");
   if (g_dtype != DION_DTYPE_F32 && g_dtype != DION_DTYPE_BF16) return fail(DION_E_UNSUPPORTED, "grad dtype %d", g_dtype);
-  if (m_dtype != DION_DTYPE_F32 && m_dtype != DION_DTYPE_BF16) return fail(DION_E_UNSUPPORTED, "moment dtype %d", m_dtype);
+  if (m1_dtype != DION_DTYPE_F32 && m1_dtype != DION_DTYPE_BF16) return fail(DION_E_UNSUPPORTED, "moment dtype %d", m1_dtype);
+  if (!lion && m2_dtype != DION_DTYPE_F32 && m2_dtype != DION_DTYPE_BF16)
+    return fail(DION_E_UNSUPPORTED, "second moment dtype %d", m2_dtype);
   for (int t0 = 0; t0 < n_tensors; t0 += MAXB) {
     const int nt = n_tensors - t0 < MAXB ? n_tensors - t0 : MAXB;
     EwArgs a;
@@ -131,18 +136,24 @@ int run(int n_tensors, const int64_t* numels, float* const* W, const void* const
     long gx = ceil_div(maxn, 256 * 4);
     if (gx > 2048) gx = 2048;
     const dim3 grid(static_cast<unsigned>(gx), nt);
-    auto launch = [&](auto Gc, auto Mc) {
-      constexpr int GD = decltype(Gc)::value, MD = decltype(Mc)::value;
-      if (lion) hipLaunchKernelGGL((elementwise_kernel<GD, MD, true>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((elementwise_kernel<GD, MD, false>), grid, dim3(256), 0, st, a);
+    auto launch = [&](auto Gc, auto M1c, auto M2c) {
+      constexpr int GD = decltype(Gc)::value, MD1 = decltype(M1c)::value, MD2 = decltype(M2c)::value;
+      if (lion) hipLaunchKernelGGL((elementwise_kernel<GD, MD1, MD1, true>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((elementwise_kernel<GD, MD1, MD2, false>), grid, dim3(256), 0, st, a);
     };
     using F32 = std::integral_constant<int, DION_DTYPE_F32>;
     using B16 = std::integral_constant<int, DION_DTYPE_BF16>;
-    if (g_dtype == DION_DTYPE_BF16) {
-      if (m_dtype == DION_DTYPE_BF16) launch(B16{}, B16{}); else launch(B16{}, F32{});
-    } else {
-      if (m_dtype == DION_DTYPE_BF16) launch(F32{}, B16{}); else launch(F32{}, F32{});
-    }
+    auto with_m2 = [&](auto Gc, auto M1c) {
+      if (!lion && m2_dtype != m1_dtype) {
+        if (m2_dtype == DION_DTYPE_BF16) launch(Gc, M1c, B16{}); else launch(Gc, M1c, F32{});
+      } else {
+        launch(Gc, M1c, M1c);
+      }
+    };
+    auto with_m1 = [&](auto Gc) {
+      if (m1_dtype == DION_DTYPE_BF16) with_m2(Gc, B16{}); else with_m2(Gc, F32{});
+    };
+    if (g_dtype == DION_DTYPE_BF16) with_m1(B16{}); else with_m1(F32{});
     const int rc = check_launch(lion ? "elementwise(lion)" : "elementwise(adamw)");
     if (rc != DION_OK) return rc;
   }

@@ -29,6 +29,11 @@ CASES = [
          gdtype="float32", state_dtype="bfloat16"),
     dict(name="e5_lion_bf16_moments", opt="lion", betas=(0.9, 0.99), wd=0.1, lr=0.003, eps=1e-8,
          gdtype="bfloat16", state_dtype="bfloat16"),
+    # independent momentum_dtype / variance_dtype (algorithm.py:308-332)
+    dict(name="e6_adamw_bf16m_f32v", opt="adam", betas=(0.9, 0.95), wd=0.01, lr=0.01, eps=1e-8,
+         gdtype="bfloat16", state_dtype="bfloat16", variance_dtype="float32"),
+    dict(name="e7_adamw_f32m_bf16v", opt="adam", betas=(0.8, 0.99), wd=0.05, lr=0.01, eps=1e-6,
+         gdtype="float32", state_dtype="float32", variance_dtype="bfloat16"),
 ]
 TENSORS = [("ln", (64,)), ("emb", (40, 24)), ("bias", (33,)), ("head", (17, 96))]
 STEPS = 3
@@ -41,7 +46,8 @@ def run_case(case):
     gen = torch.Generator().manual_seed(7)
     params = {n: torch.nn.Parameter(torch.randn(*s, generator=gen) * 0.02) for n, s in TENSORS}
     sdt = getattr(torch, case.get("state_dtype", "float32"))
-    mpc = DionMixedPrecisionConfig(momentum_dtype=sdt, q_dtype=sdt, variance_dtype=sdt) \
+    vdt = getattr(torch, case.get("variance_dtype", case.get("state_dtype", "float32")))
+    mpc = DionMixedPrecisionConfig(momentum_dtype=sdt, q_dtype=sdt, variance_dtype=vdt) \
         if case.get("state_dtype") else None
     opt = MegatronDion(list(params.values()), lr=case["lr"], weight_decay=case["wd"], betas=case["betas"],
                        elementwise_eps=case["eps"], elementwise_optimizer=case["opt"], mixed_precision_config=mpc)

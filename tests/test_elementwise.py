@@ -51,8 +51,9 @@ def test_oracle_matches_reference_elementwise(name):
     names = [n for n, _ in man["tensors"]]
     W = [arr[f"s0_{n}_W0"].clone() for n in names]
     sdt = getattr(torch, case.get("state_dtype", "float32"))
+    vdt = getattr(torch, case.get("variance_dtype", case.get("state_dtype", "float32")))
     m1 = [torch.zeros_like(w, dtype=sdt) for w in W]
-    m2 = [torch.zeros_like(w, dtype=sdt) for w in W]
+    m2 = [torch.zeros_like(w, dtype=vdt) for w in W]
     b1, b2 = case["betas"]
     for step in range(man["steps"]):
         G = [arr[f"s{step}_{n}_G"].to(getattr(torch, case["gdtype"])) for n in names]
@@ -74,7 +75,8 @@ def run_through_optimizer(name, dev, codec=None):
     names = [n for n, _ in man["tensors"]]
     params = {n: torch.nn.Parameter(arr[f"s0_{n}_W0"].clone().to(dev)) for n in names}
     sdt = getattr(torch, case.get("state_dtype", "float32"))
-    mpc = mda.DionMixedPrecisionConfig(momentum_dtype=sdt, q_dtype=sdt, variance_dtype=sdt) \
+    vdt = getattr(torch, case.get("variance_dtype", case.get("state_dtype", "float32")))
+    mpc = mda.DionMixedPrecisionConfig(momentum_dtype=sdt, q_dtype=sdt, variance_dtype=vdt) \
         if case.get("state_dtype") else None
     opt = mda.MegatronDion(list(params.values()), lr=case["lr"], weight_decay=case["wd"], betas=tuple(case["betas"]),
                            elementwise_eps=case["eps"], elementwise_optimizer=case["opt"], codec=codec,
