@@ -63,8 +63,12 @@ constexpr int kStreamAux = DION_NT ? 2 : 0;  // buffer-op cache-policy bits (nt)
 // streaming projection kernels: issue the next step's split-operand staging loads before the big
 // operand's prefetch, so the wait before the LDS store retires only the split and the
 // prefetch stays in flight across the barrier (tuning knob)
+// (pass A kernels; _B: the pass-B kernels, measured neutral there)
 #ifndef DION_SPLIT_FIRST
-#define DION_SPLIT_FIRST 0
+#define DION_SPLIT_FIRST 1
+#endif
+#ifndef DION_SPLIT_FIRST_B
+#define DION_SPLIT_FIRST_B 0
 #endif
 
 template <typename T>
@@ -3159,9 +3163,9 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !DION_H3_PAIRS) ? 1 : 2) 
         const int i = i0 + 32 * k;
         if (i >= i_end) break;
         const bool more = i + 32 < i_end;
-        if (DION_SPLIT_FIRST && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
+        if (DION_SPLIT_FIRST_B && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
         if (i + 32 * (PD - 1) < i_end) cpx_load<CT>(S[(k + PD - 1) % PD], M, a.ld_m, i + 32 * (PD - 1));
-        if (!DION_SPLIT_FIRST && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
+        if (!DION_SPLIT_FIRST_B && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
         {
           const ColStepX6<CT>& X = S[k];
           Split2h B[CT];
@@ -3835,9 +3839,9 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >=
     for (int j0 = j_begin; j0 < j_end; j0 += 64) {
       const bool more = j0 + 32 < j_end;
       if (more) {
-        if (!DION_SPLIT_FIRST) xload(SB, cj(j0 + 32));
+        if (!DION_SPLIT_FIRST_B) xload(SB, cj(j0 + 32));
         split_copy_load_n(TA, qs + static_cast<long>(cj(j0 + 32) / 32) * NQ, tid);
-        if (DION_SPLIT_FIRST) xload(SB, cj(j0 + 32));
+        if (DION_SPLIT_FIRST_B) xload(SB, cj(j0 + 32));
       }
       xpose(SA);
       compute(SA, tq[cur]);
@@ -3847,9 +3851,9 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >=
       cur ^= 1;
       const bool more2 = j0 + 64 < j_end;
       if (more2) {
-        if (!DION_SPLIT_FIRST) xload(SA, cj(j0 + 64));
+        if (!DION_SPLIT_FIRST_B) xload(SA, cj(j0 + 64));
         split_copy_load_n(TA, qs + static_cast<long>(cj(j0 + 64) / 32) * NQ, tid);
-        if (DION_SPLIT_FIRST) xload(SA, cj(j0 + 64));
+        if (DION_SPLIT_FIRST_B) xload(SA, cj(j0 + 64));
       }
       xpose(SB);
       compute(SB, tq[cur]);
