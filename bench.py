@@ -92,8 +92,8 @@ KERNEL_OF_BF16 = {("project_p", False): ("b16_proj_kernel<false, 4, 2>", 1),
                   ("project_p", True): ("b16_proj_kernel<true, 4, 2>", 1),
                   ("project_r", False): ("b16_proj_kernel<true, 4, 0>", 1),
                   ("project_r", True): ("b16_proj_kernel<false, 4, 0>", 1),
-                  ("ef_apply", False): ("b16_update_kernel<2>", 1),
-                  ("ef_apply", True): ("b16_update_kernel<2>", 1)}
+                  ("ef_apply", False): ("b16_stream_kernel<4, 8, false>", 1),
+                  ("ef_apply", True): ("b16_stream_kernel<4, 8, true>", 1)}
 
 
 class TimedCodec:

@@ -392,8 +392,187 @@ __global__ void __launch_bounds__(256) b16_update_kernel(const B16UpdArgs a) {
   }
 }
 
+// The same update in rank_stream_kernel's geometry (dion_codec.hip): NW-wave blocks, a
+// wave owns a 32-column strip of the storage and walks 32-row steps; the column factors
+// of the strip sit in registers (bf16, v_mfma_f32_32x32x16_bf16 B operand), the step's
+// row factors are converted to bf16 once per block into LDS (A operand); M (bf16) and W
+// (fp32) move as 32 x 32 tiles in the accumulator layout with nt buffer loads / stores
+// (a W load instruction is two whole 128-B rows), two tiles in flight.  Same per-element
+// arithmetic as b16_update_kernel; the fp32 sums of the bf16 products run in the 32x32
+// MFMA's order.  TR (transposed storage): RF_u = R, RF_w = Qn (two staged factors),
+// CF_u = CF_w = P (one register factor); otherwise RF_u = RF_w = P, CF_u = R, CF_w = Qn.
+struct B16StreamArgs {
+  uint16_t* m[MAXB];
+  float* w[MAXB];
+  const void* cf_u[MAXB];
+  const void* cf_w[MAXB];
+  const void* rf_u[MAXB];
+  const void* rf_w[MAXB];
+  int cfw_bf16, rfw_bf16;  // Qn is the bf16 Q tensor; P and R are fp32 buffers of bf16 values
+  int rows, cols, r, s_len;
+  long ld_m, ld_w;
+  float alpha, beta, decay;
+};
+
+// 8 consecutive factor values (row `row`, columns c0 .. c0 + 7) as bf16 (exact: bf16 values)
+__device__ __forceinline__ bf16x8s b16_run8(const void* base, bool is_bf16, long idx) {
+  if (is_bf16) return *reinterpret_cast<const bf16x8s*>(static_cast<const uint16_t*>(base) + idx);
+  const f32x4 x0 = *reinterpret_cast<const f32x4*>(static_cast<const float*>(base) + idx);
+  const f32x4 x1 = *reinterpret_cast<const f32x4*>(static_cast<const float*>(base) + idx + 4);
+  bf16x8s v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = static_cast<short>(f32_to_bf16_rne(x0[e]));
+    v[4 + e] = static_cast<short>(f32_to_bf16_rne(x1[e]));
+  }
+  return v;
+}
+
+template <int RU, int NW, bool TR>
+__global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) b16_stream_kernel(const B16StreamArgs a) {
+  constexpr int NT = 64 * NW;
+  constexpr int NF = TR ? 2 : 1;                 // staged row factors
+  constexpr int kGroups = NF * RU * 64;          // 8-value groups of one 32-row step
+  constexpr int kPer = (kGroups + NT - 1) / NT;
+  __shared__ bf16x8s sp[2][NF * RU * 64];
+  const int b = blockIdx.z;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(tid >> 6));
+  const int lane = tid & 63;
+  const int t = lane & 31;
+  const int h = lane >> 5;
+  const int R = a.r;
+  const int fbase = blockIdx.x * (32 * NW) + wave * 32;
+  const bool active = fbase < a.cols;
+  const int s_begin = blockIdx.y * a.s_len;
+  const int s_end = min(a.rows, s_begin + a.s_len);
+  uint16_t* M = a.m[b];
+  float* W = a.w[b];
+  const bool has_m = M != nullptr, has_w = W != nullptr;
+  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(
+      has_m ? static_cast<void*>(M) : static_cast<void*>(W), static_cast<short>(0),
+      static_cast<int>(min(static_cast<long>(a.rows) * a.ld_m * 2, 0x7FFFFFF0L)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      has_w ? static_cast<void*>(W) : static_cast<void*>(M), static_cast<short>(0),
+      static_cast<int>(min(static_cast<long>(a.rows) * a.ld_w * 4, 0x7FFFFFF0L)), 0x00020000);
+  int vrow[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) vrow[q] = (q & 3) + 8 * (q >> 2) + 4 * h;
+
+  // column factors of this lane's column fbase + t: k-run 16 u + 8 h .. + 7
+  bf16x8s Fu[RU], Fw[TR ? 1 : RU];
+  if (active) {
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const long idx = static_cast<long>(fbase + t) * R + 16 * u + 8 * h;
+      if (TR || has_m) Fu[u] = b16_run8(a.cf_u[b], false, idx);  // R or P: fp32 buffers
+      if constexpr (!TR) {
+        if (has_w) Fw[u] = b16_run8(a.cf_w[b], a.cfw_bf16 != 0, idx);
+      }
+    }
+  }
+  // staging of one step's row factors: item g -> (f, u, l): factor f, row s0 + l % 32,
+  // columns 16 u + 8 (l / 32) .. + 7
+  bf16x8s pv[kPer];
+  auto p_load = [&](int s0) {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int g = tid + NT * it;
+      if (g < kGroups) {
+        const int f = g / (RU * 64), rem = g - f * RU * 64;
+        const int u = rem >> 6, l = rem & 63;
+        const long idx = static_cast<long>(s0 + (l & 31)) * R + 16 * u + 8 * (l >> 5);
+        pv[it] = (f == 0) ? b16_run8(a.rf_u[b], false, idx) : b16_run8(a.rf_w[b], a.rfw_bf16 != 0, idx);
+      }
+    }
+  };
+  auto p_store = [&](bf16x8s* dst) {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int g = tid + NT * it;
+      if (g < kGroups) dst[g] = pv[it];
+    }
+  };
+  struct Tile {
+    float w[16];
+    uint32_t m[16];
+  };
+  Tile X[2];
+  auto x_load = [&](int s0, Tile& T) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int row = s0 + vrow[q];
+      if (has_m)
+        T.m[q] = __builtin_amdgcn_raw_buffer_load_b16(rm, static_cast<int>((static_cast<long>(row) * a.ld_m + fbase + t) * 2), 0,
+                                                      kStreamAux);
+      if (has_w)
+        T.w[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rw, static_cast<int>((static_cast<long>(row) * a.ld_w + fbase + t) * 4), 0, kStreamAux));
+    }
+  };
+  auto compute_store = [&](int s0, const Tile& T, const bf16x8s* src) {
+    if (has_m) {
+      f32x16 acc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+      for (int u = 0; u < RU; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+          __builtin_bit_cast(bf16x8, src[u * 64 + lane]), __builtin_bit_cast(bf16x8, Fu[u]), acc, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint16_t v = b16_ef(static_cast<uint16_t>(T.m[q]), acc[q], a.alpha);
+        __builtin_amdgcn_raw_buffer_store_b16(v, rm, static_cast<int>((static_cast<long>(s0 + vrow[q]) * a.ld_m + fbase + t) * 2),
+                                              0, kStreamAux);
+      }
+    }
+    if (has_w) {
+      f32x16 acc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+      for (int u = 0; u < RU; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+          __builtin_bit_cast(bf16x8, src[((TR ? 1 : 0) * RU + u) * 64 + lane]),
+          __builtin_bit_cast(bf16x8, TR ? Fu[u] : Fw[TR ? 0 : u]), acc, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float v = fmaf(a.beta, bf16_round(acc[q]), T.w[q] * a.decay);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rw,
+                                              static_cast<int>((static_cast<long>(s0 + vrow[q]) * a.ld_w + fbase + t) * 4), 0,
+                                              kStreamAux);
+      }
+    }
+  };
+
+  p_load(s_begin);
+  if (active) x_load(s_begin, X[0]);
+  p_store(sp[0]);
+  __syncthreads();
+  int cur = 0;
+  for (int s0 = s_begin; s0 < s_end; s0 += 64) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int s = s0 + 32 * k;
+      if (s >= s_end) break;
+      const bool more = s + 32 < s_end;
+      if (more) p_load(s + 32);
+      if (active && more) x_load(s + 32, X[k ^ 1]);
+      if (active) compute_store(s, X[k], sp[cur]);
+      if (!more) break;
+      p_store(sp[cur ^ 1]);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- host side
 namespace b16 {
+
+// the update on b16_stream_kernel (rank-stream geometry) where the shapes allow (tuning knob)
+#ifndef DION_B16_STREAM
+#define DION_B16_STREAM 1
+#endif
+constexpr bool kB16Stream = DION_B16_STREAM != 0;
 
 
 int rpad_of(int r) { return (r + 15) / 16 * 16; }
@@ -524,6 +703,61 @@ int update(const DionBatchDesc* d, uint16_t* const* M, float* const* W, const fl
   const int r = d->r;
   for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
     const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    if (kB16Stream && d->m % 32 == 0 && d->n % 32 == 0 && r % 16 == 0 && r <= 128) {
+      // the rank-stream geometry (b16_stream_kernel)
+      B16StreamArgs sa;
+      memset(&sa, 0, sizeof(sa));
+      bool ok = (reinterpret_cast<uintptr_t>(P) & 15u) == 0 && (reinterpret_cast<uintptr_t>(R) & 15u) == 0;
+      for (int b = 0; b < nb && ok; ++b) {
+        const float* Pb = P + static_cast<long>(b0 + b) * mp * r;
+        const float* Rb = R + static_cast<long>(b0 + b) * nq * r;
+        sa.m[b] = M ? M[b0 + b] : nullptr;
+        sa.w[b] = W ? W[b0 + b] : nullptr;
+        if ((M && sa.m[b] == nullptr) || (W && sa.w[b] == nullptr) || Qn[b0 + b] == nullptr)
+          return fail(DION_E_INVALID, "null pointer at entry %d", b0 + b);
+        ok = (reinterpret_cast<uintptr_t>(Qn[b0 + b]) & 15u) == 0;
+        if (!d->transposed) {
+          sa.rf_u[b] = Pb; sa.rf_w[b] = Pb; sa.cf_u[b] = Rb; sa.cf_w[b] = Qn[b0 + b];
+        } else {
+          sa.rf_u[b] = Rb; sa.rf_w[b] = Qn[b0 + b]; sa.cf_u[b] = Pb; sa.cf_w[b] = Pb;
+        }
+      }
+      if (ok) {
+        sa.cfw_bf16 = d->transposed ? 0 : 1;
+        sa.rfw_bf16 = d->transposed ? 1 : 0;
+        sa.rows = d->m;
+        sa.cols = d->n;
+        sa.r = r;
+        sa.s_len = 512;
+        sa.ld_m = ldv(d->ld_m, d->n);
+        sa.ld_w = ldv(d->ld_w, d->n);
+        sa.alpha = alpha;
+        sa.beta = beta;
+        sa.decay = decay;
+        constexpr int NW = 8;
+        const dim3 grid(static_cast<unsigned>(ceil_div(d->n, 32 * NW)), static_cast<unsigned>(ceil_div(d->m, sa.s_len)), nb);
+        auto go = [&](auto RUc) {
+          constexpr int RU = decltype(RUc)::value;
+          if (d->transposed)
+            hipLaunchKernelGGL((b16_stream_kernel<RU, NW, true>), grid, dim3(64 * NW), 0, st, sa);
+          else
+            hipLaunchKernelGGL((b16_stream_kernel<RU, NW, false>), grid, dim3(64 * NW), 0, st, sa);
+        };
+        switch (r / 16) {
+          case 1: go(std::integral_constant<int, 1>{}); break;
+          case 2: go(std::integral_constant<int, 2>{}); break;
+          case 3: go(std::integral_constant<int, 3>{}); break;
+          case 4: go(std::integral_constant<int, 4>{}); break;
+          case 5: go(std::integral_constant<int, 5>{}); break;
+          case 6: go(std::integral_constant<int, 6>{}); break;
+          case 7: go(std::integral_constant<int, 7>{}); break;
+          default: go(std::integral_constant<int, 8>{}); break;
+        }
+        const int rc = check_launch("b16_stream");
+        if (rc != DION_OK) return rc;
+        continue;
+      }
+    }
     B16UpdArgs a;
     memset(&a, 0, sizeof(a));
     for (int b = 0; b < nb; ++b) {
