@@ -2292,18 +2292,18 @@ constexpr int kRBE = DION_KRBE;   // 16-row blocks per wave in the fused row ker
 
 // ---- row kernel (not transposed): wave = kRBE x 16 rows, step = 32 columns;
 // lane (t, g) holds columns 16c + 4g .. +3 (c = 0, 1) of rows 16 rb + t.
-template <int GDT>
+template <int GDT, int KR = kRBE>
 struct RowStepE {
-  f32x4 x[kRBE][2];
-  uint2 gb[kRBE][2];
-  f32x4 gf[kRBE][2];
+  f32x4 x[KR][2];
+  uint2 gb[KR][2];
+  f32x4 gf[KR][2];
 };
 
-template <int GDT>
-__device__ __forceinline__ void rpe_load(RowStepE<GDT>& S, const float* __restrict__ M, const void* __restrict__ G,
+template <int GDT, int KR = kRBE>
+__device__ __forceinline__ void rpe_load(RowStepE<GDT, KR>& S, const float* __restrict__ M, const void* __restrict__ G,
                                          long ld_m, long ld_g, int j) {
 #pragma unroll
-  for (int rb = 0; rb < kRBE; ++rb)
+  for (int rb = 0; rb < KR; ++rb)
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       if (M != nullptr) S.x[rb][c] = ld_part(reinterpret_cast<const f32x4*>(M + rb * 16 * ld_m + j + 16 * c));
@@ -3100,6 +3100,19 @@ __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a)
 // pre-split P is the A operand (A[row j = 16 cb + t'][k]), one scale per matrix.  Each
 // step's product lands in a fresh accumulator D[j][col] (lane (t, g): R rows CT t + c,
 // r columns 16 cb + 4 g + q) and is added as acc += D / s_col.
+// 16-row blocks per wave of the r = 128 fused pass A row kernel (1 halves its accumulators
+// and EF operand, so the prefetch stage fits; tuning knob) and its pipeline depth
+#ifndef DION_PA_KR8
+#define DION_PA_KR8 2
+#endif
+constexpr int kKR8 = DION_PA_KR8;
+#ifndef DION_PA_PD8
+#define DION_PA_PD8 (DION_PA_KR8 == 1 ? 2 : 1)
+#endif
+// blocks per CU the r = 128 transposed fused pass A is compiled for (tuning knob)
+#ifndef DION_CPEH3_MINB8
+#define DION_CPEH3_MINB8 1
+#endif
 // pipeline depth of the r <= 64 fused pass A row kernel (tuning knob)
 #ifndef DION_PA_PD
 #define DION_PA_PD 2
@@ -3292,14 +3305,14 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !DION_H3_PAIRS) ? 1 : 2) 
 // holds row 16 rb + t, k-run KMAP 1) with a per-step scale per row (max over the lanes
 // (t, g = 0..3)), Q the A operand: each step lands in a fresh accumulator
 // D[16 cb + 4 g + q][row t] and is added as acc += D / s_row.
-template <int RB, int GDT, int PD>
+template <int RB, int GDT, int PD, int KR = kRBE>
 __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(const EfProjArgs e) {
   constexpr int R = 16 * RB;
   constexpr int KK = RB / 2;
   constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;  // f16x8 units of one K-step's splits
   __shared__ f16x8 tq[2][NQ];
   __shared__ f16x8 rs[2][NR];
-  __shared__ f32x4 xt[kPaNW][32 * 8];
+  __shared__ f32x4 xt[kPaNW][16 * KR * 8];
   const ProjArgs& a = e.p;
   const BlockXYZ blk = xcd_block();
   const int b = blk.z;
@@ -3310,7 +3323,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
-  const int row_base = blk.x * (16 * kRBE * kPaNW) + wave * (16 * kRBE);
+  const int row_base = blk.x * (16 * KR * kPaNW) + wave * (16 * KR);
   const int j_begin = kc * a.kchunk;
   const int j_end = min(a.cols, j_begin + a.kchunk);
   const void* G = nullptr;
@@ -3326,10 +3339,10 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
   const float sF = h3_scale(__uint_as_float(e.amax[2 * nb + b]), invF);  // power of two: P' s is exact
   const float efinv = e.alpha * invF * invR;
 
-  Split2h F[kRBE][KK];
+  Split2h F[KR][KK];
   if (has_ef) {
 #pragma unroll
-    for (int rb = 0; rb < kRBE; ++rb)
+    for (int rb = 0; rb < KR; ++rb)
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
         const float* src = e.efp[b] + static_cast<long>(row_base + 16 * rb + t) * R + 32 * kk + 8 * g;
@@ -3337,14 +3350,14 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
       }
   } else {
 #pragma unroll
-    for (int rb = 0; rb < kRBE; ++rb)
+    for (int rb = 0; rb < KR; ++rb)
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) F[rb][kk] = Split2h{};
   }
 
-  f32x4 acc[kRBE][RB];
+  f32x4 acc[KR][RB];
 #pragma unroll
-  for (int rb = 0; rb < kRBE; ++rb)
+  for (int rb = 0; rb < KR; ++rb)
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
   uint32_t nzb = 0;
@@ -3352,66 +3365,66 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
 
   const u32x4* qs = e.qsplit + b * e.split_stride;
   const u32x4* rsp = e.rsplit + b * e.split_stride;
-  RowStepE<GDT> S[PD];
-  auto xload = [&](RowStepE<GDT>& T, int j) {
+  RowStepE<GDT, KR> S[PD];
+  auto xload = [&](RowStepE<GDT, KR>& T, int j) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < 2 * KR; ++q)
       T.x[q >> 1][q & 1] = ld_stream(reinterpret_cast<const f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j));
-    rpe_load<GDT>(T, nullptr, G, 0, a.ld_g, j);
+    rpe_load<GDT, KR>(T, nullptr, G, 0, a.ld_g, j);
   };
-  auto xpose = [&](RowStepE<GDT>& T) {
+  auto xpose = [&](RowStepE<GDT, KR>& T) {
     f32x4* xw = xt[wave];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 2 * KR; ++q) {
       const int r = 8 * q + (lane >> 3), k = lane & 7;
       xw[r * 8 + (k ^ xt_swz(r))] = T.x[q >> 1][q & 1];
     }
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int rb = 0; rb < KR; ++rb)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int r = 16 * rb + t, k = 4 * c + g;
         T.x[rb][c] = xw[r * 8 + (k ^ xt_swz(r))];
       }
   };
-  auto xstore = [&](const RowStepE<GDT>& T, int j) {
+  auto xstore = [&](const RowStepE<GDT, KR>& T, int j) {
     f32x4* xw = xt[wave];
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int rb = 0; rb < KR; ++rb)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int r = 16 * rb + t, k = 4 * c + g;
         xw[r * 8 + (k ^ xt_swz(r))] = T.x[rb][c];
       }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 2 * KR; ++q) {
       const int r = 8 * q + (lane >> 3), k = lane & 7;
       st_stream(reinterpret_cast<f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j), xw[r * 8 + (k ^ xt_swz(r))]);
     }
   };
-  auto compute = [&](RowStepE<GDT>& X, const f16x8* tqc, const f16x8* rsc) {
+  auto compute = [&](RowStepE<GDT, KR>& X, const f16x8* tqc, const f16x8* rsc) {
     if (has_ef) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        f32x4 ev[kRBE];
+        f32x4 ev[KR];
 #pragma unroll
-        for (int rb = 0; rb < kRBE; ++rb) ev[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int rb = 0; rb < KR; ++rb) ev[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk) {
           Split2h A;
           A.hi = rsc[((c * KK + kk) * 2 + 0) * 64 + lane];
           A.lo = rsc[((c * KK + kk) * 2 + 1) * 64 + lane];
 #pragma unroll
-          for (int rb = 0; rb < kRBE; ++rb) ev[rb] = mfma3h(A, F[rb][kk], ev[rb]);
+          for (int rb = 0; rb < KR; ++rb) ev[rb] = mfma3h(A, F[rb][kk], ev[rb]);
         }
 #pragma unroll
-        for (int rb = 0; rb < kRBE; ++rb)
+        for (int rb = 0; rb < KR; ++rb)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) X.x[rb][c][q] = fmaf(ev[rb][q], efinv, X.x[rb][c][q]);
+          for (int q = 0; q < 2 * KR; ++q) X.x[rb][c][q] = fmaf(ev[rb][q], efinv, X.x[rb][c][q]);
       }
     }
 #pragma unroll
-    for (int rb = 0; rb < kRBE; ++rb)
+    for (int rb = 0; rb < KR; ++rb)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         if constexpr (GDT == DION_DTYPE_BF16) {
@@ -3426,10 +3439,10 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
         nzb |= __float_as_uint(X.x[rb][c][0]) | __float_as_uint(X.x[rb][c][1]) | __float_as_uint(X.x[rb][c][2]) |
                __float_as_uint(X.x[rb][c][3]);
       }
-    Split2h Bx[kRBE];
-    float invx[kRBE];
+    Split2h Bx[KR];
+    float invx[KR];
 #pragma unroll
-    for (int rb = 0; rb < kRBE; ++rb) {
+    for (int rb = 0; rb < KR; ++rb) {
       float m8 = max8abs(X.x[rb][0], X.x[rb][1]);
       m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
       m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
@@ -3443,10 +3456,10 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
       A.hi = tqc[(cb * 2 + 0) * 64 + lane];
       A.lo = tqc[(cb * 2 + 1) * 64 + lane];
 #pragma unroll
-      for (int rb = 0; rb < kRBE; ++rb) {
+      for (int rb = 0; rb < KR; ++rb) {
         const f32x4 d = mfma3h(A, Bx[rb], f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[rb][cb][q] = fmaf(d[q], invx[rb], acc[rb][cb][q]);
+        for (int q = 0; q < 2 * KR; ++q) acc[rb][cb][q] = fmaf(d[q], invx[rb], acc[rb][cb][q]);
       }
     }
   };
@@ -3489,7 +3502,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
 
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
 #pragma unroll
-  for (int rb = 0; rb < kRBE; ++rb)
+  for (int rb = 0; rb < KR; ++rb)
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb)
       *reinterpret_cast<f32x4*>(out + static_cast<long>(row_base + 16 * rb + t) * R + 16 * cb + 4 * g) =
@@ -3514,7 +3527,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
 // four lanes (t, g = 0..3)), Q the A operand: D[16 cb + 4 g + q][col 2t + c] is added as
 // acc += D / s_col.  The matrix's max |M| goes into the flag for a fixed-scale pass B.
 template <int RB, int GDT>
-__global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_efh3_kernel(const EfProjArgs e) {
+__global__ void __launch_bounds__(256, RB >= 8 ? DION_CPEH3_MINB8 : 2) colproj_efh3_kernel(const EfProjArgs e) {
   constexpr int R = 16 * RB;
   constexpr int KK = RB / 2;
   constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;  // f16x8 units of one K-step's splits
@@ -4066,10 +4079,13 @@ size_t presplit_stride(int nq, int r) { return static_cast<size_t>(nq) * r * 3 /
 size_t presplit_bytes(int nq, int r, int batch) { return 2 * 16 * presplit_stride(nq, r) * batch + 256; }
 
 // deferred-EF pass A (rowproj_ef_kernel / colproj_ef_kernel)
+// rows per block of the fused pass A row kernel (r = 128 may run 16-row waves)
+int pa_row_block(int r) { return 16 * (r > 64 ? kKR8 : kRBE) * kPaNW; }
+
 bool proj_ef_ok(int m, int n, int r, bool transposed) {
   // r = 128 (the Mixtral config) only through the h3 kernels
   if (r != 32 && r != 64 && !(r == 128 && (transposed ? DION_PA_H3T : DION_PA_H3))) return false;
-  return transposed ? (n % 128 == 0 && m % 32 == 0) : (m % (16 * kRBE * kPaNW) == 0 && n % 32 == 0);
+  return transposed ? (n % 128 == 0 && m % 32 == 0) : (m % pa_row_block(r) == 0 && n % 32 == 0);
 }
 
 // rowproj_ef_kernel loads M in whole lines (TJ, default) or in the MFMA layout directly
@@ -4082,8 +4098,8 @@ bool pa_lines() {
   return v;
 }
 
-Geo proj_ef_geo(int m, int n, int batch, bool transposed) {
-  if (!transposed) return rowproj_geo(m, n, batch, 16 * kRBE * kPaNW);
+Geo proj_ef_geo(int m, int n, int batch, bool transposed, int r) {
+  if (!transposed) return rowproj_geo(m, n, batch, pa_row_block(r));
   Geo g;
   g.gx = static_cast<int>(ceil_div(n, 128));
   long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
@@ -4547,7 +4563,7 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
       case DION_OP_PROJECT_P_EF: {
         if (!proj_ef_ok(d->m, d->n, d->r, d->transposed != 0))
           return fail(DION_E_UNSUPPORTED, "no deferred-EF pass A for %dx%d r=%d", d->m, d->n, d->r);
-        n = slab_bytes(proj_ef_geo(d->m, d->n, chunk, d->transposed != 0), chunk, d->r) +
+        n = slab_bytes(proj_ef_geo(d->m, d->n, chunk, d->transposed != 0, d->r), chunk, d->r) +
             presplit_bytes(nq, d->r, chunk);
         break;
       }
@@ -4634,7 +4650,7 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
     const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
-    const Geo geo = proj_ef_geo(d->m, d->n, nb, tr);
+    const Geo geo = proj_ef_geo(d->m, d->n, nb, tr, d->r);
     const int nq = tr ? d->m : d->n;
     const size_t slab = (slab_bytes(geo, nb, d->r) + 255) / 256 * 256;
     const size_t need = slab + presplit_bytes(nq, d->r, nb);
@@ -4744,7 +4760,7 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
           if (tr)
             hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
           else
-            hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, 1>), grid, dim3(64 * kPaNW), 0, st, e);
+            hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, DION_PA_PD8, kKR8>), grid, dim3(64 * kPaNW), 0, st, e);
         } else {
           if (tr && h3)
             hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
