@@ -3420,7 +3420,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
 #pragma unroll
         for (int rb = 0; rb < KR; ++rb)
 #pragma unroll
-          for (int q = 0; q < 2 * KR; ++q) X.x[rb][c][q] = fmaf(ev[rb][q], efinv, X.x[rb][c][q]);
+          for (int q = 0; q < 4; ++q) X.x[rb][c][q] = fmaf(ev[rb][q], efinv, X.x[rb][c][q]);
       }
     }
 #pragma unroll
@@ -3459,7 +3459,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
       for (int rb = 0; rb < KR; ++rb) {
         const f32x4 d = mfma3h(A, Bx[rb], f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-        for (int q = 0; q < 2 * KR; ++q) acc[rb][cb][q] = fmaf(d[q], invx[rb], acc[rb][cb][q]);
+        for (int q = 0; q < 4; ++q) acc[rb][cb][q] = fmaf(d[q], invx[rb], acc[rb][cb][q]);
       }
     }
   };
