@@ -41,7 +41,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 11
+#define DION_ABI_VERSION 12
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -218,10 +218,14 @@ int dion_colnorm_apply(const DionBatchDesc* desc, const float* R, void* const* Q
  * Entries with nonzero[b] == 0 keep M and only decay W.
  * `ws` is optional: with dion_workspace_bytes(desc, DION_OP_EF_APPLY) bytes the
  * streamed factor P is split into bf16 limbs once per call instead of per tile.
+ * The hyper-parameters are the reference's Python doubles (ABI 12): -(1 - mu), 1 - lr*wd
+ * and -scaled_lr are formed in double and rounded to fp32 once, as torch casts a Python
+ * scalar operand (kernels.py:54-83 _foreach_mul(update, alpha); runtime.py:1110-1113
+ * W.mul_(1 - lr*wd), W.add_(delta, alpha=-scaled_lr)).
  */
 int dion_ef_apply(const DionBatchDesc* desc, float* const* M, float* const* W,
                   const float* P, const float* R, const float* const* Qn,
-                  const uint32_t* nonzero, float mu, float lr, float wd, float scaled_lr,
+                  const uint32_t* nonzero, double mu, double lr, double wd, double scaled_lr,
                   void* ws, size_t ws_bytes, dion_stream_t stream);
 
 /*

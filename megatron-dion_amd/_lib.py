@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # DION_LIB_PATH: load another build of the same ABI (kernel-variant A/B runs during tuning)
 LIB_PATH = os.environ.get("DION_LIB_PATH") or os.path.join(HERE, "csrc", "libdion_codec.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -100,8 +100,8 @@ _SIGNATURES = {
     "dion_fixup_colnorm": ([_DESC, _P, _P, _PP, _P, ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_fixup_colsum": ([_DESC, _P, _P, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_colnorm_apply": ([_DESC, _P, _PP, _P, ctypes.c_float, _P], ctypes.c_int),
-    "dion_ef_apply": ([_DESC, _PP, _PP, _P, _P, _PP, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
-                       ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "dion_ef_apply": ([_DESC, _PP, _PP, _P, _P, _PP, _P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                       ctypes.c_double, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_dortho_sketch": ([_DESC, _P, _P, ctypes.c_uint64, ctypes.c_int64, ctypes.c_float, _P, _P, ctypes.c_size_t,
                             _P], ctypes.c_int),
     "dion_dortho_qr_inv": ([ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P], ctypes.c_int),

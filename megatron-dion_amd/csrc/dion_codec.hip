@@ -1691,9 +1691,9 @@ struct RankArgs {
   // rank_stream_kernel<..., H3 = true> (the weight update: both factors bounded by 1 in
   // magnitude, P orthonormal, Qn column-normalised): power-of-two h3 scales fixed by that
   // bound instead of measured
-  float h3_fixed_mul;        // scale * s_fixed
-  float h3_stream_scale;     // s_streamed
-  float h3_inv;              // 1 / (s_fixed s_streamed)
+  float h3_fixed_mul;        // s_fixed (a power of two)
+  float h3_stream_scale;     // s_streamed (a power of two)
+  float h3_inv;              // scale / (s_fixed s_streamed)
 };
 
 // fp16x3 ("h3") split types and helpers: see the h3 section below
@@ -1712,6 +1712,10 @@ __device__ __forceinline__ float h3_scale(float amax, float& inv) {
   return __uint_as_float(static_cast<uint32_t>(es) << 23);
 }
 
+// s MUST be a power of two (every caller's is): x s is then exact, so the hi limb is the
+// same whether the compiler forms it from the product in one step (v_fma_mixlo_f16) or
+// from the fp32 product, and hi + lo represents x s.  With any other s the two roundings
+// differ now and then and the pair misses x s by an ulp of hi.
 __device__ __forceinline__ void split2h(const f32x4& a, const f32x4& b, float s, Split2h& o) {
   // x s is rounded to fp32 ONCE and both limbs come from that value: with contraction the
   // compiler fuses x s - hi into one mixed-precision FMA on the exact product, and where
@@ -1853,7 +1857,7 @@ __global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const
     const int so = (row0 * ld + col0) * 4;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const float v = T.x[q] * a.decay + acc[q];
+      const float v = __fmul_rn(T.x[q], a.decay) + acc[q];
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[q], so, kStreamAux);
     }
   };
@@ -2016,7 +2020,8 @@ __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_st
     const float ainv = H3 ? a.h3_inv : 1.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const float v = H3 ? fmaf(acc[q], ainv, T[q] * a.decay) : T[q] * a.decay + acc[q];
+      // X d rounded first (the reference's W.mul_(1 - lr wd)), then the update added
+      const float v = H3 ? fmaf(acc[q], ainv, __fmul_rn(T[q], a.decay)) : __fmul_rn(T[q], a.decay) + acc[q];
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[q], so, kStreamAux);
     }
   };
@@ -5118,8 +5123,8 @@ int dion_colnorm_apply(const DionBatchDesc* d, const float* R, void* const* Q, c
 }
 
 int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, const float* P, const float* R,
-                  const float* const* Qn, const uint32_t* nonzero, float mu, float lr, float wd, float scaled_lr,
-                  void* ws, size_t ws_bytes, dion_stream_t stream) {
+                  const float* const* Qn, const uint32_t* nonzero, double mu, double lr, double wd,
+                  double scaled_lr, void* ws, size_t ws_bytes, dion_stream_t stream) {
   int rc = validate(d);
   if (rc != DION_OK) return rc;
   if (P == nullptr || R == nullptr || Qn == nullptr || nonzero == nullptr || (M == nullptr && W == nullptr))
@@ -5127,10 +5132,10 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (d->m_dtype == DION_DTYPE_BF16) {
     // kernels.py:54-83 (bf16): M = rne(M + rne(alpha rne(P R^T)));  runtime.py:1111-1113: W = W d - s rne(P Qn^T)
-    const float alpha = static_cast<float>(-(1.0 - static_cast<double>(mu)));
+    const float alpha = static_cast<float>(-(1.0 - mu));
     return b16::update(d, reinterpret_cast<uint16_t* const*>(M), W, P, R,
-                       reinterpret_cast<const uint16_t* const*>(Qn), alpha, -scaled_lr,
-                       (wd > 0.f) ? (1.0f - lr * wd) : 1.0f, st);
+                       reinterpret_cast<const uint16_t* const*>(Qn), alpha, static_cast<float>(-scaled_lr),
+                       (wd > 0.0) ? static_cast<float>(1.0 - lr * wd) : 1.0f, st);
   }
   const int mp = d->transposed ? d->n : d->m;
   const int nq = d->transposed ? d->m : d->n;
@@ -5156,9 +5161,9 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
     a.transposed = d->transposed;
     a.ld_m = ldv(d->ld_m, d->n);
     a.ld_w = ldv(d->ld_w, d->n);
-    a.alpha = -(1.0f - mu);
-    a.beta = -scaled_lr;
-    a.decay = (wd > 0.f) ? (1.0f - lr * wd) : 1.0f;
+    a.alpha = static_cast<float>(-(1.0 - mu));
+    a.beta = static_cast<float>(-scaled_lr);
+    a.decay = (wd > 0.0) ? static_cast<float>(1.0 - lr * wd) : 1.0f;
     a.has_w = W ? 1 : 0;
     const int flen = d->transposed ? d->m : d->n;
     const int slen = d->transposed ? d->n : d->m;
@@ -5216,12 +5221,19 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
         ra.decay = pass == 0 ? 1.0f : a.decay;
         ra.skip_zero = pass == 0 ? 1 : 0;
         if (pass == 1) {
-          // h3 scales from the factors' bound |P|, |Qn| <= 1 (2 leaves headroom for rounding)
-          const float sf = h3_scale_host(2.f * fabsf(ra.scale));
+          // h3 scales from the factors' bound |P|, |Qn| <= 1 (2 leaves headroom for rounding).
+          // Both are powers of two, so x s is exact and each limb pair splits one value; the
+          // step's -scaled_lr rides on the final fma instead: W = fma(acc, -s / (s_f s_s), W d),
+          // the reference's W.mul_(d) then W.add_(P Qn^T, alpha=-s) (runtime.py:1110-1113).
+          // (Folding -s into the fixed factor's split made x s inexact: the compiler then forms
+          // the hi limb from the exact product (v_fma_mix) and the lo limb from the rounded
+          // one, and where the two roundings differ the pair misses x by an ulp of hi: ~3e-5
+          // of max |dW|, tests/test_gpu_update_precision.py.)
+          const float sf = h3_scale_host(2.f);
           const float ss = h3_scale_host(2.f);
-          ra.h3_fixed_mul = ra.scale * sf;
+          ra.h3_fixed_mul = sf;
           ra.h3_stream_scale = ss;
-          ra.h3_inv = 1.f / (sf * ss);
+          ra.h3_inv = ra.scale / (sf * ss);
         }
         auto launch = [&](auto RUc) {
           constexpr int RUv = decltype(RUc)::value;

@@ -24,13 +24,15 @@ This module keeps the returned value and replaces the exchange:
     rounding, not bitwise.
   * mode="local_bound": no gradient traffic at all.  Returns mean_i ||G_i||^2 over the
     replicas (one scalar all-reduce), which bounds ||mean_i G_i||^2 from above (convexity
-    of the square), so clipping with it never clips less than the exact norm would.
+    of the square); under the SUM replicate op W sum_i ||G_i||^2, which bounds
+    ||sum_i G_i||^2.  Clipping with it never clips less than the exact norm would.
     An opt-in deviation from the reference's number, for runs where the dense exchange
     costs more than the conservative clip.
 The sum of squares runs in the HIP kernel `dion_grad_sum_sq` (fp64, exact squares,
 fixed order), reading each gradient once in its own dtype: the reference's chunked
-`.to(float64)` copies (:54-68) disappear.  The reference's dense-RP reduced-gradient
-cache (:161-211, only for parameters without low-rank sync) is outside this path.
+`.to(float64)` copies (:54-68) disappear.  Gradients of parameters without low-rank sync
+(`dense_reuse`) are all-reduced in place instead and reused by the step (the reference's
+dense-RP reduced-gradient cache, :161-211 and dion/dense_grad_cache.py).
 """
 from __future__ import annotations
 
@@ -40,7 +42,9 @@ from typing import List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
-__all__ = ["dion_grad_norm_sq", "dion_grad_norm", "as_matrices"]
+from .dense_grad_cache import can_reuse_dense_grad, lookup, mark_reduced
+
+__all__ = ["dion_grad_norm_sq", "dion_grad_norm", "dense_reuse_flags", "as_matrices"]
 
 _FLAT_COLS = 1 << 20
 _CHUNK_BYTES = 256 << 20
@@ -117,14 +121,49 @@ def _reduced_sum_sq(codec, members, op, group, world, device, dtype, chunk_bytes
     return total
 
 
+def _reduce_dense_in_place(optimizer, codec, grads, op, group, device) -> torch.Tensor:
+    """grad_norm.py:174-258 for the dense-reuse gradients: all-reduce each in place (once per
+    step: one already reduced by this step's norm is taken as it is), mark it for the step
+    (dense_grad_cache), and return the fp64 sum of squares of the reduced values (the same
+    on every rank)."""
+    before = int(getattr(optimizer, "_step_count", 0))
+    todo = []
+    for g in grads:
+        state, _ = lookup(optimizer, g, group=group, op=op, before_step=before)
+        if state == "mismatch":
+            raise RuntimeError(f"[DION_DENSE_RP_GRAD_CACHE_MISMATCH] grad {tuple(g.shape)} was reduced with another "
+                               "replicate group or op")
+        if state == "missing":
+            todo.append(g)
+    works = []
+    for g in todo:
+        works.append((g, None, dist.all_reduce(g, op=op, group=group, async_op=True)) if g.is_contiguous() else
+                     (g, (c := g.contiguous()), dist.all_reduce(c, op=op, group=group, async_op=True)))
+    for g, c, w in works:
+        w.wait()
+        if c is not None:
+            g.copy_(c)
+        mark_reduced(optimizer, g, group=group, op=op, before_step=before)
+    return _local_sum_sq(codec, grads, device)
+
+
 def dion_grad_norm_sq(optimizer, grads: Sequence[torch.Tensor], *, count_dion_grad: bool = True,
-                      replica_group=None, mode: str = "exact",
-                      chunk_bytes: int = _CHUNK_BYTES) -> Optional[torch.Tensor]:
+                      replica_group=None, mode: str = "exact", chunk_bytes: int = _CHUNK_BYTES,
+                      dense_reuse: Optional[Sequence[bool]] = None) -> Optional[torch.Tensor]:
     """Sum of squares (fp64, shape (1,), on the gradients' device) of the Dion gradients
-    (of their replica reduction when `replica_group` has more than one rank)."""
+    (of their replica reduction when `replica_group` has more than one rank).
+
+    `dense_reuse[i]` (distrib_dion/grad_norm.py:37-52, `can_reuse_dense_grad`): gradient i
+    belongs to a parameter without low-rank sync, whose step all-reduces it anyway.  It is
+    all-reduced here in place, once, and the step reuses it (dense_grad_cache): one exchange
+    per step for those gradients (the reference's flow)."""
     if mode not in ("exact", "local_bound"):
         raise RuntimeError(f"[DION_INVALID_GRAD_NORM_MODE] mode={mode!r}")
-    grads = [g for g in grads if g is not None]
+    flags = list(dense_reuse) if dense_reuse is not None else [False] * len(grads)
+    if len(flags) != len(grads):
+        raise RuntimeError(f"[DION_GRAD_NORM_REUSE_FLAGS] {len(flags)} flags for {len(grads)} gradients")
+    keep = [i for i, g in enumerate(grads) if g is not None]
+    grads, flags = [grads[i] for i in keep], [bool(flags[i]) for i in keep]
     if not grads:
         return None
     codec = optimizer.codec
@@ -132,23 +171,40 @@ def dion_grad_norm_sq(optimizer, grads: Sequence[torch.Tensor], *, count_dion_gr
     dev = grads[0].device
     if world <= 1:
         return _local_sum_sq(codec, grads, dev) if count_dion_grad else None
-    if mode == "local_bound":
-        total = _local_sum_sq(codec, grads, dev)
-        dist.all_reduce(total, op=dist.ReduceOp.SUM, group=replica_group)
-        total /= world
-        return total if count_dion_grad else None
     op = _replicate_op(optimizer)
-    groups = {}
-    for g in grads:
-        groups.setdefault((g.dtype, g.device), []).append(g)
+    dense = [g for g, f in zip(grads, flags) if f]
+    grads = [g for g, f in zip(grads, flags) if not f]
+    dense_sq = _reduce_dense_in_place(optimizer, codec, dense, op, replica_group, dev) if dense else None
     total = torch.zeros(1, dtype=torch.float64, device=dev)
-    for (dtype, device), members in groups.items():
-        if sum(int(g.numel()) for g in members) <= 0:
-            continue
-        total += _reduced_sum_sq(codec, members, op, replica_group, world, device, dtype,
-                                 int(chunk_bytes)).to(dev)
-    dist.all_reduce(total, op=dist.ReduceOp.SUM, group=replica_group)
+    if mode == "local_bound":
+        if grads:
+            total = _local_sum_sq(codec, grads, dev)
+        dist.all_reduce(total, op=dist.ReduceOp.SUM, group=replica_group)
+        # ||mean_i G_i||^2 <= mean_i ||G_i||^2 (AVG);  ||sum_i G_i||^2 <= W sum_i ||G_i||^2 (SUM)
+        if op == dist.ReduceOp.SUM:
+            total *= world
+        else:
+            total /= world
+    else:
+        groups = {}
+        for g in grads:
+            groups.setdefault((g.dtype, g.device), []).append(g)
+        for (dtype, device), members in groups.items():
+            if sum(int(g.numel()) for g in members) <= 0:
+                continue
+            total += _reduced_sum_sq(codec, members, op, replica_group, world, device, dtype,
+                                     int(chunk_bytes)).to(dev)
+        dist.all_reduce(total, op=dist.ReduceOp.SUM, group=replica_group)
+    if dense_sq is not None:
+        total += dense_sq  # every rank holds the same reduced dense gradients
     return total if count_dion_grad else None
+
+
+def dense_reuse_flags(optimizer, params: Sequence[torch.Tensor]) -> List[bool]:
+    """`dense_reuse` for dion_grad_norm_sq from the adapter's per-parameter metadata
+    (`optimizer.dist_metas`, as distrib_dion/grad_norm.py:27-34 looks it up)."""
+    metas = getattr(optimizer, "dist_metas", None) or {}
+    return [can_reuse_dense_grad(metas.get(p)) for p in params]
 
 
 def dion_grad_norm(optimizer, grads: Sequence[torch.Tensor], **kwargs) -> float:

@@ -440,6 +440,9 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
     mult = int(optimizer.defaults.get("rank_multiple_of", 1))
     pred = dion_predicate or is_dion_param
     metas = {}
+    # shard param -> its DionDistMeta, where the reference's helpers look it up
+    # (distrib_dion/grad_norm.py:27-34; split parents stay out: their children are the Dion params)
+    dist_metas = optimizer.__dict__.setdefault("dist_metas", {})
     group_of = {id(p): g for g in optimizer.param_groups for p in g["params"]}
     dion_named, ew_named = [], []
     for name, p in named_params:
@@ -501,6 +504,7 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
             meta.extra.update(tp_group=tp_group, tp_shard_dim=int(tspec[1]), tp_start_idx=int(tspec[2]),
                               tp_end_idx=int(tspec[3]), tp_world_size=int(dist.get_world_size(tp_group)))
         metas[name] = (cfg, meta)
+        dist_metas[p] = meta
     ordered = sorted(dion_named, key=lambda kv: kv[0])
 
     def grad_of(p):

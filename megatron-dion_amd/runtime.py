@@ -23,6 +23,7 @@ import torch
 import torch.distributed as dist
 
 from .codec import factor_rows
+from .dense_grad_cache import consume_if_reduced
 from .kernels import scaled_lr_for_shape
 
 
@@ -117,6 +118,23 @@ def _shape_of(meta, state, fallback):
     shape = st.get("per_expert_global_shape") or st.get("global_shape") \
         or getattr(meta, "per_expert_global_shape", None) or getattr(meta, "global_shape", None) or fallback
     return tuple(int(d) for d in shape)
+
+
+def replicate_op(optimizer):
+    """runtime.py:361-364: AVG when rp_average_in_collective, else SUM."""
+    return dist.ReduceOp.AVG if optimizer.defaults.get("rp_average_in_collective", True) else dist.ReduceOp.SUM
+
+
+def dense_replica_all_reduce(optimizer, grads, group) -> Generator[None, None, None]:
+    """runtime.py:439-491: all-reduce the dense gradients across the replicas, unless this
+    step's grad norm already did (dense_grad_cache, runtime.py:387-435)."""
+    op = replicate_op(optimizer)
+    if consume_if_reduced(optimizer, grads, group=group, op=op):
+        return
+    works = [dist.all_reduce(g, op=op, group=group, async_op=True) for g in grads]
+    yield
+    for w in works:
+        w.wait()
 
 
 def check_supported_batch(optimizer, *, batch_group, batch_collectives, configs, dist_metas, optimizer_states,
@@ -278,12 +296,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         return
 
     if W > 1 and not use_low_rank and real_grads:
-        # runtime.py:439-491: dense all-reduce of the gradients across replicas
-        op = dist.ReduceOp.AVG if optimizer.defaults.get("rp_average_in_collective", True) else dist.ReduceOp.SUM
-        works = [dist.all_reduce(g, op=op, group=group, async_op=True) for g in real_grads]
-        yield
-        for w in works:
-            w.wait()
+        yield from dense_replica_all_reduce(optimizer, real_grads, group)
 
     kch = int(chunks) if (W > 1 and int(chunks) > 1 and B == real == int(chunks) * W) else 0
     if kch:
@@ -442,7 +455,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         # weights now; this step's error feedback waits for the next pass A (or a flush)
         codec.ef_apply(None, list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd, scaled, transposed)
         for i in range(real):
-            _record_pending(optimizer_states[i], P[i], R[i], -(1.0 - mu))
+            _record_pending(optimizer_states[i], P[i], R[i], -(1.0 - mu), transposed)
     else:
         codec.ef_apply(list(momentums[:real]), list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd,
                        scaled, transposed)
@@ -485,11 +498,7 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     group = getattr(batch_group, "replicate_group", None)
     if not use_low_rank and _group_world(group) > 1 and real_grads:
         # runtime.py:1553-1558 -> :439-491: dense all-reduce of the shard gradients across replicas
-        op = dist.ReduceOp.AVG if optimizer.defaults.get("rp_average_in_collective", True) else dist.ReduceOp.SUM
-        works = [dist.all_reduce(g, op=op, group=group, async_op=True) for g in real_grads]
-        yield
-        for w in works:
-            w.wait()
+        yield from dense_replica_all_reduce(optimizer, real_grads, group)
     B = len(params)
     m, n = (int(d) for d in param_shapes[0])
     transposed = bool(configs[0].is_transposed)
@@ -571,11 +580,7 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     group = getattr(batch_group, "replicate_group", None)
     W = _group_world(group)
     if W > 1 and not use_low_rank and real_grads:
-        op = dist.ReduceOp.AVG if optimizer.defaults.get("rp_average_in_collective", True) else dist.ReduceOp.SUM
-        works = [dist.all_reduce(g, op=op, group=group, async_op=True) for g in real_grads]
-        yield
-        for w in works:
-            w.wait()
+        yield from dense_replica_all_reduce(optimizer, real_grads, group)
     B = len(params)
     m, n = (int(d) for d in param_shapes[0])
     transposed = bool(configs[0].is_transposed)
@@ -802,7 +807,7 @@ def _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim
     if defer:
         codec.ef_apply(None, list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd, scaled, transposed)
         for i in range(real):
-            _record_pending(optimizer_states[i], P[i], R[i], -(1.0 - mu))
+            _record_pending(optimizer_states[i], P[i], R[i], -(1.0 - mu), transposed)
     else:
         codec.ef_apply(list(momentums[:real]), list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd,
                        scaled, transposed)
@@ -816,7 +821,9 @@ def _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim
         sink(P[:real], R[:real])
 
 
-# optimizer-state key of a pending (deferred) error feedback: (P_b, R_b, alpha, M ref).
+# optimizer-state key of a pending (deferred) error feedback: (P_b, R_b, alpha, M ref,
+# transposed).  The orientation is recorded with the factors: it cannot be told from the
+# shapes (a square FS or TP shard has m_P == m in either orientation).
 # The leading underscore keeps it out of the reference's persistent checkpoint state
 # (distrib_dion/checkpoint_io.py:247-266), so the momentum must carry it before anything
 # outside the step reads it: DionParamState applies it on such a read, and
@@ -827,23 +834,24 @@ def _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim
 _PENDING_EF = "_dion_pending_ef"
 
 
-def _record_pending(state, P_b, R_b, alpha) -> None:
+def _record_pending(state, P_b, R_b, alpha, transposed: bool) -> None:
     M = dict.get(state, "momentum")
-    dict.__setitem__(state, _PENDING_EF, (P_b, R_b, alpha, weakref.ref(M) if M is not None else None))
+    dict.__setitem__(state, _PENDING_EF, (P_b, R_b, alpha, weakref.ref(M) if M is not None else None,
+                                          bool(transposed)))
 
 
 def _take_pending(state):
-    """Pop one state's pending error feedback as (P_b, R_b, alpha); None when there is none
-    or when it was recorded for a momentum tensor the state no longer holds."""
+    """Pop one state's pending error feedback as (P_b, R_b, alpha, transposed); None when there
+    is none or when it was recorded for a momentum tensor the state no longer holds."""
     if state is None:
         return None
     pend = dict.pop(state, _PENDING_EF, None)
     if pend is None:
         return None
-    ref = pend[3] if len(pend) > 3 else None
+    ref = pend[3]
     if ref is not None and ref() is not dict.get(state, "momentum"):
         return None
-    return pend[:3]
+    return pend[0], pend[1], pend[2], pend[4]
 
 
 class DionParamState(dict):
@@ -869,9 +877,8 @@ class DionParamState(dict):
         pend = _take_pending(self)
         if pend is not None:
             M = dict.__getitem__(self, "momentum")
-            transposed = pend[0].shape[0] != M.shape[0]
             _apply_pending(opt.codec, M, dict.__getitem__(self, "Q"), pend, int(M.shape[0]), int(M.shape[1]),
-                           transposed)
+                           pend[3])
 
     def __getitem__(self, key):
         if key == "momentum":
@@ -886,6 +893,17 @@ class DionParamState(dict):
     def items(self):
         self._sync()
         return dict.items(self)
+
+    # dict(state), {**state} and dict.update(other, state) copy a dict subclass through
+    # CPython's fast path (no __getitem__) unless its type overrides __iter__: with these
+    # overrides they go through keys() / __getitem__ and see the eager momentum
+    def __iter__(self):
+        self._sync()
+        return dict.__iter__(self)
+
+    def keys(self):
+        self._sync()
+        return dict.keys(self)
 
     def values(self):
         self._sync()
@@ -930,7 +948,7 @@ class DionStateMap(collections.defaultdict):
 
 def _apply_pending(codec, M, Q, pending, m, n, transposed):
     """M += alpha P R^T (or alpha R P^T) for one matrix: the eager error feedback, late."""
-    Pb, Rb, alpha = pending
+    Pb, Rb, alpha = pending[:3]
     mu = 1.0 + float(alpha)
     ones = torch.ones((1,), dtype=torch.int32, device=M.device)
     codec.ef_apply([M], None, Pb.unsqueeze(0), Rb.unsqueeze(0), [Q], ones, mu, 0.0, 0.0, 0.0, transposed)
@@ -946,8 +964,7 @@ def flush_pending_error_feedback(optimizer, get_codec) -> int:
             continue
         codec = codec or get_codec()
         M, Q = dict.__getitem__(st, "momentum"), dict.__getitem__(st, "Q")
-        transposed = pend[0].shape[0] != M.shape[0]  # P has n rows iff transposed (m_P = n != m)
-        _apply_pending(codec, M, Q, pend, int(M.shape[0]), int(M.shape[1]), transposed)
+        _apply_pending(codec, M, Q, pend, int(M.shape[0]), int(M.shape[1]), pend[3])
         count += 1
     return count
 

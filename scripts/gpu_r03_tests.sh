@@ -1,0 +1,13 @@
+# one GPU box call: the whole gpu suite (verbose, measured full-size errors), smoke, the default bench line
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -a -E "passed|failed|FAILED|Error" gpurun_out/pytest_gpu.log | tail -20
+if [ $rc -gt 1 ]; then exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -4 gpurun_out/smoke.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log
+exit $rc

@@ -94,3 +94,72 @@ def test_w2_dense_branch_equals_the_step_on_the_averaged_gradient():
                 assert torch.equal(got0, got1), (s, n, key)  # identical across replicas
                 err = (got0 - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
                 assert err <= 1e-6, (s, n, key, err)
+
+
+def _clip_worker(rank, world, port, out_dir):
+    """Grad norm (clipping) then step, both without low-rank sync: count the dense exchanges."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    import megatron_dion_amd.grad_norm as gn
+    from tests._cpu_codec import OracleCodec
+
+    calls = []
+    real_all_reduce = dist.all_reduce
+
+    def counting_all_reduce(tensor, *args, **kwargs):
+        calls.append(int(tensor.numel()))
+        return real_all_reduce(tensor, *args, **kwargs)
+
+    dist.all_reduce = counting_all_reduce
+    out = {}
+    try:
+        for clip in (False, True):
+            cur = {"s": 0}
+            opt, params = _make(OracleCodec(sketch_lookup=lambda P: _sketch(P, cur["s"])), dist.group.WORLD)
+            grad_sizes = sorted(int(p.numel()) for p in params.values())
+            for s in range(STEPS):
+                cur["s"] = s
+                for n, g in _grads(rank, s).items():
+                    params[n].grad = g
+                calls.clear()
+                if clip:
+                    plist = list(params.values())
+                    grads = [p.grad for p in plist]
+                    flags = gn.dense_reuse_flags(opt, plist)
+                    assert all(flags), flags
+                    out[f"clip_s{s}_norm"] = gn.dion_grad_norm_sq(opt, grads, replica_group=dist.group.WORLD,
+                                                                  dense_reuse=flags)
+                opt.step()
+                dense = sorted(c for c in calls if c > 1)
+                out[f"{int(clip)}_s{s}_exchanges"] = torch.tensor([int(dense == grad_sizes)])
+                for n, p in params.items():
+                    out[f"{int(clip)}_s{s}_{n}_W"] = p.detach().clone()
+                    out[f"{int(clip)}_s{s}_{n}_M"] = opt.state[p]["momentum"].clone()
+                if clip:
+                    out[f"clip_s{s}_cache_left"] = torch.tensor([int(hasattr(opt, "_dion_dense_grad_reduction_cache"))])
+    finally:
+        dist.all_reduce = real_all_reduce
+    torch.save(out, os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_w2_clip_then_step_exchanges_each_dense_gradient_once():
+    """distrib_dion/grad_norm.py:161-258 + dion/dense_grad_cache.py: with clipping, the norm
+    all-reduces the dense (no low-rank sync) gradients in place and the step reuses them --
+    one exchange per gradient per step, and the same W, M as without clipping."""
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_clip_worker, args=(2, _free_port(), tmp), nprocs=2, join=True, start_method="spawn")
+        res = [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+    for r in range(2):
+        for s in range(STEPS):
+            # one all-reduce per gradient: in the step without clipping, in the norm with it
+            assert int(res[r][f"0_s{s}_exchanges"]) == 1 and int(res[r][f"1_s{s}_exchanges"]) == 1, (r, s)
+            assert int(res[r][f"clip_s{s}_cache_left"]) == 0  # the step consumed every mark
+            g0, g1 = _grads(0, s), _grads(1, s)
+            ref = sum(((g0[n].double() + g1[n].double()) / 2).square().sum().item() for n in g0)
+            assert res[r][f"clip_s{s}_norm"].item() == pytest.approx(ref, rel=1e-6)
+            for n, _, _ in SHAPES:
+                for key in ("W", "M"):
+                    assert torch.equal(res[r][f"1_s{s}_{n}_{key}"], res[r][f"0_s{s}_{n}_{key}"]), (r, s, n, key)

@@ -16,10 +16,13 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from tests._metrics import dw_err
+
 pytestmark = pytest.mark.gpu
 
 TOL_WM = 1e-5
 TOL_Q = 1e-5
+TOL_DW = 5e-6  # the weight step alone against the reference's (tests/_metrics.dw_err), fp32 state
 
 
 def _free_port():
@@ -94,6 +97,7 @@ def test_hip_codec_w2_matches_reference(name, deferred):
     from tests._golden import Case
 
     case = Case(name)
+    h = case.hyper
     bf16 = bool(case.entry.get("bf16"))
     with tempfile.TemporaryDirectory() as tmp:
         mp.start_processes(_worker, args=(2, _free_port(), case.name, tmp, deferred), nprocs=2, join=True,
@@ -114,6 +118,11 @@ def test_hip_codec_w2_matches_reference(name, deferred):
                 for k, ref, tol in keys:
                     err = maxrel(res[rank][f"s{step}_{n}_{k}"].float(), case.t(rank, step, f"{n}_{ref}"))
                     assert err <= tol, (rank, step, n, k, err)
+                if not bf16:
+                    w_prev = case.t(rank, 0, f"{n}_W0") if step == 0 else res[rank][f"s{step - 1}_{n}_W"]
+                    err = dw_err(w_prev, res[rank][f"s{step}_{n}_W"], case.t(rank, step, f"{n}_W0"),
+                                 case.t(rank, step, f"{n}_W1"), 1.0 - h["lr"] * h["weight_decay"])
+                    assert err <= TOL_DW, (rank, step, n, "dW", err)
     for n in names:
         assert torch.equal(res[0][f"s1_{n}_W"], res[1][f"s1_{n}_W"])
         assert torch.equal(res[0][f"s1_{n}_Q"], res[1][f"s1_{n}_Q"])

@@ -17,8 +17,16 @@ explicit sketches so no sign alignment is needed:
             launch groups of k = 2 and 3 chunks (coalesce_replicated_batches), deferred EF,
             two slot streams, against the same runtime driven by the CPU oracle codec
 
-Tolerance: max |a - b| / max |b| <= 1e-5 for W, M and Q.  The measured
-errors are written to gpurun_out/fullsize_errors.json when that directory exists.
+Tolerance: max |a - b| / max |b| <= 1e-5 for W, M and Q.  W0 (0.02 N(0,1))
+dwarfs one step's update (~1e-3 of it), so W is also scored on the update alone ("dW"):
+
+  dW_x(t) = W_x(t) - fp32(W_x(t-1) (1 - lr wd))       (fp64 arithmetic, x = hip | oracle)
+  err_dW  = max(|dW_hip - dW_or| - ulp(W(t))) / max |dW_or|    <= TOL_DW
+
+(the ulp is the two final fp32 roundings of W(t)).  dW also carries the P / Q differences
+between the two runs (~1e-6), so TOL_DW = 5e-6; the isolated weight update is held to 1e-6
+of its own scale in tests/test_gpu_update_precision.py.  The measured errors are written to
+gpurun_out/fullsize_errors.json when that directory exists.
 """
 import json
 import math
@@ -35,10 +43,12 @@ import torch.multiprocessing as mp
 import megatron_dion_amd as mda
 from megatron_dion_amd.optimizer import attach_dp_routing
 from oracle import dion_oracle as O
+from tests._metrics import dw_err
 
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-5
+TOL_DW = 5e-6
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _ERRORS = {}
 
@@ -109,9 +119,11 @@ def _run_vs_oracle(label, shapes, r, steps, check=None):
         return out
 
     opt._sketch_override = override
-    worst = {"W": 0.0, "M": 0.0, "Q": 0.0}
+    worst = {"W": 0.0, "dW": 0.0, "M": 0.0, "Q": 0.0}
+    decay = 1.0 - 0.01 * 0.01
     for step in range(steps):
         cur["step"] = step
+        prev = {name: (p.detach().cpu().clone(), mats[name].W.clone()) for name, p in named if name in mats}
         grads = {}
         for idx, (name, p) in enumerate(named):
             g = torch.Generator(device=dev).manual_seed(99 + 17 * step + 131 * idx)
@@ -132,12 +144,13 @@ def _run_vs_oracle(label, shapes, r, steps, check=None):
                 continue
             mt = mats[name]
             st = opt.state[p]
-            errs = {"W": maxrel(p, mt.W), "Q": maxrel(st["Q"], mt.Q)}
+            errs = {"W": maxrel(p, mt.W), "Q": maxrel(st["Q"], mt.Q),
+                    "dW": dw_err(prev[name][0], p.detach().cpu(), prev[name][1], mt.W, decay)}
             if step == steps - 1:
                 errs["M"] = maxrel(st["momentum"], mt.M)
             for key, v in errs.items():
                 worst[key] = max(worst[key], v)
-            assert all(v <= TOL for v in errs.values()), (label, step, name, errs)
+            assert all(v <= (TOL_DW if key == "dW" else TOL) for key, v in errs.items()), (label, step, name, errs)
     for name, p in named:
         Q = opt.state[p]["Q"].double()
         assert torch.isfinite(p).all() and torch.isfinite(opt.state[p]["momentum"]).all()
@@ -219,6 +232,8 @@ def _w2_worker(rank, world, port, out_dir):
             return out
 
         opt._sketch_override = override
+        for n, p in named:
+            res[f"{backend}_sinit_{n}_W"] = p.detach().cpu().clone()
         chunks = []
         for s in range(steps):
             cur["s"] = s
@@ -250,12 +265,22 @@ def test_w2_rank_major_groups_k_gt_1_on_gpu():
     with tempfile.TemporaryDirectory() as tmp:
         mp.start_processes(_w2_worker, args=(2, _port(), tmp), nprocs=2, join=True, start_method="spawn")
         res = [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(2)]
-    worst = {"W": 0.0, "M": 0.0, "Q": 0.0}
+    worst = {"W": 0.0, "dW": 0.0, "M": 0.0, "Q": 0.0}
+    decay = 1.0 - 0.01 * 0.01
+    for rank in range(2):
+        R = res[rank]
+        for s in range(3):
+            for n, _, _ in W2_SHAPES:
+                before = "sinit" if s == 0 else f"s{s - 1}"
+                e = dw_err(R[f"hip_{before}_{n}_W"], R[f"hip_s{s}_{n}_W"], R[f"oracle_{before}_{n}_W"],
+                           R[f"oracle_s{s}_{n}_W"], decay)
+                worst["dW"] = max(worst["dW"], e)
+                assert e <= TOL_DW, (rank, s, n, e)
     for rank in range(2):
         assert max(res[rank]["hip_chunks"].tolist()) == 3, res[rank]["hip_chunks"]
         assert res[rank]["hip_chunks"].tolist() == res[rank]["oracle_chunks"].tolist()
         for key, v in res[rank].items():
-            if not key.startswith("hip_s"):
+            if not key.startswith("hip_s") or key.startswith("hip_sinit"):
                 continue
             ref = res[rank]["oracle" + key[3:]]
             e = maxrel(v, ref)

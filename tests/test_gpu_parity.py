@@ -393,6 +393,12 @@ def test_llama_shape_properties(m, n):
         ew = (1 - 1e-4) * (W0.double() @ u) - s * (Pd @ (Qd.t() @ u))
     assert maxrel(M.double() @ u, em) <= 1e-5
     assert maxrel(W.double() @ u, ew) <= 1e-5
+    # the weight step alone, scored on its own scale (W0 above dwarfs it): the deferred-EF
+    # schedule's update of a zero W is exactly -s P Qn^T (tests/test_gpu_update_precision.py)
+    Wz = torch.zeros(m, n, device=dev)
+    codec.ef_apply(None, [Wz], P, R, Qs, nz, 0.95, 0.01, 0.01, s, transposed)
+    upd = -s * ((Qd @ Pd.t()) if transposed else (Pd @ Qd.t()))
+    assert maxrel(Wz, upd) <= 1e-6, maxrel(Wz, upd)
 
 
 # ---------------------------------------------------------------------------------------------- deferred EF

@@ -72,6 +72,9 @@ def _worker(rank, world, port, out_dir):
     out["kat_untouched"] = torch.tensor(ga.tolist() == [1.0, 2.0] and gb.tolist() == [3.0])
     out["kat_none"] = torch.tensor(gn.dion_grad_norm_sq(opt_sum, [ga, gb], replica_group=dist.group.WORLD,
                                                         count_dion_grad=False) is None)
+    # local_bound under SUM: W sum_i ||G_i||^2 bounds ||sum_i G_i||^2 (here 2 * 28 = 56, exact 56)
+    out["kat_bound_sum"] = gn.dion_grad_norm_sq(opt_sum, [ga, gb], replica_group=dist.group.WORLD,
+                                                mode="local_bound")
     gen = torch.Generator().manual_seed(10 + rank)
     grads = [(torch.randn(48, 80, generator=gen) * 1e-3).to(torch.bfloat16),
              torch.randn(33, 17, generator=gen), (torch.randn(8, 8, generator=gen)).to(torch.bfloat16),
@@ -94,6 +97,7 @@ def test_gloo_w2_grad_norm_of_the_averaged_gradient():
     for r in range(2):
         assert res[r]["kat"].item() == 2.0 ** 2 + 4.0 ** 2 + 6.0 ** 2
         assert bool(res[r]["kat_untouched"]) and bool(res[r]["kat_none"])
+        assert res[r]["kat_bound_sum"].item() == 56.0 >= res[r]["kat"].item()
     # the reference's semantics: all-reduce(AVG) in the gradient dtype, then the fp64 sum of squares
     avg = [((a.float() + b.float()) / 2).to(a.dtype) if a.dtype == torch.bfloat16 else (a + b) / 2
            for a, b in zip(res[0]["grads"], res[1]["grads"])]
