@@ -138,6 +138,16 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// N independent wave sums in the butterfly order of wave_sum (bit-identical to N calls):
+// the N cross-lane permutes of a level are issued back to back, so their latencies overlap
+template <int N>
+__device__ __forceinline__ void wave_sum_n(float (&v)[N]) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += __shfl_xor(v[i], off, 64);
+}
+
 // Counter-based N(0,1) draw for the on-device sketch: two 32-bit outputs of a
 // splitmix64-style mix of (seed, row, col) feed Box-Muller.  Stateless, so any
 // tile of S can be regenerated anywhere without storing S in HBM.
@@ -1015,23 +1025,42 @@ __global__ void __launch_bounds__(256) householder_qr_kernel(const float* __rest
 //   does not raise; the fix-up's nan_to_num then zeroes those P columns).
 // ============================================================================
 template <typename XT>
-__device__ void tri_inverse_lds(const float* Rs, int rld, XT* Xs, int r, int tid) {
-  // X = R^-1 (upper): lane c = tid computes column c by back substitution;
-  // R is read by broadcast, X columns are lane-contiguous (conflict-free)
-  if (tid < r) {
-    const int c = tid;
-    for (int i = r - 1; i >= 0; --i) {
-      double acc = (i == c) ? 1.0 : 0.0;
-      for (int k = i + 1; k < r; ++k)
-        acc -= static_cast<double>(Rs[i * rld + k]) * static_cast<double>(Xs[k * r + c]);
-      Xs[i * r + c] = static_cast<XT>(acc / static_cast<double>(Rs[i * rld + i]));
-    }
+__device__ void tri_inverse_lds(const float* Rs, int rld, XT* Xs, int r, int tid, int nthreads) {
+  // X = R^-1 (upper) by back substitution, column c by a group of tpc lanes of one wave:
+  //   X[i][c] = ((i == c) - sum_{k=i+1..c} R[i][k] X[k][c]) / R[i][i],  i = c .. 0
+  // the group splits the k-sum (stride tpc) and combines it with xor shuffles; X[k][c] comes
+  // back from LDS, written by the group's lane 0 in an earlier i (same wave: LDS in order)
+  int tpc = 1;
+  while (tpc < 16 && 2 * tpc * r <= nthreads) tpc *= 2;
+  const int c = tid / tpc, p = tid % tpc;
+  const bool act = c < r;
+  for (int i = r - 1; i >= 0; --i) {
+    double acc = 0.0;
+    if (act && i < c)
+      for (int k = i + 1 + p; k <= c; k += tpc)
+        acc += static_cast<double>(Rs[i * rld + k]) * static_cast<double>(Xs[k * r + c]);
+    for (int off = tpc >> 1; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (act && p == 0)
+      Xs[i * r + c] = static_cast<XT>(i > c ? 0.0 : ((i == c ? 1.0 : 0.0) - acc) / static_cast<double>(Rs[i * rld + i]));
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
-template <int RPL, int CPW, typename XT>
+// Output of the factor kernels without the inverse (INV = false): per matrix the factor
+// padded to rt x rt (unit diagonal, zero off-diagonal past r) and then its rt reciprocal
+// diagonal entries, the operand layout of trsm_right_kernel<rt>.
+__device__ __forceinline__ void write_padded_factor(const float* Rs, int rld, int r, int rt, float* O, int tid,
+                                                    int nt) {
+  for (int idx = tid; idx < rt * rt; idx += nt) {
+    const int i = idx / rt, c = idx - i * rt;
+    O[idx] = (i < r && c < r) ? (c >= i ? Rs[i * rld + c] : 0.f) : (i == c ? 1.f : 0.f);
+  }
+  for (int j = tid; j < rt; j += nt) O[rt * rt + j] = j < r ? 1.f / Rs[j * rld + j] : 1.f;
+}
+
+template <int RPL, int CPW, typename XT, bool INV = true>
 __global__ void __launch_bounds__(256) sketch_qr_inv_kernel(const float* __restrict__ SP, float* __restrict__ Rinv,
-                                                            int K, int r) {
+                                                            int K, int r, int rt = 0) {
   extern __shared__ __attribute__((aligned(16))) char qsm[];
   const int rld = r + 1;
   float* vbuf = reinterpret_cast<float*>(qsm);         // 2 x 256
@@ -1102,73 +1131,105 @@ __global__ void __launch_bounds__(256) sketch_qr_inv_kernel(const float* __restr
     float v[RPL];
 #pragma unroll
     for (int s = 0; s < RPL; ++s) v[s] = vbuf[buf * 256 + lane + 64 * s];
+    // H_j on this wave's live columns; consumed columns were shifted out and are zero, so a
+    // column past `rem` takes d = 0 and stays zero.  The column sums of a pivot are reduced
+    // together (wave_sum_n), over the first 4, 8 or all CPW columns as `rem` allows
     const int rem = n_w - consumed;
+    auto trail = [&](auto NCc) {
+      constexpr int NC = decltype(NCc)::value;
+      float d[NC];
 #pragma unroll
-    for (int cc = 0; cc < CPW; ++cc) {
-      if (cc < rem) {
-        float d = 0.f;
+      for (int cc = 0; cc < NC; ++cc) {
+        d[cc] = 0.f;
 #pragma unroll
-        for (int s = 0; s < RPL; ++s) d += v[s] * A[s][cc];
-        d = wave_sum(d) * tau;
-#pragma unroll
-        for (int s = 0; s < RPL; ++s) A[s][cc] -= d * v[s];
+        for (int s = 0; s < RPL; ++s) d[cc] += v[s] * A[s][cc];
       }
-    }
+      wave_sum_n<NC>(d);
+#pragma unroll
+      for (int cc = 0; cc < NC; ++cc) {
+        const float dt = d[cc] * tau;
+#pragma unroll
+        for (int s = 0; s < RPL; ++s) A[s][cc] -= dt * v[s];
+      }
+    };
+    if (rem > CPW / 2)
+      trail(std::integral_constant<int, CPW>{});
+    else if (rem > CPW / 4 || CPW < 8)
+      trail(std::integral_constant<int, (CPW / 2 > 0 ? CPW / 2 : 1)>{});
+    else if (rem > 0)
+      trail(std::integral_constant<int, (CPW / 4 > 0 ? CPW / 4 : 1)>{});
   }
   __syncthreads();
-  tri_inverse_lds<XT>(Rs, rld, Xs, r, tid);
+  if constexpr (!INV) {
+    write_padded_factor(Rs, rld, r, rt, Rinv + static_cast<long>(b) * (rt * rt + rt), tid, blockDim.x);
+    return;
+  }
+  tri_inverse_lds<XT>(Rs, rld, Xs, r, tid, blockDim.x);
   __syncthreads();
   float* O = Rinv + static_cast<long>(b) * r * r;
   for (int idx = tid; idx < r * r; idx += blockDim.x) O[idx] = static_cast<float>(Xs[idx]);
 }
 
-template <typename XT>
+template <typename XT, bool INV = true>
 __global__ void __launch_bounds__(256) chol_inv_kernel(const float* __restrict__ G_in, float* __restrict__ Uinv,
-                                                       int r) {
+                                                       int r, int rt = 0) {
+  // Right-looking upper Cholesky: at pivot j the whole block updates the trailing upper
+  // triangle, G[i][c] -= u_ji u_jc (u_j* = row j / sqrt(d_j)), one barrier per pivot.  Every
+  // element receives the same fused products in the same order (k = 0, 1, ..) as the
+  // left-looking dpotf2 dot products, so the factor is the same.  Factor row j is parked
+  // transposed in the strictly lower triangle (G[c][j] = u_jc, never read by the upper
+  // updates) and its diagonal in ud[], then moved to the upper triangle for the inverse.
   extern __shared__ __attribute__((aligned(16))) char csm[];
   const int ld = r + 1;
-  float* Us = reinterpret_cast<float*>(csm);       // r x ld
-  float* bc = Us + r * ld;                          // pivot broadcast (+pad)
-  XT* Xs = reinterpret_cast<XT*>(csm + ((sizeof(float) * (r * ld + 4) + 15) / 16) * 16);
+  float* Gs = reinterpret_cast<float*>(csm);       // r x ld
+  float* ud = Gs + r * ld;                          // r: the factor's diagonal
+  XT* Xs = reinterpret_cast<XT*>(csm + ((sizeof(float) * (r * ld + r + 4) + 15) / 16) * 16);
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
+  const int nt = blockDim.x;
   const float* Gm = G_in + static_cast<long>(b) * r * r;
-  for (int idx = tid; idx < r * r; idx += blockDim.x) {
+  for (int idx = tid; idx < r * r; idx += nt) {
     const int i = idx / r, c = idx - i * r;
-    Us[i * ld + c] = Gm[idx];
+    Gs[i * ld + c] = (c >= i) ? Gm[idx] : 0.f;
   }
-  __syncthreads();
   int jf = r;
   for (int j = 0; j < r; ++j) {
-    float sacc = 0.f;
-    if (tid < r && tid >= j) {
-      sacc = Us[j * ld + tid];
-      for (int k = 0; k < j; ++k) sacc -= Us[k * ld + j] * Us[k * ld + tid];
-    }
-    if (tid == j) bc[0] = sacc;
     __syncthreads();
-    const float d = bc[0];
+    const float d = Gs[j * ld + j];
     if (!(d > 0.f)) {  // uniform
       jf = j;
       break;
     }
     const float ujj = sqrtf(d);
     const float inv = 1.f / ujj;
-    if (tid < r && tid > j) Us[j * ld + tid] = sacc * inv;
-    if (tid == j) Us[j * ld + j] = ujj;
-    __syncthreads();
-  }
-  // zero the strictly lower part, keep the factored rows
-  for (int idx = tid; idx < r * r; idx += blockDim.x) {
-    const int i = idx / r, c = idx - i * r;
-    if (i > c) Us[i * ld + c] = 0.f;
-    if (i >= jf && i <= c) Us[i * ld + c] = (i == c) ? 1.f : 0.f;  // placeholder rows, poisoned below
+    if (tid == 0) ud[j] = ujj;
+    for (int c = j + 1 + tid; c < r; c += nt) Gs[c * ld + j] = Gs[j * ld + c] * inv;
+    // trailing update: lane tid % 64 takes columns c, the block's 4 waves split the rows
+    for (int c = j + 1 + (tid & 63); c < r; c += 64) {
+      const float ujc = Gs[j * ld + c] * inv;
+      for (int i = j + 1 + (tid >> 6); i <= c; i += nt >> 6)
+        Gs[i * ld + c] -= (Gs[j * ld + i] * inv) * ujc;
+    }
   }
   __syncthreads();
-  tri_inverse_lds<XT>(Us, ld, Xs, r, tid);
+  // factor rows to the upper triangle; rows from a failed pivot on: placeholders whose
+  // columns are poisoned with NaN (cholesky_ex does not raise; the fix-up's nan_to_num then
+  // zeroes those P columns): in the inverse below, or through a NaN diagonal for the solve
+  for (int idx = tid; idx < r * r; idx += nt) {
+    const int i = idx / r, c = idx - i * r;
+    if (c < i) continue;
+    Gs[i * ld + c] = (i >= jf) ? (i == c ? (INV ? 1.f : __builtin_nanf("")) : 0.f)
+                               : (i == c ? ud[i] : Gs[c * ld + i]);
+  }
+  __syncthreads();
+  if constexpr (!INV) {
+    write_padded_factor(Gs, ld, r, rt, Uinv + static_cast<long>(b) * (rt * rt + rt), tid, nt);
+    return;
+  }
+  tri_inverse_lds<XT>(Gs, ld, Xs, r, tid, nt);
   __syncthreads();
   float* O = Uinv + static_cast<long>(b) * r * r;
-  for (int idx = tid; idx < r * r; idx += blockDim.x) {
+  for (int idx = tid; idx < r * r; idx += nt) {
     const int c = idx % r;
     O[idx] = (c >= jf) ? __builtin_nanf("") : static_cast<float>(Xs[idx]);
   }
@@ -2051,6 +2112,161 @@ __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_st
       cur ^= 1;
     }
   }
+}
+
+// ============================================================================
+// X_b = P_b R_b^-1 for an upper-triangular R_b: the triangular solves of the RCQR
+// (ortho.py:105-121, torch.linalg.solve_triangular(R, P, upper=True, left=False)), one row
+// per thread as the reference BLAS strsm (right, upper, no transpose) orders it:
+//   x_j = (p_j - sum_{k<j} R_kj x_k) * (1 / R_jj)
+// with the subtractions in k order (right-looking: once x_k is final, every later x_j takes
+// its fused term).  R (the factor kernels' padded RT x RT layout plus reciprocal diagonal)
+// is read with uniform loads, so the vector traffic is the row in and out; columns past r
+// are zero and stay zero.  In place (src == dst) is allowed.
+// ============================================================================
+template <int RT>
+__global__ void __launch_bounds__(256) trsm_right_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                         const float* __restrict__ Rf, int mp, int r) {
+  const int b = blockIdx.y;
+  const long row = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
+  if (row >= mp) return;
+  const float* __restrict__ R = Rf + static_cast<long>(b) * (RT * RT + RT);
+  const float* p = src + (static_cast<long>(b) * mp + row) * r;
+  float x[RT];
+  if ((r & 3) == 0) {
+#pragma unroll
+    for (int j = 0; j < RT; j += 4) {
+      if (j < r) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(p + j);
+        x[j] = v[0], x[j + 1] = v[1], x[j + 2] = v[2], x[j + 3] = v[3];
+      } else {
+        x[j] = x[j + 1] = x[j + 2] = x[j + 3] = 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < RT; ++j) x[j] = j < r ? p[j] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < RT; ++k) {
+    x[k] *= R[RT * RT + k];
+#pragma unroll
+    for (int j = k + 1; j < RT; ++j) x[j] = fmaf(-x[k], R[k * RT + j], x[j]);
+  }
+  float* q = dst + (static_cast<long>(b) * mp + row) * r;
+  if ((r & 3) == 0) {
+#pragma unroll
+    for (int j = 0; j < RT; j += 4)
+      if (j < r) *reinterpret_cast<f32x4*>(q + j) = f32x4{x[j], x[j + 1], x[j + 2], x[j + 3]};
+  } else {
+#pragma unroll
+    for (int j = 0; j < RT; ++j)
+      if (j < r) q[j] = x[j];
+  }
+}
+
+// ============================================================================
+// S P for a generated sketch (ortho.py:90-104: SP = sketch @ P, k = ceil(1.25 r / 128) 128
+// rows).  The reference draws S ~ N(0, 1/k) from the unseeded global RNG (ortho.py:659-661),
+// so any draw is as valid as its own, and the randomised Cholesky QR returns the same
+// orthonormal P up to column signs for every full-rank sketch.  Here S is
+// a Rademacher sketch, S[k][i] = +-1/sqrt(k) with the sign the bit (i mod 32) of a 32-bit
+// hash of (seed, matrix, k, i / 32): exact in bf16, so one operand of the product needs no
+// split, P is split into three bf16 limbs (24 bits), and S P is three bf16 MFMAs per tile
+// instead of the fp32 MFMA (16x slower) with a Box-Muller draw per element.
+//   v_mfma_f32_32x32x16_bf16: A = S tile (32 sketch rows x 16 P rows, from the sign
+//   bits), B = P tile (16 rows x 32 columns, 8 rows of one column per lane, coalesced
+//   across the 32 lanes of a row).  A block takes kchunk rows of one matrix; wave w owns
+//   sketch-row tiles w, w + 4 (KT4 of them) and all NT column tiles, so no cross-wave
+//   reduction; partial sums go to fixed-order slabs (reduce_slabs_kernel).
+// ============================================================================
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// 8 sign bits -> 8 bf16 values +-1 (bit j set: element j is -1)
+__device__ __forceinline__ bf16x8 signs_bf16x8(uint32_t bits) {
+  u32x4 w;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t v = bits >> (2 * q);
+    w[q] = 0x3F803F80u | ((v & 1u) << 15) | ((v & 2u) << 30);
+  }
+  return __builtin_bit_cast(bf16x8, w);
+}
+
+struct SketchArgs {
+  const float* P;   // (batch, mp, r)
+  float* out;       // (batch, nchunk, K, r) partial sums (the final (batch, K, r) when nchunk == 1)
+  uint64_t seed;
+  float scale;      // 1 / sqrt(K)
+  int mp, r, K, kchunk, nchunk;
+};
+
+template <int KT4, int NT>
+__global__ void __launch_bounds__(256) sketch_rad_kernel(const SketchArgs a) {
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63, t = lane & 31, h = lane >> 5;
+  const int i_begin = chunk * a.kchunk;
+  const int i_end = min(a.mp, i_begin + a.kchunk);
+  const int r = a.r;
+  const float* __restrict__ Pb = a.P + static_cast<long>(b) * a.mp * r;
+  const uint32_t sb = hash32(static_cast<uint32_t>(a.seed) ^ hash32(static_cast<uint32_t>(a.seed >> 32) +
+                                                                      0x9E3779B9u * static_cast<uint32_t>(b + 1)));
+  uint32_t hk[KT4];
+#pragma unroll
+  for (int q = 0; q < KT4; ++q) hk[q] = hash32(sb + 0x85EBCA6Bu * static_cast<uint32_t>(32 * (wave + 4 * q) + t));
+  f32x16 acc[KT4][NT];
+#pragma unroll
+  for (int q = 0; q < KT4; ++q)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[q][nt][e] = 0.f;
+  for (int i0 = i_begin; i0 < i_end; i0 += 16) {
+    Split3 B[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int col = 32 * nt + t;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = i0 + 8 * h + j;
+        v[j] = (row < i_end && col < r) ? Pb[static_cast<long>(row) * r + col] : 0.f;
+      }
+      split3(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, 1.f, B[nt]);
+    }
+#pragma unroll
+    for (int q = 0; q < KT4; ++q) {
+      const uint32_t bits = hash32(hk[q] ^ (0xC2B2AE35u * static_cast<uint32_t>(i0 >> 5)));
+      const bf16x8 S = signs_bf16x8(bits >> ((i0 & 16) + 8 * h));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        acc[q][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(S, B[nt].lo, acc[q][nt], 0, 0, 0);
+        acc[q][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(S, B[nt].mid, acc[q][nt], 0, 0, 0);
+        acc[q][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(S, B[nt].hi, acc[q][nt], 0, 0, 0);
+      }
+    }
+  }
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + chunk) * a.K * r;
+#pragma unroll
+  for (int q = 0; q < KT4; ++q)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int col = 32 * nt + t;
+      if (col >= r) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int krow = 32 * (wave + 4 * q) + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (krow < a.K) out[static_cast<long>(krow) * r + col] = acc[q][nt][e] * a.scale;
+      }
+    }
 }
 
 // ============================================================================
@@ -4125,6 +4341,24 @@ int sketch_k(int r, float oversample) {
   return static_cast<int>(ceil(static_cast<double>(oversample) * r / 128.0)) * 128;
 }
 
+// sketch_rad_kernel: ~512 blocks over the batch (2 per CU), 16-row aligned row chunks
+Geo sketch_rad_geo(int mp, int K, int batch) {
+  Geo g;
+  const long want = ceil_div(512L, batch > 0 ? batch : 1);
+  const long maxc = ceil_div(mp, 256);
+  long nc = want < maxc ? want : maxc;
+  if (nc < 1) nc = 1;
+  g.kchunk = round_up(ceil_div(mp, nc), 16);
+  g.nchunk = static_cast<int>(ceil_div(mp, g.kchunk));
+  g.gx = g.nchunk;
+  g.out_rows = K;
+  return g;
+}
+
+// the padded order of trsm_right_kernel and its factor layout (rt x rt + rt floats per matrix)
+int trsm_rt(int r) { return r <= 32 ? 32 : (r <= 64 ? 64 : 128); }
+size_t factor_floats(int r) { return static_cast<size_t>(trsm_rt(r)) * (trsm_rt(r) + 1); }
+
 struct OrthoPlan {
   bool plain_qr;
   int k;
@@ -4145,13 +4379,15 @@ OrthoPlan ortho_plan(int mp, int r, int batch, float oversample) {
     off += (bytes + 255) / 256 * 256;
     return o;
   };
-  p.off_sk_slab = take(slab_bytes(p.sk, batch, r));
+  const Geo rad = sketch_rad_geo(mp, p.k, batch);
+  const size_t rad_slab = rad.nchunk > 1 ? sizeof(float) * static_cast<size_t>(batch) * rad.nchunk * p.k * r : 0;
+  p.off_sk_slab = take(std::max(slab_bytes(p.sk, batch, r), rad_slab));
   p.off_sp = take(sizeof(float) * static_cast<size_t>(batch) * p.k * r);
   p.off_r1 = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
   p.off_gslab = take(slab_bytes(p.gr, batch, r));
   p.off_g = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
   p.off_r2 = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
-  p.off_inv = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
+  p.off_inv = take(sizeof(float) * static_cast<size_t>(batch) * std::max(static_cast<size_t>(r) * r, factor_floats(r)));
   p.off_p1 = take(sizeof(float) * static_cast<size_t>(batch) * mp * r);
   p.total = off;
   return p;
@@ -4387,7 +4623,9 @@ int allow_lds(K kernel, size_t bytes) {
   return DION_OK;
 }
 
-int launch_sketch_qr_inv(const float* SP, float* Rinv, int K, int r, int batch, hipStream_t st) {
+// inv: R^-1 (r x r, the distributed RCQR's exchange format); else the padded factor for
+// trsm_right_kernel (factor_floats(r) per matrix)
+int launch_sketch_qr_inv(const float* SP, float* Rinv, int K, int r, int batch, hipStream_t st, bool inv = true) {
   if (K > 256 || r > 128 || r > K) return fail(DION_E_UNSUPPORTED, "sketch QR %dx%d", K, r);
   const bool dbl = r <= 64;
   const size_t lds = ((sizeof(float) * (520 + static_cast<size_t>(r) * (r + 1)) + 15) / 16) * 16 +
@@ -4396,9 +4634,16 @@ int launch_sketch_qr_inv(const float* SP, float* Rinv, int K, int r, int batch, 
     constexpr int RPLv = decltype(RPLc)::value;
     constexpr int CPWv = decltype(CPWc)::value;
     using XTv = typename decltype(XTc)::type;
+    if (!inv) {
+      int rc = allow_lds(sketch_qr_inv_kernel<RPLv, CPWv, XTv, false>, lds);
+      if (rc != DION_OK) return rc;
+      hipLaunchKernelGGL((sketch_qr_inv_kernel<RPLv, CPWv, XTv, false>), dim3(batch), dim3(256), lds, st, SP, Rinv,
+                         K, r, trsm_rt(r));
+      return check_launch("sketch_qr");
+    }
     int rc = allow_lds(sketch_qr_inv_kernel<RPLv, CPWv, XTv>, lds);
     if (rc != DION_OK) return rc;
-    hipLaunchKernelGGL((sketch_qr_inv_kernel<RPLv, CPWv, XTv>), dim3(batch), dim3(256), lds, st, SP, Rinv, K, r);
+    hipLaunchKernelGGL((sketch_qr_inv_kernel<RPLv, CPWv, XTv>), dim3(batch), dim3(256), lds, st, SP, Rinv, K, r, 0);
     return check_launch("sketch_qr_inv");
   };
   struct D { using type = double; };
@@ -4413,21 +4658,78 @@ int launch_sketch_qr_inv(const float* SP, float* Rinv, int K, int r, int batch, 
   return go(std::integral_constant<int, 4>{}, std::integral_constant<int, 32>{}, F{});
 }
 
-int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t st) {
+int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t st, bool inv = true) {
   const bool dbl = r <= 96;
-  const size_t lds = ((sizeof(float) * (static_cast<size_t>(r) * (r + 1) + 4) + 15) / 16) * 16 +
+  const size_t lds = ((sizeof(float) * (static_cast<size_t>(r) * (r + 1) + r + 4) + 15) / 16) * 16 +
                      (dbl ? sizeof(double) : sizeof(float)) * static_cast<size_t>(r) * r;
-  const int threads = r <= 64 ? 64 : (r <= 128 ? 128 : 256);
+  const int threads = 256;
+  if (!inv) {
+    int rc = allow_lds(chol_inv_kernel<float, false>, lds);
+    if (rc != DION_OK) return rc;
+    hipLaunchKernelGGL((chol_inv_kernel<float, false>), dim3(batch), dim3(threads), lds, st, G, Uinv, r, trsm_rt(r));
+    return check_launch("chol");
+  }
   if (dbl) {
     int rc = allow_lds(chol_inv_kernel<double>, lds);
     if (rc != DION_OK) return rc;
-    hipLaunchKernelGGL((chol_inv_kernel<double>), dim3(batch), dim3(threads), lds, st, G, Uinv, r);
+    hipLaunchKernelGGL((chol_inv_kernel<double>), dim3(batch), dim3(threads), lds, st, G, Uinv, r, 0);
   } else {
     int rc = allow_lds(chol_inv_kernel<float>, lds);
     if (rc != DION_OK) return rc;
-    hipLaunchKernelGGL((chol_inv_kernel<float>), dim3(batch), dim3(threads), lds, st, G, Uinv, r);
+    hipLaunchKernelGGL((chol_inv_kernel<float>), dim3(batch), dim3(threads), lds, st, G, Uinv, r, 0);
   }
   return check_launch("chol_inv");
+}
+
+// dst_b = src_b R_b^-1 by forward substitution (trsm_right_kernel; factor from the INV = false
+// factor kernels)
+int launch_trsm(const float* src, float* dst, const float* fac, int mp, int r, int batch, hipStream_t st) {
+  const dim3 grid(static_cast<unsigned>(ceil_div(mp, 256)), batch);
+  switch (trsm_rt(r)) {
+    case 32: hipLaunchKernelGGL((trsm_right_kernel<32>), grid, dim3(256), 0, st, src, dst, fac, mp, r); break;
+    case 64: hipLaunchKernelGGL((trsm_right_kernel<64>), grid, dim3(256), 0, st, src, dst, fac, mp, r); break;
+    default: hipLaunchKernelGGL((trsm_right_kernel<128>), grid, dim3(256), 0, st, src, dst, fac, mp, r); break;
+  }
+  return check_launch("trsm_right");
+}
+
+// S P with the generated Rademacher sketch (sketch_rad_kernel), reduced into out (batch, K, r)
+int run_sketch_rad(const float* P, int mp, int K, int r, int batch, uint64_t seed, float* out, void* slab,
+                   hipStream_t st) {
+  const Geo g = sketch_rad_geo(mp, K, batch);
+  SketchArgs a;
+  memset(&a, 0, sizeof(a));
+  a.P = P;
+  a.out = g.nchunk > 1 ? static_cast<float*>(slab) : out;
+  a.seed = seed;
+  a.scale = 1.0f / sqrtf(static_cast<float>(K));
+  a.mp = mp;
+  a.r = r;
+  a.K = K;
+  a.kchunk = g.kchunk;
+  a.nchunk = g.nchunk;
+  const dim3 grid(static_cast<unsigned>(g.nchunk), batch);
+  auto go = [&](auto KTc, auto NTc) {
+    constexpr int KT = decltype(KTc)::value, NT = decltype(NTc)::value;
+    hipLaunchKernelGGL((sketch_rad_kernel<KT, NT>), grid, dim3(256), 0, st, a);
+    return check_launch("sketch_rad");
+  };
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  int rc;
+  const int nt = (r + 31) / 32;
+  if (K == 128) {
+    rc = nt == 1 ? go(I1{}, I1{}) : nt == 2 ? go(I1{}, I2{}) : nt == 3 ? go(I1{}, I3{}) : go(I1{}, I4{});
+  } else if (K == 256) {
+    rc = nt == 1 ? go(I2{}, I1{}) : nt == 2 ? go(I2{}, I2{}) : nt == 3 ? go(I2{}, I3{}) : go(I2{}, I4{});
+  } else {
+    return fail(DION_E_UNSUPPORTED, "generated sketch with k=%d rows", K);
+  }
+  if (rc != DION_OK) return rc;
+  if (g.nchunk > 1) return launch_reduce(out, static_cast<const float*>(slab), g.nchunk, static_cast<long>(K) * r, batch, st);
+  return DION_OK;
 }
 
 // dst_b = src_b Uinv_b for every matrix (m_P x r times r x r), an MFMA row projection
@@ -4870,27 +5172,30 @@ int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, u
     if (lds > 160 * 1024) return fail(DION_E_UNSUPPORTED, "sketch QR of %dx%d does not fit LDS", K, r);
     rc = allow_lds(householder_qr_kernel, lds);
     if (rc != DION_OK) return rc;
-    // (1) S P  (K x r)
-    const float std_ = sqrtf(1.0f / static_cast<float>(K));
-    rc = run_panel(sketch ? 1 : 2, mp, K, r, nb, Pb, sketch ? sketch + static_cast<long>(b0) * K * mp : nullptr,
-                   seed + 0x9E3779B97F4A7C15ull * static_cast<uint64_t>(b0), std_, sp, sk_slab, plan.sk, st);
+    // (1) S P  (K x r): the caller's sketch (parity replays), else a generated Rademacher one
+    const uint64_t bseed = seed + 0x9E3779B97F4A7C15ull * static_cast<uint64_t>(b0);
+    if (sketch)
+      rc = run_panel(1, mp, K, r, nb, Pb, sketch + static_cast<long>(b0) * K * mp, bseed,
+                     sqrtf(1.0f / static_cast<float>(K)), sp, sk_slab, plan.sk, st);
+    else
+      rc = run_sketch_rad(Pb, mp, K, r, nb, bseed, sp, sk_slab, st);
     if (rc != DION_OK) return rc;
-    float* uinv = reinterpret_cast<float*>(base + plan.off_inv);
+    float* fac = reinterpret_cast<float*>(base + plan.off_inv);
     float* p1 = reinterpret_cast<float*>(base + plan.off_p1);
-    // (2) R1^-1 with R1 = qr(S P).R, (3) P1 = P R1^-1  (into workspace)
-    rc = launch_sketch_qr_inv(sp, uinv, K, r, nb, st);
+    // (2) R1 = qr(S P).R, (3) P1 = P R1^-1 by forward substitution (into workspace)
+    rc = launch_sketch_qr_inv(sp, fac, K, r, nb, st, false);
     if (rc != DION_OK) return rc;
     (void)r1;
-    rc = apply_right(Pb, p1, uinv, mp, r, nb, st);
+    rc = launch_trsm(Pb, p1, fac, mp, r, nb, st);
     if (rc != DION_OK) return rc;
     // (4) Gram = P1^T P1, (5) R2 = chol_upper(Gram)
     rc = run_panel(0, mp, r, r, nb, p1, nullptr, 0, 0.f, gm, gslab, plan.gr, st);
     if (rc != DION_OK) return rc;
-    // (5) R2^-1 with R2 = chol_upper(Gram), (6) P = P1 R2^-1  (back into the caller's buffer)
-    rc = launch_chol_inv(gm, uinv, r, nb, st);
+    rc = launch_chol_inv(gm, fac, r, nb, st, false);
     if (rc != DION_OK) return rc;
     (void)r2;
-    rc = apply_right(p1, Pb, uinv, mp, r, nb, st);
+    // (6) P = P1 R2^-1 (back into the caller's buffer)
+    rc = launch_trsm(p1, Pb, fac, mp, r, nb, st);
     if (rc != DION_OK) return rc;
   }
   // ortho.py:123: the fp32 result is cast back to P's dtype

@@ -272,12 +272,13 @@ class MegatronDion(Optimizer):
         if not all(getattr(b.params[0], "is_cuda", False) for b in batches):
             return False
         dev = batches[0].params[0].device
-        if self._pstreams is None or self._pstreams[0].device != dev:
-            self._pstreams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
-        S, L = self._pstreams
+        ns = max(1, self._local_streams - 1)  # streaming streams; the last one is the latency stream
+        if self._pstreams is None or len(self._pstreams) != ns + 1 or self._pstreams[0].device != dev:
+            self._pstreams = [torch.cuda.Stream(device=dev) for _ in range(ns + 1)]
+        Ss, L = self._pstreams[:ns], self._pstreams[ns]
         main = torch.cuda.current_stream(dev)
-        S.wait_stream(main)
-        L.wait_stream(main)
+        for s in self._pstreams:
+            s.wait_stream(main)
 
         def advance(gen, stream):
             with torch.cuda.stream(stream):
@@ -286,8 +287,17 @@ class MegatronDion(Optimizer):
                 except StopIteration:
                     return None
 
-        pending = []
-        for b in batches:
+        def finish(entry):
+            g0, e0, s0 = entry
+            s0.wait_event(e0)
+            if advance(g0, s0) is not None:
+                raise RuntimeError("[DION_INTERNAL] pipelined batch yielded after its phases")
+
+        # group k streams on Ss[k % ns]; each streaming stream keeps `lookahead` groups' pass A
+        # ahead of their pass B, so it never waits for its own group's orthonormalisation
+        pending = [[] for _ in range(ns)]
+        for k, b in enumerate(batches):
+            S = Ss[k % ns]
             gen = run_dion_batch_async(self, b, sketches=sketches(b) if sketches else None, phase_marks=True)
             if advance(gen, S) != "ortho":
                 continue
@@ -298,18 +308,15 @@ class MegatronDion(Optimizer):
                 raise RuntimeError("[DION_INTERNAL] pipelined batch lost its phase marks")
             done = torch.cuda.Event()
             done.record(L)
-            pending.append((gen, done))
-            while len(pending) > self._pipeline_lookahead:
-                g0, e0 = pending.pop(0)
-                S.wait_event(e0)
-                if advance(g0, S) is not None:
-                    raise RuntimeError("[DION_INTERNAL] pipelined batch yielded after its phases")
-        for g0, e0 in pending:
-            S.wait_event(e0)
-            if advance(g0, S) is not None:
-                raise RuntimeError("[DION_INTERNAL] pipelined batch yielded after its phases")
-        main.wait_stream(S)
-        main.wait_stream(L)
+            q = pending[k % ns]
+            q.append((gen, done, S))
+            while len(q) > self._pipeline_lookahead:
+                finish(q.pop(0))
+        for q in pending:
+            for entry in q:
+                finish(entry)
+        for s in self._pstreams:
+            main.wait_stream(s)
         return True
 
     def _replica_streams(self, batches, width):

@@ -182,9 +182,6 @@ def check_supported_batch(optimizer, *, batch_group, batch_collectives, configs,
                 not len(tuple(getattr(batch_collectives, "fs_p_collectives", None) or ()))
                 or getattr(batch_group, "q_norm_group", None) is None):
             why = "an FS-sharded fsdp_tp batch without its FS P reduction and q_norm group"
-        elif any(optimizer_states[i] is not None and getattr(optimizer_states[i].get("momentum"), "dtype", None)
-                 == torch.bfloat16 for i in range(int(real_batch_size))):
-            why = "bf16 momentum with the fsdp_tp kind (not built)"
     elif getattr(batch_group, "ortho_group", None) is not None and world(batch_group.ortho_group) > 1:
         why = "a distributed ortho_group (TP-sharded P)"
     elif tp_colls or any(bool(getattr(c, "use_tp_shard", False)) for c in configs[:int(real_batch_size)]):
@@ -197,9 +194,6 @@ def check_supported_batch(optimizer, *, batch_group, batch_collectives, configs,
             why = "an fsdp batch with entries that are not FS shards"
         elif len(param_shapes) != int(fs.world_size) or len(tuple(fs.indices)) != len(param_shapes):
             why = f"fsdp batch size {len(param_shapes)} != FS world {fs.world_size} ([DION_FSONLY_BATCH_SIZE_MISMATCH])"
-        elif any(optimizer_states[i] is not None and getattr(optimizer_states[i].get("momentum"), "dtype", None)
-                 == torch.bfloat16 for i in range(int(real_batch_size))):
-            why = "bf16 momentum with the fsdp kind (not built)"
     else:
         if getattr(batch_group, "q_norm_group", None) is not None and world(batch_group.q_norm_group) > 1:
             why = "a q_norm_group on a ddp batch (FS-sharded column norm)"
@@ -318,6 +312,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     mp, nq = factor_rows(m, n, transposed)
     dev = momentums[0].device
     oversample = float(optimizer.defaults["rcqr_oversample"])
+    Qs, commit_qs = _qs_in_state_dtype(list(Qs), real, momentums[0].dtype)
     # bf16 momentum and Q (the speedrun's DionMixedPrecisionConfig): P and R stay fp32
     # buffers of bf16 values; the kernels round where the reference's bf16 tensors round,
     # and an averaging collective is followed by the same rounding (round_bf16)
@@ -459,6 +454,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     else:
         codec.ef_apply(list(momentums[:real]), list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd,
                        scaled, transposed)
+    commit_qs()
     if commit_updates is not None:
         for i in range(real):
             if commit_updates[i] is not None:
@@ -506,11 +502,15 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     mp, nq = factor_rows(m, n, transposed)
     dev = momentums[0].device
     oversample = float(optimizer.defaults["rcqr_oversample"])
+    Qs, commit_qs = _qs_in_state_dtype(list(Qs), real, momentums[0].dtype)
+    # bf16 momentum and Q (the speedrun's FS = 4 recipe): P and R stay fp32 buffers of bf16
+    # values, rounded where the reference's bf16 tensors round (after each reduction)
+    bf16_state = momentums[0].dtype == torch.bfloat16
     P = torch.zeros((B, mp, r), dtype=torch.float32, device=dev)
     nonzero = torch.zeros((B,), dtype=torch.int32, device=dev)
     defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
              and (commit_updates is None or all(c is None for c in commit_updates[:real]))
-             and codec.supports_deferred_ef(m, n, r, transposed))
+             and not bf16_state and codec.supports_deferred_ef(m, n, r, transposed))
     _project_with_pending(codec, real_grads, momentums, Qs, P, nonzero, optimizer_states, real, m, n, transposed,
                           defer)
     # reduce-scatter(sum): this rank receives entry fs_rank summed over the FS shards
@@ -518,10 +518,14 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     work = dist.reduce_scatter_tensor(P_own, P, op=dist.ReduceOp.SUM, group=fs_group, async_op=True)
     yield
     work.wait()
+    if bf16_state:
+        codec.round_bf16(P_own)
     if use_low_rank and rworld > 1:
         work = dist.all_reduce(P_own, op=dist.ReduceOp.AVG, group=rgroup, async_op=True)  # runtime.py:367-369
         yield
         work.wait()
+        if bf16_state:
+            codec.round_bf16(P_own)
     own = indices[fs_rank]
     if own >= real or dist_metas[own] is None:
         P_own.zero_()  # a padded entry stays inert (runtime.py:1242-1248)
@@ -545,6 +549,8 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=rgroup, async_op=True)
         yield
         work.wait()
+        if bf16_state:
+            codec.round_bf16(R)
     colsum = torch.empty((real, r), dtype=torch.float32, device=dev)
     codec.fixup_colsum(P, R, list(Qs[:real]), nonzero, colsum, m, n, transposed)
     qgroup = getattr(batch_group, "q_norm_group", None)
@@ -554,7 +560,7 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         work.wait()
     codec.colnorm_apply(R, list(Qs[:real]), colsum, float(optimizer.defaults["epsilon"]), m, n, transposed)
     _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim_groups, optimizer_states,
-                   dist_metas, real, m, n, transposed, defer, commit_updates)
+                   dist_metas, real, m, n, transposed, defer, commit_updates, commit_qs)
 
 
 def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, optim_groups, real_grads,
@@ -586,6 +592,8 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     transposed = bool(configs[0].is_transposed)
     mp, nq = factor_rows(m, n, transposed)
     dev = momentums[0].device
+    bf16_state = momentums[0].dtype == torch.bfloat16  # P, R round after reductions
+    qdt = momentums[0].dtype  # Q computes in the momentum's dtype (runtime.py:1576-1590), commits in its own
     # Q unshard: all-gather this rank's columns (padded to the widest rank) over TP
     gath = batch_collectives.tp_q_gathers[0]
     tp_group, T, tp_rank = gath.process_group, int(gath.world_size), int(gath.rank)
@@ -599,15 +607,15 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         if tuple(Qs[i].shape) != (nq, c1 - c0):
             raise RuntimeError(f"[DION_Q_UNSHARD_LOCAL_RANK_MISMATCH] step={optimizer._step_count} entry={i} "
                                f"local_shape={tuple(Qs[i].shape)} expected={(nq, c1 - c0)} r={r} tp={T}")
-    local = torch.zeros((B, nq, widest), dtype=torch.float32, device=dev)
+    local = torch.zeros((B, nq, widest), dtype=qdt, device=dev)
     for i in range(B):
         local[i, :, :c1 - c0].copy_(Qs[i])
-    gathered = torch.empty((T * B, nq, widest), dtype=torch.float32, device=dev)
+    gathered = torch.empty((T * B, nq, widest), dtype=qdt, device=dev)
     work = dist.all_gather_into_tensor(gathered, local, group=tp_group, async_op=True)
     yield
     work.wait()
     gathered = gathered.view(T, B, nq, widest)
-    Qfull = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
+    Qfull = torch.empty((B, nq, r), dtype=qdt, device=dev)
     for k, (a, b) in enumerate(cols):
         Qfull[:, :, a:b].copy_(gathered[k, :, :, :b - a])
     del local, gathered
@@ -616,7 +624,7 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     nonzero = torch.zeros((B,), dtype=torch.int32, device=dev)
     defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
              and (commit_updates is None or all(c is None for c in commit_updates[:real]))
-             and codec.supports_deferred_ef(m, n, r, transposed))
+             and not bf16_state and codec.supports_deferred_ef(m, n, r, transposed))
     _project_with_pending(codec, real_grads, momentums, qviews, P, nonzero, optimizer_states, real, m, n, transposed,
                           defer)
     for coll in tuple(getattr(batch_collectives, "fs_p_collectives", None) or ()):
@@ -628,12 +636,18 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
                                               async_op=True))
             yield
             work.wait()
+            if bf16_state:
+                codec.round_bf16(P)
     if use_low_rank and W > 1:
         work = dist.all_reduce(P, op=dist.ReduceOp.AVG, group=group, async_op=True)
         yield
         work.wait()
+        if bf16_state:
+            codec.round_bf16(P)
     yield from distributed_orthonormalize(optimizer, P, real, m, n, transposed, batch_group.ortho_group, dist_metas,
                                           batch_cache_key, sketches)
+    if bf16_state:
+        codec.round_bf16(P)  # ortho.py:829 P_local.to(original_dtype)
     R = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
     codec.project_r(list(momentums[:real]), P[:real], R[:real], transposed, nonzero=nonzero)
     if real < B:
@@ -642,10 +656,14 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     work = dist.all_reduce(R, op=dist.ReduceOp.SUM, group=rsum.process_group, async_op=True)
     yield
     work.wait()
+    if bf16_state:
+        codec.round_bf16(R)
     if use_low_rank and W > 1:
         work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
         yield
         work.wait()
+        if bf16_state:
+            codec.round_bf16(R)
     eps = float(optimizer.defaults["epsilon"])
     qgroup = getattr(batch_group, "q_norm_group", None)
     if qgroup is not None and _group_world(qgroup) > 1:
@@ -771,6 +789,23 @@ def distributed_orthonormalize(optimizer, P, real, m, n, transposed, ortho_group
     codec.dortho_apply(P1, unpack(allf), Pa, m, n, transposed)
 
 
+def _qs_in_state_dtype(Qs, real, dtype):
+    """Q states in the momentum's dtype, as the reference computes with them: Q_batch is cast to
+    M_batch.dtype for P = M Q (runtime.py:1576-1590), Q_new keeps R's dtype for the update
+    (kernels.py:229-276) and is cast into the Q state on commit (runtime.py:1132).  With
+    independent momentum / Q dtypes (DionMixedPrecisionConfig, types.py:10-17) the batch runs on
+    a cast copy; `commit()` writes the new Q back in the state's own dtype."""
+    if all(q.dtype == dtype for q in Qs):
+        return list(Qs), (lambda: None)
+    work = [q if q.dtype == dtype else q.to(dtype) for q in Qs]
+
+    def commit():
+        for i in range(real):
+            if work[i] is not Qs[i]:
+                Qs[i].copy_(work[i])
+    return work, commit
+
+
 def _project_with_pending(codec, real_grads, momentums, Qs, P, nonzero, optimizer_states, real, m, n, transposed,
                           defer):
     """Pass A: M (+ the pending error feedback of the previous step) += G; P = X Q."""
@@ -789,7 +824,7 @@ def _project_with_pending(codec, real_grads, momentums, Qs, P, nonzero, optimize
 
 
 def _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim_groups, optimizer_states,
-                   dist_metas, real, m, n, transposed, defer, commit_updates):
+                   dist_metas, real, m, n, transposed, defer, commit_updates, commit_qs=None):
     """Error feedback (now, or pending for the next pass A) and the weight update with the
     global shape's scaled LR (runtime.py:1015-1113, kernels.py:25-51)."""
     grp = optim_groups[0] or {}
@@ -811,6 +846,8 @@ def _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim
     else:
         codec.ef_apply(list(momentums[:real]), list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd,
                        scaled, transposed)
+    if commit_qs is not None:
+        commit_qs()
     if commit_updates is not None:
         for i in range(real):
             if commit_updates[i] is not None:
@@ -950,6 +987,7 @@ def _apply_pending(codec, M, Q, pending, m, n, transposed):
     """M += alpha P R^T (or alpha R P^T) for one matrix: the eager error feedback, late."""
     Pb, Rb, alpha = pending[:3]
     mu = 1.0 + float(alpha)
+    Q = Q if Q.dtype == M.dtype else Q.to(M.dtype)  # independent Q dtype: only its dtype is read here
     ones = torch.ones((1,), dtype=torch.int32, device=M.device)
     codec.ef_apply([M], None, Pb.unsqueeze(0), Rb.unsqueeze(0), [Q], ones, mu, 0.0, 0.0, 0.0, transposed)
 

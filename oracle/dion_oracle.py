@@ -436,6 +436,8 @@ def dion_batch_step_tp(per_rank: List[List[DionMatrix]], hyper: DionHyper, m_glo
         Ps.append(X @ torch.stack([q.to(X.dtype) for q in Qfull], dim=0))
     rows = [int(P.shape[1]) for P in Ps]
     P_raw = [P.clone() for P in Ps]
+    pdt = Ps[0].dtype  # ortho.py:699-750: fp32 inside, back to P's dtype at the end (:770, :829)
+    Ps = [P.to(torch.float32) for P in Ps]
     if sum(rows) <= r:
         full = torch.linalg.qr(torch.cat(Ps, dim=1), mode="reduced")[0].to(torch.float32)
         offs = [sum(rows[:k]) for k in range(T)]
@@ -454,6 +456,7 @@ def dion_batch_step_tp(per_rank: List[List[DionMatrix]], hyper: DionHyper, m_glo
             Gm = part if Gm is None else Gm + part
         R2 = torch.linalg.cholesky_ex(Gm.to(torch.float32), upper=True)[0].to(torch.float32)
         Ps = [torch.linalg.solve_triangular(R2, P, upper=True, left=False).to(torch.float32) for P in Ps]
+    Ps = [P.to(pdt) for P in Ps]
     R = None
     for k in range(T):
         part = Xs[k].mT @ Ps[k]

@@ -108,6 +108,26 @@ CASES = [
         steps=2,
         bf16=True,
     ),
+    # independent momentum / Q dtypes (DionMixedPrecisionConfig, dion/types.py:10-17,
+    # state.py:502-547): fp32 momentum with bf16 Q, and bf16 momentum with fp32 Q
+    dict(
+        name="c13_m32_q16_two_steps",
+        mats=[("p", 96, 64), ("q", 64, 160)],
+        r=16,
+        world=1,
+        steps=2,
+        m_dtype="float32",
+        q_dtype="bfloat16",
+    ),
+    dict(
+        name="c14_m16_q32_two_steps",
+        mats=[("p", 96, 64), ("q", 64, 160)],
+        r=16,
+        world=1,
+        steps=2,
+        m_dtype="bfloat16",
+        q_dtype="float32",
+    ),
 ]
 
 HYPER = dict(lr=0.01, mu=0.95, weight_decay=0.01, epsilon=1e-8, rcqr_oversample=1.25,
@@ -171,7 +191,10 @@ def _worker(rank, world, case, port, out_path):
     m0, n0 = inputs[names[0]]["m"], inputs[names[0]]["n"]
     rank_fraction = r / min(m0, n0)
     state_dtype = torch.bfloat16 if case.get("bf16") else torch.float32
-    mixed = DionMixedPrecisionConfig(momentum_dtype=state_dtype, q_dtype=state_dtype) if case.get("bf16") else None
+    m_dtype = getattr(torch, case["m_dtype"]) if "m_dtype" in case else state_dtype
+    q_dtype = getattr(torch, case["q_dtype"]) if "q_dtype" in case else state_dtype
+    mixed = DionMixedPrecisionConfig(momentum_dtype=m_dtype, q_dtype=q_dtype) \
+        if (case.get("bf16") or "m_dtype" in case) else None
     opt = MegatronDion(
         [params[n] for n in names],
         lr=HYPER["lr"],
@@ -196,8 +219,8 @@ def _worker(rank, world, case, port, out_path):
             param_config=configs[name], is_transposed=d["transposed"],
         )
         opt.state[params[name]] = dict(
-            momentum=torch.zeros(m, n, dtype=state_dtype),
-            Q=d["q0"].clone().to(state_dtype),
+            momentum=torch.zeros(m, n, dtype=m_dtype),
+            Q=d["q0"].clone().to(q_dtype),
             r=r,
             local_shape=(m, n),
             global_shape=(m, n),

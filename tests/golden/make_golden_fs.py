@@ -38,6 +38,11 @@ CASES = [
     # uneven shards (51 columns over 2 ranks: 26 + 25), mixed with a row-sharded key
     dict(name="f3_fs2_uneven_mixed", mats=[("u", 80, 51, 1), ("v", 80, 51, 1), ("w", 72, 56, 0)], rf=0.25,
          steps=2),
+    # the speedrun's bf16 momentum and Q (examples/dion/speedrun_nanogpt_mcore.py:36-62, 417-431:
+    # FS = 4 with mixed_precision) on the FS kind: columns, and uneven + row-sharded mixed
+    dict(name="f4_fs2_bf16_cols", mats=[("a", 64, 48, 1), ("b", 64, 48, 1)], rf=1 / 6, steps=2, bf16=True),
+    dict(name="f5_fs2_bf16_mixed", mats=[("u", 80, 51, 1), ("v", 80, 51, 1), ("w", 72, 56, 0)], rf=0.25,
+         steps=2, bf16=True),
 ]
 HYPER = dict(lr=0.01, mu=0.95, weight_decay=0.01, epsilon=1e-8, rcqr_oversample=1.25,
              scale_mode="spectral", extra_scale_factor=0.2)
@@ -57,7 +62,8 @@ def _worker(rank, world, case, port, out_path):
     from megatron.core.optimizer.dion import ortho as d_ortho
     from megatron.core.optimizer.dion import runtime as d_rt
     from megatron.core.optimizer.dion.algorithm import MegatronDion
-    from megatron.core.optimizer.dion.types import DionDistMeta, DionParamConfig, DionStepParam
+    from megatron.core.optimizer.dion.types import (DionDistMeta, DionMixedPrecisionConfig, DionParamConfig,
+                                                    DionStepParam)
     from megatron.core.optimizer.distrib_dion.batches import build_dion_batches
     from megatron.core.optimizer.distrib_dion.sharding import compute_fs_shard_range
 
@@ -92,11 +98,14 @@ def _worker(rank, world, case, port, out_path):
             g_full = g_full.to(torch.bfloat16).float()
             grads.append((g_full[start:end] if dim == 0 else g_full[:, start:end]).clone().contiguous())
         info[name] = dict(m=m, n=n, dim=dim, start=start, end=end, r=r, q=q_loc, grads=grads)
-    opt = MegatronDion([params[n] for n in names], rank_fraction=rf, use_fs_collectives=True, **HYPER)
+    sdt = torch.bfloat16 if case.get("bf16") else torch.float32
+    mixed = DionMixedPrecisionConfig(momentum_dtype=sdt, q_dtype=sdt) if case.get("bf16") else None
+    opt = MegatronDion([params[n] for n in names], rank_fraction=rf, use_fs_collectives=True,
+                       mixed_precision_config=mixed, **HYPER)
     for name in names:
         d = info[name]
         p = params[name]
-        opt.state[p] = dict(momentum=torch.zeros_like(p), Q=d["q"].clone(), r=d["r"],
+        opt.state[p] = dict(momentum=torch.zeros_like(p, dtype=sdt), Q=d["q"].clone().to(sdt), r=d["r"],
                             local_shape=tuple(p.shape), global_shape=(d["m"], d["n"]))
     id2name = {id(params[n]): n for n in names}
     grads_now, cache = {}, {}

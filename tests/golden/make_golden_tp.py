@@ -40,6 +40,10 @@ CASES = [
     dict(name="t3_tp2_odd_r_mixed", mats=[("u", 48, 36, 0), ("w", 56, 40, 1)], rf=0.125, steps=2),
     # global P rows <= r: the plain-QR branch of the distributed orthogonalize (ortho.py:752-775)
     dict(name="t4_tp2_plain_qr", mats=[("p", 16, 64, 0)], rf=1.0, steps=2),
+    # the speedrun's bf16 momentum and Q (examples/dion/speedrun_nanogpt_mcore.py:36-62, 417-431:
+    # TP = 2 with mixed_precision): rows, and odd r with a transposed key
+    dict(name="t5_tp2_bf16_rows", mats=[("a", 64, 48, 0), ("b", 64, 48, 0)], rf=1 / 6, steps=2, bf16=True),
+    dict(name="t6_tp2_bf16_odd_mixed", mats=[("u", 48, 36, 0), ("w", 56, 40, 1)], rf=0.125, steps=2, bf16=True),
 ]
 HYPER = dict(lr=0.01, mu=0.95, weight_decay=0.01, epsilon=1e-8, rcqr_oversample=1.25,
              scale_mode="spectral", extra_scale_factor=0.2)
@@ -60,7 +64,8 @@ def _worker(rank, world, case, port, out_path):
     from megatron.core.optimizer.dion import runtime as d_rt
     from megatron.core.optimizer.dion.algorithm import MegatronDion
     from megatron.core.optimizer.dion.state import is_p_tp_sharded
-    from megatron.core.optimizer.dion.types import DionDistMeta, DionParamConfig, DionStepParam
+    from megatron.core.optimizer.dion.types import (DionDistMeta, DionMixedPrecisionConfig, DionParamConfig,
+                                                    DionStepParam)
     from megatron.core.optimizer.distrib_dion.batches import build_dion_batches
 
     tp_group = dist.group.WORLD
@@ -93,11 +98,14 @@ def _worker(rank, world, case, port, out_path):
             g_full = g_full.to(torch.bfloat16).float()
             grads.append((g_full[start:end] if dim == 0 else g_full[:, start:end]).clone().contiguous())
         info[name] = dict(m=m, n=n, dim=dim, start=start, end=end, r=r, c0=c0, c1=c1, q=q_loc, grads=grads)
-    opt = MegatronDion([params[n] for n in names], rank_fraction=rf, use_fs_collectives=True, **HYPER)
+    sdt = torch.bfloat16 if case.get("bf16") else torch.float32
+    mixed = DionMixedPrecisionConfig(momentum_dtype=sdt, q_dtype=sdt) if case.get("bf16") else None
+    opt = MegatronDion([params[n] for n in names], rank_fraction=rf, use_fs_collectives=True,
+                       mixed_precision_config=mixed, **HYPER)
     for name in names:
         d = info[name]
         p = params[name]
-        opt.state[p] = dict(momentum=torch.zeros_like(p), Q=d["q"].clone(), r=d["r"],
+        opt.state[p] = dict(momentum=torch.zeros_like(p, dtype=sdt), Q=d["q"].clone().to(sdt), r=d["r"],
                             local_shape=tuple(p.shape), global_shape=(d["m"], d["n"]))
     id2name = {id(params[n]): n for n in names}
     grads_now, cache = {}, {}

@@ -49,6 +49,9 @@ def _worker(rank, world, port, name, out_dir, deferred, device):
     if dev.type == "cpu":
         kw["codec"] = OracleCodec(sketch_lookup=lambda P: case.sketch_for(rank, state["step"], P.cpu()),
                                   deferred=deferred)
+    if case.entry.get("bf16"):  # the speedrun's bf16 momentum and Q
+        kw["mixed_precision_config"] = mda.DionMixedPrecisionConfig(momentum_dtype=torch.bfloat16,
+                                                                    q_dtype=torch.bfloat16)
     opt = mda.MegatronDion([params[n] for n in names], lr=h["lr"], mu=h["mu"], weight_decay=h["weight_decay"],
                            rank_fraction=case.rank_fraction, epsilon=h["epsilon"],
                            rcqr_oversample=h["rcqr_oversample"], defer_error_feedback=deferred, **kw)
@@ -111,7 +114,13 @@ def _maxrel(a, b):
     return (a.double() - b.double()).abs().max().item() / max(b.double().abs().max().item(), 1e-30)
 
 
-def check_fs_results(res, name, deferred, tol):
+# bf16 state on the GPU: the HIP kernels accumulate in another order than torch's CPU bf16
+# matmuls, so a product next to a bf16 rounding boundary can round the other way: one bf16
+# ulp of the largest element (tests/test_gpu_bf16.py explains the bars)
+BF16_GPU_TOLS = {"W": 1e-3, "M": 2 ** -6, "Q": 2e-2}
+
+
+def check_fs_results(res, name, deferred, tol, bf16_tols=None):
     from tests._golden import FsCase
 
     case = FsCase(name)
@@ -127,13 +136,15 @@ def check_fs_results(res, name, deferred, tol):
                 if not deferred or step == case.steps - 1:
                     keys.append(("M", "M1"))
                 for k, ref in keys:
-                    err = _maxrel(res[rank][f"s{step}_{n}_{k}"], case.t(rank, step, f"{n}_{ref}"))
+                    err = _maxrel(res[rank][f"s{step}_{n}_{k}"].float(), case.t(rank, step, f"{n}_{ref}"))
                     worst = max(worst, err)
-                    assert err <= tol, (name, rank, step, n, k, err)
+                    bar = bf16_tols[k] if (bf16_tols and case.entry.get("bf16")) else tol
+                    assert err <= bar, (name, rank, step, n, k, err)
     return worst
 
 
-@pytest.mark.parametrize("name", ["f1_fs2_cols", "f2_fs2_rows_pad", "f3_fs2_uneven_mixed"])
+@pytest.mark.parametrize("name", ["f1_fs2_cols", "f2_fs2_rows_pad", "f3_fs2_uneven_mixed", "f4_fs2_bf16_cols",
+                                  "f5_fs2_bf16_mixed"])
 @pytest.mark.parametrize("deferred", [False, True], ids=["eager_ef", "deferred_ef"])
 def test_gloo_fs2_matches_reference(name, deferred):
     res = run_fs(name, deferred=deferred)

@@ -54,9 +54,14 @@ def maxrel(a, b):
     return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
 
 
-def test_bf16_golden_replay_through_optimizer():
+@pytest.mark.parametrize("name", ["c11_bf16_two_steps_mixed", "c13_m32_q16_two_steps", "c14_m16_q32_two_steps"])
+def test_bf16_golden_replay_through_optimizer(name):
+    """c11: bf16 momentum and Q; c13 / c14: independent momentum / Q dtypes (a bf16 Q rounds
+    Qn, so either way a product next to a bf16 rounding boundary may round the other way)."""
     dev = _dev()
-    case = Case("c11_bf16_two_steps_mixed")
+    case = Case(name)
+    mdt = getattr(torch, case.entry["m_dtype"]) if "m_dtype" in case.entry else torch.bfloat16
+    qdt = getattr(torch, case.entry["q_dtype"]) if "q_dtype" in case.entry else torch.bfloat16
     h = case.hyper
     names = [n for n, _, _ in case.mats]
     params = {n: torch.nn.Parameter(case.t(0, 0, f"{n}_W0").to(dev)) for n in names}
@@ -64,11 +69,11 @@ def test_bf16_golden_replay_through_optimizer():
                            rank_fraction=case.rank_fraction, epsilon=h["epsilon"],
                            rcqr_oversample=h["rcqr_oversample"], scale_mode=h["scale_mode"],
                            extra_scale_factor=h["extra_scale_factor"], coalesce_local=False,
-                           mixed_precision_config=BF16)
+                           mixed_precision_config=mda.DionMixedPrecisionConfig(momentum_dtype=mdt, q_dtype=qdt))
     attach_dp_routing(opt, [(n, params[n]) for n in names])
     for n in names:
         st = opt.state[params[n]]
-        assert st["momentum"].dtype == torch.bfloat16 and st["Q"].dtype == torch.bfloat16
+        assert st["momentum"].dtype == mdt and st["Q"].dtype == qdt
         assert st["r"] == case.r
         st["Q"].copy_(case.t(0, 0, f"{n}_Q0").to(dev))
     name_of = {id(params[n]): n for n in names}
@@ -82,6 +87,7 @@ def test_bf16_golden_replay_through_optimizer():
         opt._sketch_override = lambda batch, _sk=sk: {0: _sk[name_of[id(batch.params[0])]][0].to(dev)}
         w0 = {n: params[n].detach().clone() for n in names}
         opt.step()
+        opt.flush_error_feedback()
         torch.cuda.synchronize()
         for n in names:
             p = params[n]
@@ -94,7 +100,7 @@ def test_bf16_golden_replay_through_optimizer():
                 worst[k] = max(worst.get(k, 0.0), v)
             assert errs["W"] <= TOL_W and errs["dW"] <= TOL_DW and errs["M"] <= TOL_M and errs["Q"] <= TOL_Q, \
                 (step, n, errs)
-    print("c11 bf16 worst errors", worst)
+    print(name, "worst errors", worst)
 
 
 def _seeded(shapes, r, seed, gdt, zero=()):

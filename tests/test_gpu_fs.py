@@ -18,7 +18,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from tests.test_dist_gloo_fs import check_fs_results, run_fs
+from tests.test_dist_gloo_fs import BF16_GPU_TOLS, check_fs_results, run_fs
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
@@ -29,12 +29,13 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("name", ["f1_fs2_cols", "f2_fs2_rows_pad", "f3_fs2_uneven_mixed"])
+@pytest.mark.parametrize("name", ["f1_fs2_cols", "f2_fs2_rows_pad", "f3_fs2_uneven_mixed", "f4_fs2_bf16_cols",
+                                  "f5_fs2_bf16_mixed"])
 @pytest.mark.parametrize("deferred", [False, True], ids=["eager_ef", "deferred_ef"])
 def test_hip_fs2_matches_reference(name, deferred):
     _need_gpu()
     res = run_fs(name, deferred=deferred, device="cuda:0")
-    check_fs_results(res, name, deferred, TOL)
+    check_fs_results(res, name, deferred, TOL, bf16_tols=BF16_GPU_TOLS)
 
 
 FAST = [("a", (1024, 768), 1), ("b", (1024, 768), 1), ("t", (768, 2048), 0), ("u", (768, 2048), 0),

@@ -51,7 +51,8 @@ def sign_align(Q, Qref):
 # ---------------------------------------------------------------------------------------------- golden
 # fp32-state cases; the bf16-state capture (case viii) is replayed in tests/test_gpu_bf16.py
 WORLD1 = [n for n in case_names()
-          if Case(n).world == 1 and n != "c6_rank_deficient" and not Case(n).entry.get("bf16")]
+          if Case(n).world == 1 and n != "c6_rank_deficient" and not Case(n).entry.get("bf16")
+          and "m_dtype" not in Case(n).entry]  # bf16 / mixed state dtypes: tests/test_gpu_bf16.py
 
 
 @pytest.mark.parametrize("name", WORLD1)

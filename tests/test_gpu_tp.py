@@ -21,6 +21,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from tests.test_dist_gloo_fs import BF16_GPU_TOLS
 from tests.test_dist_gloo_tp import check_tp_results, run_tp
 
 pytestmark = pytest.mark.gpu
@@ -32,12 +33,13 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("name", ["t1_tp2_rows", "t2_tp2_cols_T", "t3_tp2_odd_r_mixed", "t4_tp2_plain_qr"])
+@pytest.mark.parametrize("name", ["t1_tp2_rows", "t2_tp2_cols_T", "t3_tp2_odd_r_mixed", "t4_tp2_plain_qr",
+                                  "t5_tp2_bf16_rows", "t6_tp2_bf16_odd_mixed"])
 @pytest.mark.parametrize("deferred", [False, True], ids=["eager_ef", "deferred_ef"])
 def test_hip_tp2_matches_reference(name, deferred):
     _need_gpu()
     res = run_tp(name, deferred=deferred, device="cuda:0")
-    check_tp_results(res, name, deferred, TOL)
+    check_tp_results(res, name, deferred, TOL, bf16_tols=BF16_GPU_TOLS)
 
 
 FAST = [("a", (2048, 1024), 0), ("b", (2048, 1024), 0), ("t", (1024, 3072), 1), ("u", (1024, 3072), 1),

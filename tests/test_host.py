@@ -235,6 +235,50 @@ def test_local_path_end_to_end_with_oracle_codec(deferred):
                 assert (got.detach() - ref).abs().max().item() <= 1e-6 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("name", ["c11_bf16_two_steps_mixed", "c13_m32_q16_two_steps", "c14_m16_q32_two_steps"])
+@pytest.mark.parametrize("deferred", [False, True], ids=["eager_ef", "deferred_ef"])
+def test_state_dtype_goldens_through_the_runtime(name, deferred):
+    """DionMixedPrecisionConfig with bf16 states, and with independent momentum / Q dtypes
+    (dion/types.py:10-17, state.py:502-547: fp32 M with bf16 Q, bf16 M with fp32 Q): the
+    product runtime (the Q state cast to the momentum's dtype for the batch and committed back
+    in its own) with the oracle codec reproduces the reference's captures."""
+    from megatron_dion_amd.optimizer import attach_dp_routing
+    from tests._cpu_codec import OracleCodec
+
+    case = Case(name)
+    h = case.hyper
+    bf = torch.bfloat16 if case.entry.get("bf16") else torch.float32
+    mdt = getattr(torch, case.entry["m_dtype"]) if "m_dtype" in case.entry else bf
+    qdt = getattr(torch, case.entry["q_dtype"]) if "q_dtype" in case.entry else bf
+    names = [n for n, _, _ in case.mats]
+    params = {n: torch.nn.Parameter(case.t(0, 0, f"{n}_W0").clone()) for n in names}
+    cur = {"step": 0}
+    opt = mda.MegatronDion([params[n] for n in names], lr=h["lr"], mu=h["mu"], weight_decay=h["weight_decay"],
+                           rank_fraction=case.rank_fraction,
+                           codec=OracleCodec(sketch_lookup=lambda P: case.sketch_for(0, cur["step"], P),
+                                             deferred=deferred),
+                           defer_error_feedback=deferred,
+                           mixed_precision_config=mda.DionMixedPrecisionConfig(momentum_dtype=mdt, q_dtype=qdt))
+    attach_dp_routing(opt, [(n, params[n]) for n in names])
+    for n in names:
+        st = opt.state[params[n]]
+        assert st["momentum"].dtype == mdt and st["Q"].dtype == qdt
+        st["Q"].copy_(case.t(0, 0, f"{n}_Q0"))
+    for step in range(case.steps):
+        cur["step"] = step
+        for n in names:
+            params[n].grad = case.t(0, step, f"{n}_G").clone()
+        opt.step()
+        opt.flush_error_feedback()
+        for n in names:
+            st = opt.state[params[n]]
+            assert st["Q"].dtype == qdt
+            for got, key in ((params[n], "W1"), (st["Q"], "Q1"), (st["momentum"], "M1")):
+                ref = case.t(0, step, f"{n}_{key}")
+                err = (got.detach().float() - ref).abs().max().item() / ref.abs().max().item()
+                assert err <= 1e-6, (name, step, n, key, err)
+
+
 # ---------------------------------------------------------------------------------------------- boundary guard
 def _one_batch(kind="ddp", shard=False, collectives=None):
     from megatron_dion_amd.types import (DionBatch, DionBatchCollectives, DionBatchEntry, DionBatchGroup,

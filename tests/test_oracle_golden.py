@@ -39,11 +39,14 @@ def _run_oracle(case, shared_p_buffer=True):
     shapes = {n: (m, k) for n, m, k in case.mats}
     # case (viii): bf16 momentum and Q (stored as their exact fp32 values)
     sdt = torch.bfloat16 if case.entry.get("bf16") else torch.float32
+    # independent momentum / Q dtypes (cases c13, c14; DionMixedPrecisionConfig)
+    mdt = getattr(torch, case.entry["m_dtype"]) if "m_dtype" in case.entry else sdt
+    qdt = getattr(torch, case.entry["q_dtype"]) if "q_dtype" in case.entry else sdt
     state = {}
     for rank in range(case.world):
         for n in names:
-            state[(rank, n)] = dict(W=case.t(rank, 0, f"{n}_W0"), M=case.t(rank, 0, f"{n}_M0").to(sdt),
-                                    Q=case.t(rank, 0, f"{n}_Q0").to(sdt))
+            state[(rank, n)] = dict(W=case.t(rank, 0, f"{n}_W0"), M=case.t(rank, 0, f"{n}_M0").to(mdt),
+                                    Q=case.t(rank, 0, f"{n}_Q0").to(qdt))
     traces = {}
     for step in range(case.steps):
         for rank in range(case.world):
@@ -86,7 +89,7 @@ def _run_oracle(case, shared_p_buffer=True):
                             n = members[0]
                             m, k = shapes[n]
                             st = state[(rank, n)]
-                            row.append(O.DionMatrix(W=st["W"], M=torch.zeros(m, k, dtype=sdt),
+                            row.append(O.DionMatrix(W=st["W"], M=torch.zeros(m, k, dtype=mdt),
                                                     Q=torch.zeros_like(st["Q"]),
                                                     G=torch.zeros(m, k), transposed=m < k,
                                                     rank_fraction=case.rank_fraction))

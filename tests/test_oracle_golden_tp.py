@@ -45,8 +45,10 @@ def tp_oracle_steps(case):
     names = [n for n, _, _ in case.mats]
     gshape = {n: (m, k) for n, m, k in case.mats}
     W = case.world
-    st = {(k, n): O.DionMatrix(W=case.t(k, 0, f"{n}_W0"), M=case.t(k, 0, f"{n}_M0"), Q=case.t(k, 0, f"{n}_Q0"),
-                               G=None, transposed=case.tp_dim(n) == 1, rank_fraction=case.rank_fraction)
+    sdt = torch.bfloat16 if case.entry.get("bf16") else torch.float32  # the speedrun's bf16 M and Q
+    st = {(k, n): O.DionMatrix(W=case.t(k, 0, f"{n}_W0"), M=case.t(k, 0, f"{n}_M0").to(sdt),
+                               Q=case.t(k, 0, f"{n}_Q0").to(sdt), G=None, transposed=case.tp_dim(n) == 1,
+                               rank_fraction=case.rank_fraction)
           for k in range(W) for n in names}
     for step in range(case.steps):
         for k in range(W):
