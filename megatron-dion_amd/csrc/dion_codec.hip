@@ -138,6 +138,41 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Wave sum on the DPP network (no LDS permutes): quad swaps, half-row and row mirrors give
+// every lane its 16-lane row sum, two row broadcasts carry rows 0-2 into row 3, and lane 63's
+// total comes back as a wave-uniform value (scalar register).  6 VALU adds + 1 readlane,
+// against wave_sum's 6 cross-lane permutes; another summation order than wave_sum's.
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWS, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f<0xB1>(v);        // quad_perm [1, 0, 3, 2]
+  v += dpp_f<0x4E>(v);        // quad_perm [2, 3, 0, 1]
+  v += dpp_f<0x141>(v);       // row_half_mirror
+  v += dpp_f<0x140>(v);       // row_mirror
+  v += dpp_f<0x142, 0xA>(v);  // row_bcast15 into rows 1, 3
+  v += dpp_f<0x143, 0xC>(v);  // row_bcast31 into rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+template <int N>
+__device__ __forceinline__ void wave_sum_dpp_n(float (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_f<0xB1>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_f<0x4E>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_f<0x141>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_f<0x140>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_f<0x142, 0xA>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_f<0x143, 0xC>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v[i]), 63));
+}
+
 // N independent wave sums in the butterfly order of wave_sum (bit-identical to N calls):
 // the N cross-lane permutes of a level are issued back to back, so their latencies overlap
 template <int N>
@@ -1097,8 +1132,8 @@ __global__ void __launch_bounds__(256) sketch_qr_inv_kernel(const float* __restr
         if (row > j) ss += xs[s] * xs[s];
         if (s == (j >> 6)) alpha_l = xs[s];
       }
-      ss = wave_sum(ss);
-      const float alpha = __shfl(alpha_l, j & 63, 64);
+      ss = wave_sum_dpp(ss);
+      const float alpha = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, alpha_l), j & 63));
       const float xnorm = sqrtf(ss);
       float tau, beta, scale;
       if (xnorm == 0.f) {
@@ -1144,7 +1179,7 @@ __global__ void __launch_bounds__(256) sketch_qr_inv_kernel(const float* __restr
 #pragma unroll
         for (int s = 0; s < RPL; ++s) d[cc] += v[s] * A[s][cc];
       }
-      wave_sum_n<NC>(d);
+      wave_sum_dpp_n<NC>(d);
 #pragma unroll
       for (int cc = 0; cc < NC; ++cc) {
         const float dt = d[cc] * tau;
@@ -2112,6 +2147,67 @@ __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_st
       cur ^= 1;
     }
   }
+}
+
+// ============================================================================
+// Upper Cholesky of the r x r Gram matrix (ortho.py:112-115, cholesky_ex upper) with the
+// matrix in registers: thread (g, c) of NG = 256 / RP row groups holds column c of rows
+// g, g + NG, ..  Pivot j: its owner group publishes row j through LDS (ping-pong, one
+// barrier), every thread forms u_j* = row / sqrt(d_j) for its column and rows and updates
+// them, G[i][c] -= u_ji u_jc: the fused products of chol_inv_kernel (and of dpotf2's dot
+// products) in the same k order, so the same factor.  Output: the padded factor + reciprocal
+// diagonal of trsm_right_kernel<RP>; G is padded to RP with the identity.  A non-positive
+// pivot stops the factorisation: its row and the later ones get a NaN diagonal, so the solve
+// turns their P columns into NaN (cholesky_ex does not raise; the fix-up's nan_to_num zeroes
+// them, ortho.py:113 / kernels.py:157-204).
+// ============================================================================
+template <int RP>
+__global__ void __launch_bounds__(256) chol_reg_kernel(const float* __restrict__ G_in, float* __restrict__ Fout,
+                                                       int r) {
+  constexpr int NG = 256 / RP, RPT = RP / NG;
+  __shared__ float row[2][RP];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int c = tid % RP, g = tid / RP;
+  const float* Gm = G_in + static_cast<long>(b) * r * r;
+  float* O = Fout + static_cast<long>(b) * (RP * RP + RP);
+  float a[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int i = g + NG * q;
+    a[q] = (i < r && c < r) ? Gm[i * r + c] : (i == c ? 1.f : 0.f);
+  }
+  int jf = RP;
+#pragma unroll 1
+  for (int j = 0; j < RP; ++j) {
+    const int buf = j & 1;
+    if (g == j % NG) {
+#pragma unroll
+      for (int q = 0; q < RPT; ++q)
+        if (q == j / NG) row[buf][c] = a[q];
+    }
+    __syncthreads();
+    const float d = row[buf][j];
+    if (!(d > 0.f)) {  // uniform
+      jf = j;
+      break;
+    }
+    const float ujj = sqrtf(d);
+    const float inv = 1.f / ujj;
+    const float uc = row[buf][c] * inv;
+    if (g == j % NG) O[j * RP + c] = c < j ? 0.f : (c == j ? ujj : uc);
+    if (tid == 0) O[RP * RP + j] = inv;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int i = g + NG * q;
+      if (i > j) a[q] -= (row[buf][i] * inv) * uc;
+    }
+  }
+  for (int idx = tid; idx < (RP - jf) * RP; idx += 256) {
+    const int i = jf + idx / RP, cc = idx % RP;
+    O[i * RP + cc] = (i == cc) ? __builtin_nanf("") : 0.f;
+  }
+  for (int j = jf + tid; j < RP; j += 256) O[RP * RP + j] = __builtin_nanf("");
 }
 
 // ============================================================================
@@ -4664,9 +4760,11 @@ int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t s
                      (dbl ? sizeof(double) : sizeof(float)) * static_cast<size_t>(r) * r;
   const int threads = 256;
   if (!inv) {
-    int rc = allow_lds(chol_inv_kernel<float, false>, lds);
-    if (rc != DION_OK) return rc;
-    hipLaunchKernelGGL((chol_inv_kernel<float, false>), dim3(batch), dim3(threads), lds, st, G, Uinv, r, trsm_rt(r));
+    switch (trsm_rt(r)) {
+      case 32: hipLaunchKernelGGL((chol_reg_kernel<32>), dim3(batch), dim3(256), 0, st, G, Uinv, r); break;
+      case 64: hipLaunchKernelGGL((chol_reg_kernel<64>), dim3(batch), dim3(256), 0, st, G, Uinv, r); break;
+      default: hipLaunchKernelGGL((chol_reg_kernel<128>), dim3(batch), dim3(256), 0, st, G, Uinv, r); break;
+    }
     return check_launch("chol");
   }
   if (dbl) {
