@@ -97,8 +97,17 @@ def resolve_dp_batch_group(config, *, replicate_group, group_size: Callable, fs_
             raise RuntimeError("[DION_UNSUPPORTED_SHARDING] TP on the contraction side of P is not built")
         if tp_world > 1:
             sync.append(tp_group)
+            # FS x TP (the speedrun's topology): FS shards the contraction side; its group
+            # normalises Q's columns (q_norm_group, batches.py:562-569) and sums P (:703-715)
+            qn = None
+            if bool(getattr(config, "use_fs_shard", False)):
+                if fs_group is None:
+                    raise RuntimeError("[DION_MISSING_BATCH_FS_GROUP] an FS-sharded Dion param needs its FS group")
+                if group_size(fs_group) > 1:
+                    sync.append(fs_group)
+                    qn = fs_group
             return DionBatchGroup(kernel_kind="fsdp_tp", replicate_group=replicate_group, ortho_group=tp_group,
-                                  batch_world_size=int(tp_world), sync_groups=tuple(sync))
+                                  q_norm_group=qn, batch_world_size=int(tp_world), sync_groups=tuple(sync))
     if bool(getattr(config, "use_fs_shard", False)):
         if fs_group is None:
             raise RuntimeError("[DION_MISSING_BATCH_FS_GROUP] an FS-sharded Dion param needs its FS group")
@@ -182,7 +191,13 @@ def build_dion_batches(*, dion_params: Sequence, get_replicate_group: Callable,
                 tp = bg.ortho_group
                 ax = DionAxisCollective(indices=tuple(range(size)), process_group=tp, world_size=int(group_size(tp)),
                                         rank=int(dist.get_rank(tp)))
-                coll = DionBatchCollectives(tp_q_gathers=(ax,), tp_r_collectives=(ax,), tp_q_reshards=(ax,))
+                fsp = ()
+                if bg.q_norm_group is not None:  # should_reduce_p_over_fs: P = X Q sums over the FS shards
+                    fs = bg.q_norm_group
+                    fsp = (DionAxisCollective(indices=tuple(range(size)), process_group=fs,
+                                              world_size=int(group_size(fs)), rank=int(dist.get_rank(fs))),)
+                coll = DionBatchCollectives(tp_q_gathers=(ax,), tp_r_collectives=(ax,), tp_q_reshards=(ax,),
+                                            fs_p_collectives=fsp)
             elif bg.kernel_kind == "fsdp":
                 fs = bg.q_norm_group
                 coll = DionBatchCollectives(fs_collective=DionAxisCollective(

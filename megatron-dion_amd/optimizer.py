@@ -11,8 +11,11 @@ fallback.
 
 The elementwise branch (AdamW / Lion for the ElementwiseStepParam items,
 algorithm.py:247-429) runs after the Dion batches in one multi-tensor HIP launch per
-update contract.  Out of scope on this path: TP/FS-sharded Dion and
-split-qkv children.
+update contract.  The batch kinds are the reference's: whole-matrix data parallel ("ddp"),
+FS-sharded ("fsdp") and TP-sharded ("fsdp_tp", FS on the contraction side when both are on: the
+speedrun's topology), fp32 or bf16 momentum / Q (independent dtypes); split QKV / QKVG /
+linear children of whole or sharded parents come from the stand-alone adapter
+(`attach_dp_routing`, split.py) or from the reference's own adapter.
 """
 from __future__ import annotations
 
@@ -29,7 +32,7 @@ from .batches import build_dion_batches
 from .runtime import (AsyncRuntime, DionStateMap, coalesce_local_batches, coalesce_replicated_batches,
                       drop_pending_error_feedback, flush_pending_error_feedback, is_replicated,
                       run_dion_batch_async)
-from .split import child_uid, gather_rows, make_commit, split_plan, state_key
+from .split import child_uid, gather_rows, make_commit, split_child_layouts, split_plan, state_key
 from .state import init_dion_state
 from .types import DionDistMeta, DionMixedPrecisionConfig, DionStepParam, ElementwiseStepParam
 
@@ -463,30 +466,46 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
         tspec = (tp_shards or {}).get(name)
         if tspec is not None and tp_group is None:
             raise RuntimeError(f"[DION_MISSING_BATCH_TP_GROUP] {name}: tp_shards given without tp_group")
-        plan = split_plan(p, optimizer.defaults)
+        plan = split_plan(p, optimizer.defaults, global_rows=None if (spec is None and tspec is None)
+                          else int((tspec or spec)[0][0]))
         if plan is not None:
-            if spec is not None or tspec is not None:
-                raise RuntimeError(f"[DION_SPLIT_SHARDED_PARENT] {name}: split children of FS/TP shards are not built")
-            family, kinds, segs, flags = plan
+            family, kinds, _, flags = plan
             pstate = optimizer.state[p]
             pstate.update(flags)
             pstate["momentum"] = torch.zeros_like(p, dtype=_as_dtype(getattr(mpc, "momentum_dtype", None)) or p.dtype)
+            tp_world = int(dist.get_world_size(tp_group)) if tspec is not None else 1
+            tp_rank = int(dist.get_rank(tp_group)) if tspec is not None else 0
+            layout = split_child_layouts(p, plan, fs_spec=spec, tp_spec=tspec, fs_group=fs_group,
+                                         tp_world=tp_world, tp_rank=tp_rank)
             for kind in kinds:
-                rows = sum(b - a for a, b in segs[kind])
+                lay = layout[kind]
+                rows = lay["local_rows"]
                 cname = f"{name}::{kind}"
+                cuid = child_uid((name,), family, kind)
                 cstate, ccfg = init_dion_state(p.narrow(0, 0, rows), rank_fraction=rf, rank_multiple_of=mult,
-                                               base_seed=base_seed, param_uid=child_uid((name,), family, kind),
-                                               param_name=cname,
+                                               base_seed=base_seed, param_uid=cuid, param_name=cname,
                                                q_dtype=_as_dtype(getattr(mpc, "q_dtype", None)),
                                                use_low_rank_sync=optimizer.use_low_rank_sync, with_momentum=False,
+                                               fs_shard=None if lay["fs"] is None else (*lay["fs"], fs_world),
+                                               tp_shard=None if lay["tp"] is None else (*lay["tp"], tp_world, tp_rank),
                                                q_stream=q_stream)
                 for field in ("Q", "r", "local_shape", "global_shape"):
                     pstate[state_key(family, field, kind)] = cstate[field]
                 cmeta = DionDistMeta(shape=(rows, int(p.shape[1])), global_shape=tuple(cstate["global_shape"]),
-                                     rank_fraction=rf, is_transposed=ccfg.is_transposed,
-                                     param_uid=child_uid((name,), family, kind), is_dion_param=True,
-                                     param_name=cname, param_config=ccfg, local_shape=(rows, int(p.shape[1])))
-                metas[(name, kind)] = (ccfg, cmeta)
+                                     rank_fraction=rf, is_transposed=ccfg.is_transposed, param_uid=cuid,
+                                     is_dion_param=True, param_name=cname, param_config=ccfg,
+                                     local_shape=(rows, int(p.shape[1])),
+                                     tensor_row_shard_sizes=lay["row_sizes"],
+                                     row_shard_sizes=lay["row_sizes"] if lay["row_axis"] == "tp" else None)
+                if lay["fs"] is not None:
+                    cmeta.extra.update(fs_group=fs_group, fs_shard_dim=int(lay["fs"][1]),
+                                       fs_start_idx=int(lay["fs"][2]), fs_end_idx=int(lay["fs"][3]),
+                                       fs_world_size=fs_world)
+                if lay["tp"] is not None:
+                    cmeta.extra.update(tp_group=tp_group, tp_shard_dim=int(lay["tp"][1]),
+                                       tp_start_idx=int(lay["tp"][2]), tp_end_idx=int(lay["tp"][3]),
+                                       tp_world_size=tp_world)
+                metas[(name, kind)] = (ccfg, cmeta, lay["segments"])
             metas[name] = (None, plan)
             continue
         state, cfg = init_dion_state(p, rank_fraction=rf, rank_multiple_of=mult, base_seed=base_seed,
@@ -526,18 +545,18 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
                 continue
             cfg, meta = metas[name]
             if cfg is None:  # a split parent: one step param per child (split.py)
-                family, kinds, segs, _ = meta
+                family, kinds, _, _ = meta
                 pstate = optimizer.state[p]
                 M = dict.__getitem__(pstate, "momentum")
                 for kind in kinds:
-                    ccfg, cmeta = metas[(name, kind)]
-                    cstate = {"momentum": gather_rows(M, segs[kind])}
+                    ccfg, cmeta, segs = metas[(name, kind)]
+                    cstate = {"momentum": gather_rows(M, segs)}
                     for field in ("Q", "r", "local_shape", "global_shape"):
                         cstate[field] = pstate[state_key(family, field, kind)]
-                    steps.append(DionStepParam(param=gather_rows(p.data, segs[kind]), grad=gather_rows(g, segs[kind]),
+                    steps.append(DionStepParam(param=gather_rows(p.data, segs), grad=gather_rows(g, segs),
                                                optimizer_state=cstate, optim_group=group_of.get(id(p), group),
                                                config=ccfg, dist_meta=cmeta,
-                                               commit_update=make_commit(p, M, segs[kind])))
+                                               commit_update=make_commit(p, M, segs)))
                 continue
             steps.append(DionStepParam(param=p, grad=g, optimizer_state=optimizer.state[p],
                                        optim_group=group_of.get(id(p), group), config=cfg, dist_meta=meta))

@@ -106,21 +106,36 @@ def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_
 
     `tp_shard = (global_shape, tp_shard_dim, start, end, tp_world, tp_rank)`: this rank's TP
     shard (rows for dim 0, columns for dim 1).  TP takes the P-row side (dim 0 -> not
-    transposed, dim 1 -> transposed, state.py:304-310), Q keeps all its rows and this rank's
-    columns of r (resolve_q_state_layout, state.py:159-217: split_range(r, tp, rank))."""
+    transposed, dim 1 -> transposed, state.py:304-310), Q keeps its rows and this rank's
+    columns of r (resolve_q_state_layout, state.py:159-217: split_range(r, tp, rank)).
+
+    Both (the speedrun's FS x TP topology): FS shards the other dim (get_fs_split_dim,
+    distrib_dion/sharding.py:64-70), i.e. the contraction side of P; `param` is then the
+    (TP rows x FS columns) block for TP dim 0 and Q holds the FS rows [start, end) of this
+    rank's TP columns ("shard(0)", "shard(1)", state.py:203-206)."""
     if param.dim() != 2:
         raise RuntimeError(f"[DION_NOT_2D] shape={tuple(param.shape)}")
     ml, nl = (int(d) for d in param.shape)
     if tp_shard is not None:
-        if fs_shard is not None:
-            raise RuntimeError("[DION_UNSUPPORTED_SHARDING] FS and TP shards of one param are not built "
-                               "in the stand-alone adapter")
         (m, n), dim, start, end, tp_world, tp_rank = tp_shard
         m, n, dim, tp_world, tp_rank = int(m), int(n), int(dim), int(tp_world), int(tp_rank)
         if dim not in (0, 1):
             raise RuntimeError(f"[DION_BAD_TP_SHARD_DIM] tp_shard_dim={dim}")
-        if (ml, nl) != ((end - start, n) if dim == 0 else (m, end - start)):
-            raise RuntimeError(f"[DION_BAD_TP_SHARD] local {(ml, nl)} vs global {(m, n)} dim {dim} [{start}, {end})")
+        q_rows, fs_dim, fs_world = None, -1, 1
+        exp = [end - start, n] if dim == 0 else [m, end - start]
+        if fs_shard is not None:
+            (fm, fn), fs_dim, fs0, fs1, fs_world = fs_shard
+            fs_dim, fs_world = int(fs_dim), int(fs_world)
+            if (int(fm), int(fn)) != (m, n):
+                raise RuntimeError(f"[DION_BAD_FS_TP_SHARD] FS global {(fm, fn)} != TP global {(m, n)}")
+            if fs_dim != 1 - dim:
+                raise RuntimeError(f"[DION_BAD_FS_SHARD_DIM] fs_shard_dim={fs_dim} with tp_shard_dim={dim}: FS "
+                                   "shards the dim orthogonal to TP (distrib_dion/sharding.py:64-70)")
+            exp[fs_dim] = int(fs1) - int(fs0)
+            q_rows = (int(fs0), int(fs1))
+        if (ml, nl) != tuple(exp):
+            raise RuntimeError(f"[DION_BAD_TP_SHARD] local {(ml, nl)} vs global {(m, n)} dim {dim} [{start}, {end})"
+                               + ("" if fs_shard is None else f" FS {q_rows}"))
         transposed = dim == 1
         r = rank_for_shape(m, n, rank_fraction, rank_multiple_of)
         base = r // tp_world
@@ -135,13 +150,15 @@ def init_dion_state(param: torch.Tensor, *, rank_fraction: float, rank_multiple_
         if q_stream not in ("device", "cpu"):
             raise RuntimeError(f"[DION_INVALID_Q_STREAM] q_stream={q_stream!r}")
         q = init_q(q_shape, seed, param.device if q_stream == "device" else "cpu", dtype=q_dtype or param.dtype,
-                   cols=(c0, c1)).to(param.device)
+                   rows=q_rows, cols=(c0, c1)).to(param.device)
         state = {"Q": q, "r": r, "local_shape": (ml, nl), "global_shape": (m, n)}
         if with_momentum:
             state = {"momentum": torch.zeros_like(param, dtype=momentum_dtype or param.dtype), **state}
         cfg = DionParamConfig(is_transposed=transposed, use_low_rank_sync=bool(use_low_rank_sync) and
                               should_use_low_rank_sync(global_shape=(m, n), r_global=r, rank_fraction=rank_fraction))
         cfg.has_tp_shard, cfg.use_tp_shard, cfg.tp_shard_dim = True, tp_world > 1, dim
+        if fs_shard is not None:
+            cfg.has_fs_shard, cfg.use_fs_shard, cfg.fs_shard_dim = True, fs_world > 1, fs_dim
         return state, cfg
     if fs_shard is None:
         m, n = ml, nl

@@ -55,6 +55,10 @@ class DionDistMeta:
     param_config: Optional[DionParamConfig] = None
     per_expert_global_shape: Optional[Tuple[int, int]] = None
     local_shape: Optional[Tuple[int, int]] = None
+    # uneven row layouts of split children of row-sharded parents (split_child.py:10-52):
+    # every member's rows of the sharded side; row_shard_sizes when they shard P's rows
+    tensor_row_shard_sizes: Optional[Tuple[int, ...]] = None
+    row_shard_sizes: Optional[Tuple[int, ...]] = None
     extra: Dict[str, Any] = field(default_factory=dict)
 
 
