@@ -235,6 +235,247 @@ __global__ void __launch_bounds__(256) b16_round_kernel(float* __restrict__ x, l
     x[i] = bf16_round(x[i]);
 }
 
+// ----------------------------------------------------------------------------- streaming projections
+// The two projection geometries for shapes made of whole blocks (b16_fast_*_ok), HBM-bound:
+// every M / G access is a whole 128-byte line with the non-temporal policy, the next step's
+// lines are in flight while a step computes (register double buffer), and the thin operand's
+// 32-k run of every 16-column block is staged ONCE per block per step in LDS, in the MFMA
+// operand order (double-buffered, one barrier per step).  The thin operand is the MFMA A
+// operand (lane (t, g): T column 16 cb + t, k-run 8 g .. 8 g + 7, from the tt panel), X the
+// B operand, so D[T column][X row / column] lands as four consecutive output values per lane.
+// Same per-element arithmetic as b16_proj_kernel: M = rne(M + G), exact bf16 products summed
+// in fp32 (in MFMA order), the K-chunk slabs summed in fixed order and rounded once.
+constexpr int kB16RowBlk = 128;  // row mode: 4 waves x 32 rows per block, 64-column steps
+constexpr int kB16ColBlk = 256;  // column mode: 4 waves x 64 columns per block, 32-row steps
+
+__device__ __forceinline__ uint32_t b16_add2(uint32_t m, uint32_t g) {
+  const uint32_t lo = f32_to_bf16_rne(__uint_as_float(m << 16) + __uint_as_float(g << 16));
+  const uint32_t hi = f32_to_bf16_rne(__uint_as_float(m & 0xFFFF0000u) + __uint_as_float(g & 0xFFFF0000u));
+  return lo | (hi << 16);
+}
+
+// one step's thin-operand runs: item (s, cb, lane) = tt[16 cb + lane % 16][k0 + 32 s + 8 (lane / 16) ..]
+template <int NS, int RB>
+struct B16Stage {
+  static constexpr int kItems = NS * RB * 64;
+  static constexpr int kPer = (kItems + 255) / 256;
+  u32x4 v[kPer];
+  __device__ __forceinline__ void load(const uint16_t* tt, long Kp, int k0, int tid) {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int item = tid + 256 * it;
+      if (kItems % 256 == 0 || item < kItems) {
+        const int s = item / (RB * 64), rem = item - s * (RB * 64), cb = rem >> 6, ln = rem & 63;
+        v[it] = *reinterpret_cast<const u32x4*>(tt + static_cast<long>(16 * cb + (ln & 15)) * Kp + k0 + 32 * s +
+                                                8 * (ln >> 4));
+      }
+    }
+  }
+  __device__ __forceinline__ void store(u32x4* dst, int tid) const {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int item = tid + 256 * it;
+      if (kItems % 256 == 0 || item < kItems) dst[item] = v[it];
+    }
+  }
+};
+
+// row mode: out (rows, r) = X (rows x K) T; wave = 32 rows, step = 64 columns.  Lane l loads
+// row 8 q + l / 8, 16 bytes at column 8 (l % 8) of the step (four instructions, each 8 whole
+// lines); the operand layout (lane (t, g): row t, columns 8 g ..) comes from the wave's LDS
+// tile (xt_swz swizzle, conflict-free reads).
+template <int RB, int GDT>
+__global__ void __launch_bounds__(256, 2) b16_row_kernel(const B16ProjArgs a) {
+  constexpr int NI = 2 * RB * 64;
+  __shared__ u32x4 tp[2][NI];
+  __shared__ u32x4 xt[4][32 * 8];
+  const BlockXYZ blk = xcd_block();
+  const int b = blk.z, kc = blk.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int t = lane & 15, g = lane >> 4;
+  const int lr = lane >> 3, lc = lane & 7;
+  const int r0 = blk.x * kB16RowBlk + wave * 32;
+  const int k_begin = kc * a.kchunk, k_end = min(a.K, k_begin + a.kchunk);
+  uint16_t* X = a.x[b] + static_cast<long>(r0 + lr) * a.ld_x + 8 * lc;
+  const uint16_t* G = GDT == DION_DTYPE_BF16
+                          ? static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(r0 + lr) * a.ld_g + 8 * lc
+                          : nullptr;
+  const uint16_t* tt = a.tt + static_cast<long>(b) * a.rpad * a.Kp;
+  u32x4 xs[2][4], gs[2][4];
+  auto load = [&](int s, int j) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xs[s][q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + static_cast<long>(8 * q) * a.ld_x + j));
+      if constexpr (GDT == DION_DTYPE_BF16)
+        gs[s][q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(G + static_cast<long>(8 * q) * a.ld_g + j));
+    }
+  };
+  f32x4 acc[2][RB];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t nz = 0;
+  B16Stage<2, RB> T;
+  if (k_begin < k_end) {
+    load(0, k_begin);
+    T.load(tt, a.Kp, k_begin, tid);
+    T.store(tp[0], tid);
+  }
+  __syncthreads();
+  // one 64-column step on ring slot S (a compile-time index: the two-step loop body below)
+  auto step = [&](auto Sc, int j, int cur) -> bool {
+    constexpr int S = decltype(Sc)::value;
+    const bool more = j + 64 < k_end;
+    if (more) {
+      T.load(tt, a.Kp, j + 64, tid);
+      load(S ^ 1, j + 64);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if constexpr (GDT == DION_DTYPE_BF16) {
+        u32x4 o;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] = b16_add2(xs[S][q][d], gs[S][q][d]);
+        xs[S][q] = o;
+        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(X + static_cast<long>(8 * q) * a.ld_x + j));
+      }
+      nz |= (xs[S][q][0] | xs[S][q][1] | xs[S][q][2] | xs[S][q][3]) & 0x7FFF7FFFu;
+    }
+    u32x4* xw = xt[wave];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 8 * q + lr;
+      xw[row * 8 + (lc ^ xt_swz(row))] = xs[S][q];
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      bf16x8s B[2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int row = 16 * rb + t;
+        B[rb] = __builtin_bit_cast(bf16x8s, xw[row * 8 + ((4 * ss + g) ^ xt_swz(row))]);
+      }
+#pragma unroll
+      for (int cb = 0; cb < RB; ++cb) {
+        const bf16x8s A = __builtin_bit_cast(bf16x8s, tp[cur][(ss * RB + cb) * 64 + lane]);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[rb], acc[rb][cb], 0, 0, 0);
+      }
+    }
+    if (!more) return false;
+    T.store(tp[cur ^ 1], tid);
+    __syncthreads();
+    return true;
+  };
+  for (int j = k_begin; j < k_end; j += 128) {
+    if (!step(std::integral_constant<int, 0>{}, j, 0)) break;
+    if (!step(std::integral_constant<int, 1>{}, j + 64, 1)) break;
+  }
+  // lane (t, g): rows 16 rb + t, T columns 16 cb + 4 g .. + 3
+  float* out = a.slab + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * a.r;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(r0 + 16 * rb + t) * a.r + 16 * cb + 4 * g) = acc[rb][cb];
+  if (a.nonzero != nullptr && __any(nz != 0u) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
+}
+
+// column mode: out (cols, r) = X^T T, X rows = K; wave = 64 columns, step = 32 rows.  Lane
+// (t, g) loads columns 4 t .. 4 t + 3 of the wave's 64 (8 bytes) of rows 8 g + e, e < 8
+// (eight instructions, each 4 whole lines); the B operand of column c is the lane's 8 rows
+// of that column, regrouped in registers (16-bit lanes of the 8 loads).
+template <int RB, int GDT>
+__global__ void __launch_bounds__(256, 2) b16_col_kernel(const B16ProjArgs a) {
+  constexpr int NI = RB * 64;
+  __shared__ u32x4 tp[2][NI];
+  const BlockXYZ blk = xcd_block();
+  const int b = blk.z, kc = blk.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int t = lane & 15, g = lane >> 4;
+  const int c0 = blk.x * kB16ColBlk + wave * 64 + 4 * t;
+  const int k_begin = kc * a.kchunk, k_end = min(a.K, k_begin + a.kchunk);
+  uint16_t* X = a.x[b] + static_cast<long>(8 * g) * a.ld_x + c0;
+  const uint16_t* G = GDT == DION_DTYPE_BF16
+                          ? static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(8 * g) * a.ld_g + c0
+                          : nullptr;
+  const uint16_t* tt = a.tt + static_cast<long>(b) * a.rpad * a.Kp;
+  u32x2_ xs[2][8], gs[2][8];
+  auto load = [&](int s, int i) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xs[s][e] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_*>(X + static_cast<long>(i + e) * a.ld_x));
+      if constexpr (GDT == DION_DTYPE_BF16)
+        gs[s][e] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_*>(G + static_cast<long>(i + e) * a.ld_g));
+    }
+  };
+  f32x4 acc[4][RB];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t nz = 0;
+  B16Stage<1, RB> T;
+  if (k_begin < k_end) {
+    load(0, k_begin);
+    T.load(tt, a.Kp, k_begin, tid);
+    T.store(tp[0], tid);
+  }
+  __syncthreads();
+  auto step = [&](auto Sc, int i, int cur) -> bool {
+    constexpr int S = decltype(Sc)::value;
+    const bool more = i + 32 < k_end;
+    if (more) {
+      T.load(tt, a.Kp, i + 32, tid);
+      load(S ^ 1, i + 32);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if constexpr (GDT == DION_DTYPE_BF16) {
+        const u32x2_ o{b16_add2(xs[S][e][0], gs[S][e][0]), b16_add2(xs[S][e][1], gs[S][e][1])};
+        xs[S][e] = o;
+        __builtin_nontemporal_store(o, reinterpret_cast<u32x2_*>(X + static_cast<long>(i + e) * a.ld_x));
+      }
+      nz |= (xs[S][e][0] | xs[S][e][1]) & 0x7FFF7FFFu;
+    }
+    // column c of the lane's 8 rows: 16-bit lane c % 2 of dword c / 2 of each row's load
+    bf16x8s B[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      u32x4 v;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t x0 = xs[S][2 * d][c >> 1], x1 = xs[S][2 * d + 1][c >> 1];
+        v[d] = (c & 1) ? ((x0 >> 16) | (x1 & 0xFFFF0000u)) : ((x0 & 0xFFFFu) | (x1 << 16));
+      }
+      B[c] = __builtin_bit_cast(bf16x8s, v);
+    }
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      const bf16x8s A = __builtin_bit_cast(bf16x8s, tp[cur][cb * 64 + lane]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[c], acc[c][cb], 0, 0, 0);
+    }
+    if (!more) return false;
+    T.store(tp[cur ^ 1], tid);
+    __syncthreads();
+    return true;
+  };
+  for (int i = k_begin; i < k_end; i += 64) {
+    if (!step(std::integral_constant<int, 0>{}, i, 0)) break;
+    if (!step(std::integral_constant<int, 1>{}, i + 32, 1)) break;
+  }
+  // lane (t, g): output rows (X columns) c0 + c, T columns 16 cb + 4 g .. + 3
+  float* out = a.slab + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * a.r;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(c0 + c) * a.r + 16 * cb + 4 * g) = acc[c][cb];
+  if (a.nonzero != nullptr && __any(nz != 0u) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
+}
+
 // ----------------------------------------------------------------------------- updates
 // For every element (i, j) of the m x n storage:
 //   u = sum_c RF_u[i][c] CF_u[j][c];   M = rne(M + rne(alpha rne(u)))      (error feedback)
@@ -591,10 +832,37 @@ Geo geo(int out_rows, int K, int batch) {
   return g;
 }
 
+// the streaming kernels (b16_row_kernel / b16_col_kernel): whole blocks, r a multiple of 16,
+// bf16 or no gradient (shape rules here; pointer alignment is checked at launch)
+#ifndef DION_B16_FAST
+#define DION_B16_FAST 1
+#endif
+bool fast_ok(bool row_mode, int m, int n, int r, int gdt) {
+  if (!DION_B16_FAST || r % 16 != 0 || r > 128 || (gdt != DION_DTYPE_NONE && gdt != DION_DTYPE_BF16)) return false;
+  return row_mode ? (m % kB16RowBlk == 0 && n % 64 == 0) : (n % kB16ColBlk == 0 && m % 32 == 0);
+}
+
+// split-K geometry of the streaming kernels: K chunks of whole steps, about kTargetBlocks blocks
+Geo fast_geo(bool row_mode, int out_rows, int K, int batch) {
+  Geo g;
+  const int blk = row_mode ? kB16RowBlk : kB16ColBlk, step = row_mode ? 64 : 32;
+  g.gx = static_cast<int>(ceil_div(out_rows, blk));
+  long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
+  long maxc = ceil_div(K, 256);
+  long nc = want < maxc ? want : maxc;
+  if (nc < 1) nc = 1;
+  g.kchunk = round_up(ceil_div(K, nc), step);
+  g.nchunk = static_cast<int>(ceil_div(K, g.kchunk));
+  g.out_rows = out_rows;
+  return g;
+}
+
 size_t proj_ws(int m, int n, int r, int batch, bool row_mode) {
   const int out_rows = row_mode ? m : n, K = row_mode ? n : m;
   const Geo g = geo(out_rows, K, batch);
-  const size_t slab = (sizeof(float) * static_cast<size_t>(batch) * g.nchunk * out_rows * r + 255) / 256 * 256;
+  const Geo f = fast_geo(row_mode, out_rows, K, batch);
+  const int nchunk = g.nchunk > f.nchunk ? g.nchunk : f.nchunk;  // either kernel may run (alignment)
+  const size_t slab = (sizeof(float) * static_cast<size_t>(batch) * nchunk * out_rows * r + 255) / 256 * 256;
   return slab + sizeof(uint16_t) * static_cast<size_t>(batch) * rpad_of(r) * kpad_of(K);
 }
 
@@ -656,15 +924,31 @@ int project(bool row_mode, int m, int n, int r, int nb, const void* const* G, in
             (gdt == DION_DTYPE_NONE || (reinterpret_cast<uintptr_t>(G[b]) & 15u) == 0);
     a.vec = vec ? 1 : 0;
   }
-  const dim3 grid(g.gx, g.nchunk, nb);
+  bool fast = fast_ok(row_mode, m, n, r, gdt) && a.vec;
+  const Geo fg = fast_geo(row_mode, out_rows, K, nb);
+  if (fast) {
+    a.kchunk = fg.kchunk;
+    a.nchunk = fg.nchunk;
+  }
+  const dim3 grid = fast ? dim3(fg.gx, fg.nchunk, nb) : dim3(g.gx, g.nchunk, nb);
   auto launch = [&](auto RBc) {
     constexpr int RB = decltype(RBc)::value;
     return dispatch_gdt(gdt, [&](auto Gc) {
       constexpr int GD = decltype(Gc)::value;
-      if (row_mode)
+      if constexpr (GD == DION_DTYPE_F32) {
+        if (row_mode)
+          hipLaunchKernelGGL((b16_proj_kernel<false, RB, GD>), grid, dim3(256), 0, st, a);
+        else
+          hipLaunchKernelGGL((b16_proj_kernel<true, RB, GD>), grid, dim3(256), 0, st, a);
+      } else if (fast && row_mode) {
+        hipLaunchKernelGGL((b16_row_kernel<RB, GD>), grid, dim3(256), 0, st, a);
+      } else if (fast) {
+        hipLaunchKernelGGL((b16_col_kernel<RB, GD>), grid, dim3(256), 0, st, a);
+      } else if (row_mode) {
         hipLaunchKernelGGL((b16_proj_kernel<false, RB, GD>), grid, dim3(256), 0, st, a);
-      else
+      } else {
         hipLaunchKernelGGL((b16_proj_kernel<true, RB, GD>), grid, dim3(256), 0, st, a);
+      }
       return check_launch("b16_proj");
     });
   };
@@ -683,7 +967,7 @@ int project(bool row_mode, int m, int n, int r, int nb, const void* const* G, in
   const long per = static_cast<long>(out_rows) * r;
   long blocks = ceil_div(per * nb, 256);
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(b16_reduce_round_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, out, slab, g.nchunk,
+  hipLaunchKernelGGL(b16_reduce_round_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, out, slab, a.nchunk,
                      per, nb);
   return check_launch("b16_reduce_round");
 }
