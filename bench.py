@@ -88,10 +88,10 @@ KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
 # --state-dtype bf16 (the speedrun's bf16 momentum and Q, SURVEY 8c case viii): eager EF,
 # bytes per element A: G 2 + M 2 + M 2, B: M 2, EF + weight update in one pass: M 4 + W 8
 BYTES_PER_ELEM_BF16 = {"project_p": 6.0, "project_r": 2.0, "ef_apply": 12.0}
-KERNEL_OF_BF16 = {("project_p", False): ("b16_proj_kernel<false, 4, 2>", 1),
-                  ("project_p", True): ("b16_proj_kernel<true, 4, 2>", 1),
-                  ("project_r", False): ("b16_proj_kernel<true, 4, 0>", 1),
-                  ("project_r", True): ("b16_proj_kernel<false, 4, 0>", 1),
+KERNEL_OF_BF16 = {("project_p", False): ("b16_row_kernel<4, 2>", 1),
+                  ("project_p", True): ("b16_col_kernel<4, 2>", 1),
+                  ("project_r", False): ("b16_col_kernel<4, 0>", 1),
+                  ("project_r", True): ("b16_row_kernel<4, 0>", 1),
                   ("ef_apply", False): ("b16_stream_kernel<4, 8, false>", 1),
                   ("ef_apply", True): ("b16_stream_kernel<4, 8, true>", 1)}
 
@@ -176,13 +176,10 @@ def cpu_baseline():
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense BF16/FP16, MI355X_MICROARCH.md
 MFMA_F32_PEAK_TFLOPS = 157.3
 MFMA_WORK = (("rowproj_efh3_kernel", 2 * 2 * 3, MFMA_BF16_PEAK_TFLOPS),
-             ("rowproj_ef_kernel", 2 * 2 * 6, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_efh3_kernel", 2 * 2 * 3, MFMA_BF16_PEAK_TFLOPS),
-             ("colproj_ef_kernel", 2 * 2 * 6, MFMA_BF16_PEAK_TFLOPS),
              ("rowproj_h3_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_h3_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_x6_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
-             ("rowproj_x6_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
              ("rank_stream_kernel@h3", 2 * 3, MFMA_BF16_PEAK_TFLOPS),  # <..., true>: the weight update
              ("rank_stream_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
              ("rowproj_fast_kernel", 2, MFMA_F32_PEAK_TFLOPS),

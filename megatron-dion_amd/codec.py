@@ -73,7 +73,6 @@ class HipDionCodec:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self._ws = {}  # per-stream scratch: batches may run concurrently on several streams
         self._ef_ok = {}
-        self.ef_presplit = False  # split P once per call (workspace); measured slower than per-tile splits
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
@@ -323,7 +322,7 @@ class HipDionCodec:
             raise RuntimeError("[DION_BAD_FACTOR] P and R must be contiguous (batch, rows, r)")
         d = self._desc(B, m, n, r, transposed, M=momentums[0] if momentums else None,
                        W=params[0] if params else None, state_dtype=sdt)
-        ws = self.workspace(d, _lib.OP_EF_APPLY) if self.ef_presplit else None
+        ws = None  # the update splits its factors in-kernel (no workspace)
         rc = self.lib.dion_ef_apply(ctypes.byref(d), _ptrs(momentums) if momentums else None,
                                     _ptrs(params) if params else None,
                                     P.data_ptr(), R.data_ptr(), _ptrs(qs), nonzero.data_ptr(), float(mu),

@@ -49,31 +49,20 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // read-modify-write stream rises from 5.2 to 5.8 TB/s and a read-only stream from
 // 6.3 to 7.0 TB/s with nt on both sides.  Small factors (P, Q, R) keep the default
 // policy: every block re-reads them from L2.
-#ifndef DION_NT
-#define DION_NT 1
-#endif
-// waves per block of the pass-B column kernel and its min-blocks-per-CU hint (tuning knobs)
-#ifndef DION_COLX6_NW
-#define DION_COLX6_NW 4
-#endif
-#ifndef DION_COLX6_MINB
-#define DION_COLX6_MINB 1
-#endif
-constexpr int kStreamAux = DION_NT ? 2 : 0;  // buffer-op cache-policy bits (nt)
+constexpr int kNt = 1;
+// waves per block of the pass-B column kernel and its min-blocks-per-CU hint (measured defaults)
+constexpr int kColx6Minb = 1;
+constexpr int kStreamAux = kNt ? 2 : 0;  // buffer-op cache-policy bits (nt)
 // streaming projection kernels: issue the next step's split-operand staging loads before the big
 // operand's prefetch, so the wait before the LDS store retires only the split and the
-// prefetch stays in flight across the barrier (tuning knob)
+// prefetch stays in flight across the barrier (measured default)
 // (pass A kernels; _B: the pass-B kernels, measured neutral there)
-#ifndef DION_SPLIT_FIRST
-#define DION_SPLIT_FIRST 1
-#endif
-#ifndef DION_SPLIT_FIRST_B
-#define DION_SPLIT_FIRST_B 0
-#endif
+constexpr int kSplitFirst = 1;
+constexpr int kSplitFirstB = 0;
 
 template <typename T>
 __device__ __forceinline__ T ld_stream(const T* p) {
-  if constexpr (DION_NT) return __builtin_nontemporal_load(p);
+  if constexpr (kNt) return __builtin_nontemporal_load(p);
   else return *p;
 }
 
@@ -97,7 +86,7 @@ __device__ __forceinline__ uint2 ld_stream(const uint2* p) {
 
 template <typename T>
 __device__ __forceinline__ void st_stream(T* p, const T& v) {
-  if constexpr (DION_NT) __builtin_nontemporal_store(v, p);
+  if constexpr (kNt) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
 
@@ -624,19 +613,10 @@ __device__ __forceinline__ void rp_compute(RowStep<GDT>& S, f32x4 (&acc)[kRB][RB
 // 1.7x the algorithmic bytes).  Remapped, XCD x walks the contiguous range
 // [x T/8, (x+1) T/8) of the logical blocks, so its resident blocks are neighbouring
 // row blocks of one matrix that read the same thin rows at the same time.
-// waves per block of the fused pass-A row kernel (rowproj_ef_kernel), tuning knob
-#ifndef DION_PA_NW
-#define DION_PA_NW 4
-#endif
-constexpr int kPaNW = DION_PA_NW;
+// waves per block of the fused pass-A row kernel (rowproj_efh3_kernel; 8 measured slower)
+constexpr int kPaNW = 4;
 
-#ifndef DION_XCD_REMAP
-#define DION_XCD_REMAP 1
-#endif
-// column-walk rotation of the row kernels: 0 none, 1 per block, 2 per XCD (tuning knob)
-#ifndef DION_ROW_ROT
-#define DION_ROW_ROT 0
-#endif
+constexpr int kXcdRemap = 1;
 struct BlockXYZ {
   int x, y, z, xcd;
 };
@@ -644,7 +624,7 @@ struct BlockXYZ {
 __device__ __forceinline__ BlockXYZ xcd_block() {
   const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
   const int id = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-  if (!DION_XCD_REMAP) return {static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y),
+  if (!kXcdRemap) return {static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y),
                                static_cast<int>(blockIdx.z), id & 7};
   const int T = gx * gy * gz;
   const int xcd = id & 7, slot = id >> 3;
@@ -653,21 +633,13 @@ __device__ __forceinline__ BlockXYZ xcd_block() {
 }
 
 // the same remap for the column kernels (colproj_x6 / colproj_ef), whose thin rows are
-// shared by the blocks of one (K chunk, matrix); DION_XCD_REMAP_COL=0 turns it off
-#ifndef DION_XCD_REMAP_COL
-#define DION_XCD_REMAP_COL 1
-#endif
+// shared by the blocks of one (K chunk, matrix); kXcdRemapCol=0 turns it off
+constexpr int kXcdRemapCol = 1;
 __device__ __forceinline__ BlockXYZ xcd_block_col() {
-  if (DION_XCD_REMAP_COL) return xcd_block();
+  if (kXcdRemapCol) return xcd_block();
   return {static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y), static_cast<int>(blockIdx.z), 0};
 }
 
-// K-walk start offset (multiple of 32 columns) of a row-kernel block
-__device__ __forceinline__ int walk_rotation(const BlockXYZ& B, int j_len) {
-  if (DION_ROW_ROT == 1) return static_cast<int>((static_cast<long>(B.x + 7 * B.z) * 32) % j_len) & ~31;
-  if (DION_ROW_ROT == 2) return static_cast<int>((static_cast<long>(B.xcd) * 160) % j_len) & ~31;
-  return 0;
-}
 
 template <int RB, int GDT>
 __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_fast_kernel(const ProjArgs a) {
@@ -685,9 +657,8 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_fast_kernel(cons
   const int row_base = blk.x * (64 * kRB) + wave * (16 * kRB);
   const int j_begin = kc * a.kchunk;
   const int j_end = min(a.cols, j_begin + a.kchunk);
-  const int j_len = j_end - j_begin;
-  const int j_rot = walk_rotation(blk, j_len);
-  auto cj = [&](int j) { const int x = j - j_begin + j_rot; return j_begin + (x >= j_len ? x - j_len : x); };
+
+  auto cj = [](int j) { return j; };
   float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 8 * g;
   const void* G = nullptr;
   if constexpr (GDT == DION_DTYPE_BF16)
@@ -1876,119 +1847,6 @@ struct RTile<RU, true> {
   f32x16 x;
 };
 
-template <int RU, bool ROWFIX, bool PRE>
-__global__ void __launch_bounds__(256, RU >= 7 ? 1 : 2) rank_update_kernel(const RankArgs a) {
-  constexpr int R = 16 * RU;
-  const int b = blockIdx.z;
-  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63;
-  const int t = lane & 31;
-  const int h = lane >> 5;
-  const int rows = a.rows, cols = a.cols;
-  if (a.skip_zero && __builtin_amdgcn_readfirstlane(a.nonzero[b]) == 0u) return;
-  const int fbase = blockIdx.x * 128 + wave * 32;
-  if (fbase >= (ROWFIX ? rows : cols)) return;
-  const int s_begin = blockIdx.y * a.s_len;
-  const int s_end = min(ROWFIX ? cols : rows, s_begin + a.s_len);
-  const int ld = static_cast<int>(a.ld);
-  const float* Sb = a.S + static_cast<long>(b) * a.s_stride;
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      a.x[b], static_cast<short>(0), static_cast<int>(min(static_cast<long>(rows) * ld * 4, 0x7FFFFFF0L)), 0x00020000);
-  int voff[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) voff[q] = (((q & 3) + 8 * (q >> 2) + 4 * h) * ld + t) * 4;
-
-  // fixed factor of this lane's strip index, split once
-  Split3 F[RU];
-  {
-    const float* fp = a.fixed[b] + static_cast<long>(fbase + t) * R + 8 * h;
-#pragma unroll
-    for (int u = 0; u < RU; ++u)
-      split3(*reinterpret_cast<const f32x4*>(fp + 16 * u), *reinterpret_cast<const f32x4*>(fp + 16 * u + 4),
-             a.scale, F[u]);
-  }
-
-  const u32x4* Sq = PRE ? a.Ssplit + b * a.ss_stride + lane : nullptr;
-  auto load = [&](int s0, RTile<RU, PRE>& T) {
-    if constexpr (PRE) {
-      const u32x4* sq = Sq + static_cast<long>(s0 / 32) * RU * 3 * 64;
-#pragma unroll
-      for (int u = 0; u < RU; ++u)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) T.s[u][p] = sq[(u * 3 + p) * 64];
-    } else {
-      const float* sp = Sb + static_cast<long>(s0 + t) * R + 8 * h;
-#pragma unroll
-      for (int u = 0; u < RU; ++u) {
-        T.s[u][0] = *reinterpret_cast<const f32x4*>(sp + 16 * u);
-        T.s[u][1] = *reinterpret_cast<const f32x4*>(sp + 16 * u + 4);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const int row0 = ROWFIX ? fbase : s0;
-    const int col0 = ROWFIX ? s0 : fbase;
-    const int so = (row0 * ld + col0) * 4;
-#pragma unroll
-    for (int q = 0; q < 16; ++q)
-      T.x[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff[q], so, kStreamAux));
-  };
-  auto compute = [&](int s0, RTile<RU, PRE>& T) {
-    f32x16 acc;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-#pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      Split3 Sp;
-      if constexpr (PRE) {
-        Sp.hi = __builtin_bit_cast(bf16x8, T.s[u][0]);
-        Sp.mid = __builtin_bit_cast(bf16x8, T.s[u][1]);
-        Sp.lo = __builtin_bit_cast(bf16x8, T.s[u][2]);
-      } else {
-        split3(T.s[u][0], T.s[u][1], 1.f, Sp);
-      }
-      acc = ROWFIX ? mfma6(F[u], Sp, acc) : mfma6(Sp, F[u], acc);
-    }
-    const int row0 = ROWFIX ? fbase : s0;
-    const int col0 = ROWFIX ? s0 : fbase;
-    const int so = (row0 * ld + col0) * 4;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const float v = __fmul_rn(T.x[q], a.decay) + acc[q];
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[q], so, kStreamAux);
-    }
-  };
-  auto touch_s = [&](RTile<RU, PRE>& T) {
-#pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      asm volatile("" ::"v"(T.s[u][0]));
-      asm volatile("" ::"v"(T.s[u][1]));
-      if constexpr (PRE) asm volatile("" ::"v"(T.s[u][2]));
-    }
-  };
-
-  RTile<RU, PRE> A, B;
-  load(s_begin, A);
-  touch_s(A);
-  __builtin_amdgcn_sched_barrier(0);
-  for (int s0 = s_begin; s0 < s_end; s0 += 64) {
-    const bool more = s0 + 32 < s_end;
-    if (more) load(s0 + 32, B);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(s0, A);
-    __builtin_amdgcn_sched_barrier(0);
-    if (!more) break;
-    touch_s(B);
-    __builtin_amdgcn_sched_barrier(0);
-    const bool more2 = s0 + 64 < s_end;
-    if (more2) load(s0 + 64, A);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(s0 + 32, B);
-    __builtin_amdgcn_sched_barrier(0);
-    if (more2) touch_s(A);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
 // ============================================================================
 // Rank-r update, block-shared streamed factor ("rank_stream"): the production
 // weight / error-feedback path.  Same arithmetic and order as rank_update_kernel
@@ -2502,47 +2360,6 @@ __device__ __forceinline__ f32x4 mfma6_16(const Split3& A, const Split3& B, f32x
   return acc;
 }
 
-// streamed EF factor rows of one step: NROW16 x 16 rows by KK x 32 columns, one
-// 8-value run per item, split into [row16][kk][part][lane] bf16x8 in LDS
-template <int NROW16, int KK>
-struct EfStage {
-  static constexpr int kItems = NROW16 * KK * 64;
-  static constexpr int kPer = (kItems + 255) / 256;
-  f32x4 v[kPer][2];
-};
-
-template <int NROW16, int KK>
-__device__ __forceinline__ void ef_sload(EfStage<NROW16, KK>& E, const float* __restrict__ F, int row0, int tid) {
-  constexpr int R = 32 * KK;
-#pragma unroll
-  for (int it = 0; it < EfStage<NROW16, KK>::kPer; ++it) {
-    const int item = tid + 256 * it;
-    if (item < EfStage<NROW16, KK>::kItems) {
-      const int ck = item >> 6, ln = item & 63;
-      const int c = ck / KK, kk = ck - c * KK;
-      const float* src = F + static_cast<long>(row0 + 16 * c + (ln & 15)) * R + 32 * kk + 8 * (ln >> 4);
-      E.v[it][0] = *reinterpret_cast<const f32x4*>(src);
-      E.v[it][1] = *reinterpret_cast<const f32x4*>(src + 4);
-    }
-  }
-}
-
-template <int NROW16, int KK>
-__device__ __forceinline__ void ef_sstore(const EfStage<NROW16, KK>& E, bf16x8* rs, int tid) {
-#pragma unroll
-  for (int it = 0; it < EfStage<NROW16, KK>::kPer; ++it) {
-    const int item = tid + 256 * it;
-    if (item < EfStage<NROW16, KK>::kItems) {
-      const int ck = item >> 6, ln = item & 63;
-      Split3 sp;
-      split3(E.v[it][0], E.v[it][1], 1.f, sp);
-      rs[(ck * 3 + 0) * 64 + ln] = sp.hi;
-      rs[(ck * 3 + 1) * 64 + ln] = sp.mid;
-      rs[(ck * 3 + 2) * 64 + ln] = sp.lo;
-    }
-  }
-}
-
 __device__ __forceinline__ void ef_sread(const bf16x8* rs, int ck, int lane, Split3& A) {
   A.hi = rs[(ck * 3 + 0) * 64 + lane];
   A.mid = rs[(ck * 3 + 1) * 64 + lane];
@@ -2554,58 +2371,12 @@ __device__ __forceinline__ int kmap(int g, int e) {
   return KMAP == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
 }
 
-template <int RB>
-struct ThinX6 {
-  static constexpr int kItems = RB * 64;
-  static constexpr int kPer = (kItems + 255) / 256;
-  float v[kPer][8];
-};
-
-template <int RB, int KMAP>
-__device__ __forceinline__ void thin_x6_load(ThinX6<RB>& T, const float* __restrict__ Tp, int k0, int tid) {
-  constexpr int R = 16 * RB;
-#pragma unroll
-  for (int it = 0; it < ThinX6<RB>::kPer; ++it) {
-    const int item = tid + 256 * it;
-    if (item < ThinX6<RB>::kItems) {
-      const int cb = item >> 6, ln = item & 63;
-      const float* src = Tp + 16 * cb + (ln & 15);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) T.v[it][e] = src[static_cast<long>(k0 + kmap<KMAP>(ln >> 4, e)) * R];
-    }
-  }
-}
-
-template <int RB>
-__device__ __forceinline__ void thin_x6_store(const ThinX6<RB>& T, bf16x8* tq, int tid) {
-#pragma unroll
-  for (int it = 0; it < ThinX6<RB>::kPer; ++it) {
-    const int item = tid + 256 * it;
-    if (item < ThinX6<RB>::kItems) {
-      const int cb = item >> 6, ln = item & 63;
-      Split3 sp;
-      split3(f32x4{T.v[it][0], T.v[it][1], T.v[it][2], T.v[it][3]},
-             f32x4{T.v[it][4], T.v[it][5], T.v[it][6], T.v[it][7]}, 1.f, sp);
-      tq[(cb * 3 + 0) * 64 + ln] = sp.hi;
-      tq[(cb * 3 + 1) * 64 + ln] = sp.mid;
-      tq[(cb * 3 + 2) * 64 + ln] = sp.lo;
-    }
-  }
-}
-
 // swizzle of the 32 x 8 (16-byte unit) LDS transpose tile: chunk k of row r is stored at
-// k ^ xt_swz(r).  0: (r >> 1) & 7 (conflict-free for 16 consecutive lanes on 64 banks);
-// 1: 5 (r >> 1) & 7, which also separates the two same-parity rows of every 4-row group
-// (tuning knob)
-#ifndef DION_XT_SWZ
-#define DION_XT_SWZ 0
-#endif
-__device__ __forceinline__ int xt_swz(int r) { return DION_XT_SWZ ? ((5 * (r >> 1)) & 7) : ((r >> 1) & 7); }
+// k ^ ((r >> 1) & 7), conflict-free for 16 consecutive lanes on 64 banks (the alternative
+// 5 (r >> 1) & 7 measured twice the bank conflicts, round 2)
+__device__ __forceinline__ int xt_swz(int r) { return (r >> 1) & 7; }
 
-#ifndef DION_KRBE
-#define DION_KRBE 2
-#endif
-constexpr int kRBE = DION_KRBE;   // 16-row blocks per wave in the fused row kernel (tuning knob)
+constexpr int kRBE = 2;   // 16-row blocks per wave in the fused row kernel (measured default)
 
 // ---- row kernel (not transposed): wave = kRBE x 16 rows, step = 32 columns;
 // lane (t, g) holds columns 16c + 4g .. +3 (c = 0, 1) of rows 16 rb + t.
@@ -2631,236 +2402,13 @@ __device__ __forceinline__ void rpe_load(RowStepE<GDT, KR>& S, const float* __re
     }
 }
 
-template <int RB, int GDT, bool STORE = true>
-__device__ __forceinline__ void rpe_compute(RowStepE<GDT>& S, f32x4 (&acc)[kRBE][RB], const bf16x8* tq,
-                                            const bf16x8* rs, const Split3 (&F)[kRBE][RB / 2], bool has_ef,
-                                            float* __restrict__ M, long ld_m, int j, int lane, uint32_t& nzb) {
-  constexpr int KK = RB / 2;
-  if (has_ef) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      f32x4 e[kRBE];
-#pragma unroll
-      for (int rb = 0; rb < kRBE; ++rb) e[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        Split3 A;
-        ef_sread(rs, c * KK + kk, lane, A);
-#pragma unroll
-        for (int rb = 0; rb < kRBE; ++rb) e[rb] = mfma6_16(A, F[rb][kk], e[rb]);
-      }
-#pragma unroll
-      for (int rb = 0; rb < kRBE; ++rb) S.x[rb][c] += e[rb];
-    }
-  }
-  if (GDT != DION_DTYPE_NONE || has_ef) {
-#pragma unroll
-    for (int rb = 0; rb < kRBE; ++rb)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        if constexpr (GDT == DION_DTYPE_BF16) {
-          const uint2 gv = S.gb[rb][c];
-          S.x[rb][c][0] += __uint_as_float(gv.x << 16);
-          S.x[rb][c][1] += __uint_as_float(gv.x & 0xFFFF0000u);
-          S.x[rb][c][2] += __uint_as_float(gv.y << 16);
-          S.x[rb][c][3] += __uint_as_float(gv.y & 0xFFFF0000u);
-        } else if constexpr (GDT == DION_DTYPE_F32) {
-          S.x[rb][c] += S.gf[rb][c];
-        }
-        if constexpr (STORE) st_part(reinterpret_cast<f32x4*>(M + rb * 16 * ld_m + j + 16 * c), S.x[rb][c]);
-      }
-  }
-#pragma unroll
-  for (int rb = 0; rb < kRBE; ++rb)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-      nzb |= __float_as_uint(S.x[rb][c][0]) | __float_as_uint(S.x[rb][c][1]) | __float_as_uint(S.x[rb][c][2]) |
-             __float_as_uint(S.x[rb][c][3]);
-  // P += X Q: the lane's 8 columns 16 (e >> 2) + 4 g + (e & 3) are the A operand's k-run (KMAP 1)
-  Split3 A[kRBE];
-#pragma unroll
-  for (int rb = 0; rb < kRBE; ++rb) split3(S.x[rb][0], S.x[rb][1], 1.f, A[rb]);
-#pragma unroll
-  for (int cb = 0; cb < RB; ++cb) {
-    Split3 B;
-    ef_sread(tq, cb, lane, B);
-#pragma unroll
-    for (int rb = 0; rb < kRBE; ++rb) acc[rb][cb] = mfma6_16(A[rb], B, acc[rb][cb]);
-  }
-}
-
-// TJ line stores: the updated M tile goes back through the wave's LDS tile and leaves in
-// whole 128-B lines with the non-temporal policy (tuning knob, DION_PA_STLINES)
-// measured on the Llama fc1 group (16 x 28672 x 4096): 4.10 -> 3.84 ms with both (r02)
-#ifndef DION_PA_STLINES
-#define DION_PA_STLINES 1
-#endif
-#ifndef DION_PA_NTLD
-#define DION_PA_NTLD 1
-#endif
-
-template <int RB, int GDT, int PD, bool TJ>
-__global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_ef_kernel(const EfProjArgs e) {
-  constexpr bool kLineStore = TJ && DION_PA_STLINES;
-  constexpr int R = 16 * RB;
-  constexpr int KK = RB / 2;
-  __shared__ bf16x8 tq[2][RB * 3 * 64];
-  __shared__ bf16x8 rs[2][2 * KK * 3 * 64];
-  // TJ: M arrives in whole 128-B lines (lane l: row 8 i + l / 8, 16-B chunk l % 8 of the
-  // step's 32 columns) and is turned into the MFMA layout through a wave-private LDS
-  // tile (chunk k of row r stored at k ^ ((r >> 1) & 7): conflict-free both ways)
-  __shared__ f32x4 xt[TJ ? kPaNW : 1][TJ ? 32 * 8 : 1];
-  const ProjArgs& a = e.p;
-  const BlockXYZ blk = xcd_block();
-  const int b = blk.z;
-  const int kc = blk.y;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  const int lane = tid & 63;
-  const int t = lane & 15;
-  const int g = lane >> 4;
-  const int row_base = blk.x * (16 * kRBE * kPaNW) + wave * (16 * kRBE);
-  const int j_begin = kc * a.kchunk;
-  const int j_end = min(a.cols, j_begin + a.kchunk);
-  const int j_len = j_end - j_begin;
-  const int j_rot = walk_rotation(blk, j_len);
-  auto cj = [&](int j) { const int x = j - j_begin + j_rot; return j_begin + (x >= j_len ? x - j_len : x); };
-  float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 4 * g;
-  const void* G = nullptr;
-  if constexpr (GDT == DION_DTYPE_BF16)
-    G = static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 4 * g;
-  else if constexpr (GDT == DION_DTYPE_F32)
-    G = static_cast<const float*>(a.g[b]) + static_cast<long>(row_base + t) * a.ld_g + 4 * g;
-  float* __restrict__ Mw = a.m[b] + static_cast<long>(row_base + (lane >> 3)) * a.ld_m + 4 * (lane & 7);
-  const float* __restrict__ Rp = e.efr[b];
-  const bool has_ef = Rp != nullptr;
-
-  Split3 F[kRBE][KK];
-  if (has_ef) {
-#pragma unroll
-    for (int rb = 0; rb < kRBE; ++rb)
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        const float* src = e.efp[b] + static_cast<long>(row_base + 16 * rb + t) * R + 32 * kk + 8 * g;
-        split3(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), e.alpha, F[rb][kk]);
-      }
-  } else {
-#pragma unroll
-    for (int rb = 0; rb < kRBE; ++rb)
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) F[rb][kk] = Split3{};
-  }
-
-  f32x4 acc[kRBE][RB];
-#pragma unroll
-  for (int rb = 0; rb < kRBE; ++rb)
-#pragma unroll
-    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint32_t nzb = 0;  // OR of the written bit patterns: nonzero iff some |x| > 0 (or NaN)
-
-  // the K-step's thin (Q) and streamed EF (R') operands arrive pre-split
-  // (presplit_kernel); staging them is a 16-byte copy into double-buffered LDS
-  constexpr int NQ = RB * 3 * 64, NR = 2 * KK * 3 * 64;
-  const u32x4* qs = e.qsplit + b * e.split_stride;
-  const u32x4* rsp = e.rsplit + b * e.split_stride;
-  // X (M, G) arrives PD - 1 steps ahead in a register ring; the split operands one step ahead
-  RowStepE<GDT> S[PD];
-  auto xload = [&](RowStepE<GDT>& T, int j) {
-    if constexpr (TJ) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        T.x[q >> 1][q & 1] = DION_PA_NTLD ? ld_stream(reinterpret_cast<const f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j))
-                                          : *reinterpret_cast<const f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j);
-      rpe_load<GDT>(T, nullptr, G, 0, a.ld_g, j);
-    } else {
-      rpe_load<GDT>(T, M, G, a.ld_m, a.ld_g, j);
-    }
-  };
-  auto xpose = [&](RowStepE<GDT>& T) {
-    f32x4* xw = xt[TJ ? wave : 0];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = 8 * q + (lane >> 3), k = lane & 7;
-      xw[r * 8 + (k ^ xt_swz(r))] = T.x[q >> 1][q & 1];
-    }
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int r = 16 * rb + t, k = 4 * c + g;
-        T.x[rb][c] = xw[r * 8 + (k ^ xt_swz(r))];
-      }
-  };
-  // the inverse: MFMA layout -> LDS -> whole-line non-temporal stores
-  auto xstore = [&](const RowStepE<GDT>& T, int j) {
-    f32x4* xw = xt[TJ ? wave : 0];
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int r = 16 * rb + t, k = 4 * c + g;
-        xw[r * 8 + (k ^ xt_swz(r))] = T.x[rb][c];
-      }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = 8 * q + (lane >> 3), k = lane & 7;
-      st_stream(reinterpret_cast<f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j), xw[r * 8 + (k ^ xt_swz(r))]);
-    }
-  };
-  SplitCopyN<NQ, 64 * kPaNW> TA;
-  SplitCopyN<NR, 64 * kPaNW> EA;
-#pragma unroll
-  for (int k = 0; k < PD - 1; ++k)
-    if (j_begin + 32 * k < j_end) xload(S[k], cj(j_begin + 32 * k));
-  split_copy_load_n(TA, qs + static_cast<long>(cj(j_begin) / 32) * NQ, tid);
-  split_copy_store_n(TA, tq[0], tid);
-  if (has_ef) {
-    split_copy_load_n(EA, rsp + static_cast<long>(cj(j_begin) / 32) * NR, tid);
-    split_copy_store_n(EA, rs[0], tid);
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int j0 = j_begin; j0 < j_end; j0 += 32 * PD) {
-#pragma unroll
-    for (int k = 0; k < PD; ++k) {
-      const int j = j0 + 32 * k;
-      if (j >= j_end) break;
-      const bool more = j + 32 < j_end;
-      if (j + 32 * (PD - 1) < j_end) xload(S[(k + PD - 1) % PD], cj(j + 32 * (PD - 1)));
-      if (more) {
-        split_copy_load_n(TA, qs + static_cast<long>(cj(j + 32) / 32) * NQ, tid);
-        if (has_ef) split_copy_load_n(EA, rsp + static_cast<long>(cj(j + 32) / 32) * NR, tid);
-      }
-      if constexpr (TJ) xpose(S[k]);
-      rpe_compute<RB, GDT, !kLineStore>(S[k], acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, cj(j), lane, nzb);
-      if constexpr (kLineStore) xstore(S[k], cj(j));
-      if (!more) break;
-      split_copy_store_n(TA, tq[cur ^ 1], tid);
-      if (has_ef) split_copy_store_n(EA, rs[cur ^ 1], tid);
-      __syncthreads();
-      cur ^= 1;
-    }
-  }
-
-  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
-#pragma unroll
-  for (int rb = 0; rb < kRBE; ++rb)
-#pragma unroll
-    for (int cb = 0; cb < RB; ++cb)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        out[static_cast<long>(row_base + 16 * rb + 4 * g + q) * R + 16 * cb + t] = acc[rb][cb][q];
-  if (a.nonzero != nullptr && __any((nzb & 0x7FFFFFFFu) != 0u) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
-}
 
 // ---- column kernel (transposed): block = 4 waves x 32 columns, step = 32 rows;
 // lane (t, g) holds columns 2t, 2t + 1 of rows 16 h + 4 g + q (h = 0, 1; q = 0..3):
 // per half h that is the EF accumulator's slice, and per column the 8 rows are
 // the projection's k-run (KMAP 1).
-// cache policy of the transposed pass A's bf16 G loads (64-B row pieces): 1 = nt (tuning knob)
-#ifndef DION_CPE_GNT
-#define DION_CPE_GNT 1
-#endif
+// cache policy of the transposed pass A's bf16 G loads (64-B row pieces): nt (measured faster)
+constexpr int kCpeGnt = 1;
 
 template <int GDT>
 struct ColStepE {
@@ -2879,7 +2427,7 @@ __device__ __forceinline__ void cpe_load(ColStepE<GDT>& S, const float* __restri
       const long row = i0 + 16 * h + q;
       S.x[h][q] = ld_stream(reinterpret_cast<const f32x2*>(M + row * ld_m));
       if constexpr (GDT == DION_DTYPE_BF16)
-        S.gb[h][q] = DION_CPE_GNT
+        S.gb[h][q] = kCpeGnt
                          ? ld_stream(reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(G) + row * ld_g))
                          : *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(G) + row * ld_g);
       else if constexpr (GDT == DION_DTYPE_F32)
@@ -2887,293 +2435,6 @@ __device__ __forceinline__ void cpe_load(ColStepE<GDT>& S, const float* __restri
     }
 }
 
-template <int RB, int GDT>
-__device__ __forceinline__ void cpe_compute(ColStepE<GDT>& S, f32x4 (&acc)[2][RB], const bf16x8* tq,
-                                            const bf16x8* rs, const Split3 (&F)[2][RB / 2], bool has_ef,
-                                            float* __restrict__ M, long ld_m, int i0, int lane, uint32_t& nzb) {
-  constexpr int KK = RB / 2;
-  if (has_ef) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      f32x4 e[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        Split3 A;
-        ef_sread(rs, h * KK + kk, lane, A);
-#pragma unroll
-        for (int c = 0; c < 2; ++c) e[c] = mfma6_16(A, F[c][kk], e[c]);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        S.x[h][q][0] += e[0][q];
-        S.x[h][q][1] += e[1][q];
-      }
-    }
-  }
-  if (GDT != DION_DTYPE_NONE || has_ef) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if constexpr (GDT == DION_DTYPE_BF16) {
-          S.x[h][q][0] += __uint_as_float(S.gb[h][q] << 16);
-          S.x[h][q][1] += __uint_as_float(S.gb[h][q] & 0xFFFF0000u);
-        } else if constexpr (GDT == DION_DTYPE_F32) {
-          S.x[h][q] += S.gf[h][q];
-        }
-        st_stream(reinterpret_cast<f32x2*>(M + static_cast<long>(i0 + 16 * h + q) * ld_m), S.x[h][q]);
-      }
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) nzb |= __float_as_uint(S.x[h][q][0]) | __float_as_uint(S.x[h][q][1]);
-  Split3 A[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-    split3(f32x4{S.x[0][0][c], S.x[0][1][c], S.x[0][2][c], S.x[0][3][c]},
-           f32x4{S.x[1][0][c], S.x[1][1][c], S.x[1][2][c], S.x[1][3][c]}, 1.f, A[c]);
-#pragma unroll
-  for (int cb = 0; cb < RB; ++cb) {
-    Split3 B;
-    ef_sread(tq, cb, lane, B);
-#pragma unroll
-    for (int c = 0; c < 2; ++c) acc[c][cb] = mfma6_16(A[c], B, acc[c][cb]);
-  }
-}
-
-template <int RB, int GDT>
-__global__ void __launch_bounds__(256, 2) colproj_ef_kernel(const EfProjArgs e) {
-  constexpr int R = 16 * RB;
-  constexpr int KK = RB / 2;
-  __shared__ bf16x8 tq[2][RB * 3 * 64];
-  __shared__ bf16x8 rs[2][2 * KK * 3 * 64];
-  const ProjArgs& a = e.p;
-  const BlockXYZ blk = xcd_block_col();
-  const int b = blk.z;
-  const int kc = blk.y;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  const int lane = tid & 63;
-  const int t = lane & 15;
-  const int g = lane >> 4;
-  const int col_base = blk.x * 128 + wave * 32;
-  const int i_begin = kc * a.kchunk;
-  const int i_end = min(a.rows, i_begin + a.kchunk);
-  float* __restrict__ M = a.m[b] + static_cast<long>(4 * g) * a.ld_m + col_base + 2 * t;
-  const void* G = nullptr;
-  if constexpr (GDT == DION_DTYPE_BF16)
-    G = static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(4 * g) * a.ld_g + col_base + 2 * t;
-  else if constexpr (GDT == DION_DTYPE_F32)
-    G = static_cast<const float*>(a.g[b]) + static_cast<long>(4 * g) * a.ld_g + col_base + 2 * t;
-  const float* __restrict__ Tp = a.thin[b];
-  const float* __restrict__ Rp = e.efr[b];
-  const bool has_ef = Rp != nullptr;
-
-  // fixed EF factor: P'[col_base + 2t + c][32 kk + 8 g ...] (B operand of tile c)
-  Split3 F[2][KK];
-  if (has_ef) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        const float* src = e.efp[b] + static_cast<long>(col_base + 2 * t + c) * R + 32 * kk + 8 * g;
-        split3(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), e.alpha, F[c][kk]);
-      }
-  } else {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) F[c][kk] = Split3{};
-  }
-
-  f32x4 acc[2][RB];
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint32_t nzb = 0;
-
-  // the K-step's thin (Q) and streamed EF (R') operands arrive pre-split
-  // (presplit_kernel); staging them is a 16-byte copy into double-buffered LDS
-  constexpr int NQ = RB * 3 * 64, NR = 2 * KK * 3 * 64;
-  const u32x4* qs = e.qsplit + b * e.split_stride;
-  const u32x4* rsp = e.rsplit + b * e.split_stride;
-  ColStepE<GDT> SA, SB;
-  SplitCopy<NQ> TA;
-  SplitCopy<NR> EA;
-  cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i_begin);
-  split_copy_load<NQ>(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
-  split_copy_store<NQ>(TA, tq[0], tid);
-  if (has_ef) {
-    split_copy_load<NR>(EA, rsp + static_cast<long>(i_begin / 32) * NR, tid);
-    split_copy_store<NR>(EA, rs[0], tid);
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int i0 = i_begin; i0 < i_end; i0 += 64) {
-    const bool more = i0 + 32 < i_end;
-    if (more) {
-      if (!DION_SPLIT_FIRST) cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
-      split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 1) * NQ, tid);
-      if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 1) * NR, tid);
-      if (DION_SPLIT_FIRST) cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
-    }
-    cpe_compute<RB, GDT>(SA, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, i0, lane, nzb);
-    if (!more) break;
-    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
-    if (has_ef) split_copy_store<NR>(EA, rs[cur ^ 1], tid);
-    __syncthreads();
-    cur ^= 1;
-    const bool more2 = i0 + 64 < i_end;
-    if (more2) {
-      if (!DION_SPLIT_FIRST) cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
-      split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 2) * NQ, tid);
-      if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 2) * NR, tid);
-      if (DION_SPLIT_FIRST) cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
-    }
-    cpe_compute<RB, GDT>(SB, acc, tq[cur], rs[cur], F, has_ef, M, a.ld_m, i0 + 32, lane, nzb);
-    if (!more2) break;
-    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
-    if (has_ef) split_copy_store<NR>(EA, rs[cur ^ 1], tid);
-    __syncthreads();
-    cur ^= 1;
-  }
-
-  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int cb = 0; cb < RB; ++cb)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        out[static_cast<long>(col_base + 2 * (4 * g + q) + c) * R + 16 * cb + t] = acc[c][cb][q];
-  if (a.nonzero != nullptr && __any((nzb & 0x7FFFFFFFu) != 0u) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
-}
-
-// ---- row projection, no gradient (pass B, transposed: R = M P):
-// the fused row kernel's geometry and loads (lane (t, g): columns 16 c + 4 g .. +3,
-// c = 0, 1, of rows 16 rb + t = the A operand's k-run), KMAP 1.
-template <int RB>
-__device__ __forceinline__ void rpx_compute(const RowStepE<DION_DTYPE_NONE>& S, f32x4 (&acc)[kRBE][RB],
-                                            const bf16x8* tq, int lane) {
-  Split3 A[kRBE];
-#pragma unroll
-  for (int rb = 0; rb < kRBE; ++rb) split3(S.x[rb][0], S.x[rb][1], 1.f, A[rb]);
-#pragma unroll
-  for (int cb = 0; cb < RB; ++cb) {
-    Split3 B;
-    ef_sread(tq, cb, lane, B);
-#pragma unroll
-    for (int rb = 0; rb < kRBE; ++rb) acc[rb][cb] = mfma6_16(A[rb], B, acc[rb][cb]);
-  }
-}
-
-// TJ loads for the pass-B row kernel: M arrives in whole 128-B lines with the
-// non-temporal policy and is turned into the MFMA layout through a wave-private LDS
-// tile, as in rowproj_ef_kernel (tuning knob, DION_PBX_TJ)
-#ifndef DION_PBX_TJ
-#define DION_PBX_TJ 1
-#endif
-
-template <int RB>
-__global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) rowproj_x6_kernel(const ProjArgs a) {
-  constexpr int R = 16 * RB;
-  constexpr bool TJ = DION_PBX_TJ && kRBE == 2;
-  __shared__ bf16x8 tq[2][RB * 3 * 64];
-  __shared__ f32x4 xt[TJ ? 4 : 1][TJ ? 32 * 8 : 1];
-  const BlockXYZ blk = xcd_block();
-  const int b = blk.z;
-  const int kc = blk.y;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  const int lane = tid & 63;
-  const int t = lane & 15;
-  const int g = lane >> 4;
-  const int row_base = blk.x * (64 * kRBE) + wave * (16 * kRBE);
-  const int j_begin = kc * a.kchunk;
-  const int j_end = min(a.cols, j_begin + a.kchunk);
-  const int j_len = j_end - j_begin;
-  const int j_rot = walk_rotation(blk, j_len);
-  auto cj = [&](int j) { const int x = j - j_begin + j_rot; return j_begin + (x >= j_len ? x - j_len : x); };
-  const float* __restrict__ M = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 4 * g;
-  const float* __restrict__ Mw = a.m[b] + static_cast<long>(row_base + (lane >> 3)) * a.ld_m + 4 * (lane & 7);
-  auto xload = [&](RowStepE<DION_DTYPE_NONE>& T, int j) {
-    if constexpr (TJ) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        T.x[q >> 1][q & 1] = ld_stream(reinterpret_cast<const f32x4*>(Mw + static_cast<long>(8 * q) * a.ld_m + j));
-    } else {
-      rpe_load<DION_DTYPE_NONE>(T, M, nullptr, a.ld_m, 0, j);
-    }
-  };
-  auto xpose = [&](RowStepE<DION_DTYPE_NONE>& T) {
-    if constexpr (TJ) {
-      f32x4* xw = xt[wave];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = 8 * q + (lane >> 3), k = lane & 7;
-        xw[r * 8 + (k ^ xt_swz(r))] = T.x[q >> 1][q & 1];
-      }
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const int r = 16 * rb + t, k = 4 * c + g;
-          T.x[rb][c] = xw[r * 8 + (k ^ xt_swz(r))];
-        }
-    }
-  };
-
-  f32x4 acc[kRBE][RB];
-#pragma unroll
-  for (int rb = 0; rb < kRBE; ++rb)
-#pragma unroll
-    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  RowStepE<DION_DTYPE_NONE> SA, SB;
-  constexpr int NQ = RB * 3 * 64;
-  const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
-  SplitCopy<NQ> TA;
-  xload(SA, cj(j_begin));
-  split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j_begin) / 32) * NQ, tid);
-  split_copy_store<NQ>(TA, tq[0], tid);
-  __syncthreads();
-  int cur = 0;
-  for (int j0 = j_begin; j0 < j_end; j0 += 64) {
-    const bool more = j0 + 32 < j_end;
-    if (more) {
-      xload(SB, cj(j0 + 32));
-      split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j0 + 32) / 32) * NQ, tid);
-    }
-    xpose(SA);
-    rpx_compute<RB>(SA, acc, tq[cur], lane);
-    if (!more) break;
-    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
-    __syncthreads();
-    cur ^= 1;
-    const bool more2 = j0 + 64 < j_end;
-    if (more2) {
-      xload(SA, cj(j0 + 64));
-      split_copy_load<NQ>(TA, qs + static_cast<long>(cj(j0 + 64) / 32) * NQ, tid);
-    }
-    xpose(SB);
-    rpx_compute<RB>(SB, acc, tq[cur], lane);
-    if (!more2) break;
-    split_copy_store<NQ>(TA, tq[cur ^ 1], tid);
-    __syncthreads();
-    cur ^= 1;
-  }
-
-  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
-#pragma unroll
-  for (int rb = 0; rb < kRBE; ++rb)
-#pragma unroll
-    for (int cb = 0; cb < RB; ++cb)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        out[static_cast<long>(row_base + 16 * rb + 4 * g + q) * R + 16 * cb + t] = acc[rb][cb][q];
-}
 
 // ---- column projection, no gradient (pass B, not transposed: R = M^T P):
 // block = 4 waves x 16 CT columns, K-step = 32 rows; lane (t, g) loads the run
@@ -3213,13 +2474,10 @@ __device__ __forceinline__ void cpx_compute(const ColStepX6<CT>& S, f32x4 (&acc)
 template <int RB>
 constexpr int colx6_ct() { return RB >= 4 ? 2 : 4; }
 
-#ifndef DION_COLX6_PD
-#define DION_COLX6_PD 2
-#endif
-constexpr int kColX6PD = DION_COLX6_PD;  // register-ring depth of the pass-B column kernel (tuning knob)
+constexpr int kColX6PD = 2;  // register-ring depth of the pass-B column kernel (measured default)
 
 template <int RB, int NW>
-__global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : (NW >= 8 ? DION_COLX6_MINB : 2)) colproj_x6_kernel(const ProjArgs a) {
+__global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : (NW >= 8 ? kColx6Minb : 2)) colproj_x6_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int CT = colx6_ct<RB>();
   __shared__ bf16x8 tq[2][RB * 3 * 64];
@@ -3235,7 +2493,6 @@ __global__ void __launch_bounds__(64 * NW, RB >= 8 ? 1 : (NW >= 8 ? DION_COLX6_M
   const int i_begin = kc * a.kchunk;
   const int i_end = min(a.rows, i_begin + a.kchunk);
   const float* __restrict__ M = a.m[b] + static_cast<long>(8 * g) * a.ld_m + col_base + CT * t;
-  const float* __restrict__ Tp = a.thin[b];
 
   f32x4 acc[CT][RB];
 #pragma unroll
@@ -3417,36 +2674,17 @@ __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a)
 // pre-split P is the A operand (A[row j = 16 cb + t'][k]), one scale per matrix.  Each
 // step's product lands in a fresh accumulator D[j][col] (lane (t, g): R rows CT t + c,
 // r columns 16 cb + 4 g + q) and is added as acc += D / s_col.
-// 16-row blocks per wave of the r = 128 fused pass A row kernel (1 halves its accumulators
-// and EF operand, so the prefetch stage fits; tuning knob) and its pipeline depth
-#ifndef DION_PA_KR8
-#define DION_PA_KR8 2
-#endif
-constexpr int kKR8 = DION_PA_KR8;
-#ifndef DION_PA_PD8
-#define DION_PA_PD8 (DION_PA_KR8 == 1 ? 2 : 1)
-#endif
-// blocks per CU the r = 128 transposed fused pass A is compiled for (tuning knob)
-#ifndef DION_CPEH3_MINB8
-#define DION_CPEH3_MINB8 1
-#endif
-// pipeline depth of the r <= 64 fused pass A row kernel (tuning knob)
-#ifndef DION_PA_PD
-#define DION_PA_PD 2
-#endif
-// blocks per CU the r <= 64 pass-B row kernel is compiled for (tuning knob)
-#ifndef DION_PBR_MINB
-#define DION_PBR_MINB 2
-#endif
-// r > 64 pass-B h3 kernels: the split P two cb at a time, two waves per SIMD (tuning knob)
-#ifndef DION_H3_PAIRS
-#define DION_H3_PAIRS 1
-#endif
-#ifndef DION_PBX
-#define DION_PBX 0  // dev experiments on colproj_h3_kernel's fixed-scale loop (0 = product)
-#endif
+// 16-row blocks per wave of the r = 128 fused pass A row kernel (16-row waves with a prefetch
+// stage measured slower, 5.33 vs 4.60 ms, round 2); it runs with a one-step pipeline
+constexpr int kKR8 = 2;
+// blocks per CU the r = 128 transposed fused pass A is compiled for
+constexpr int kCpeh3Minb8 = 1;
+// blocks per CU the r <= 64 pass-B row kernel is compiled for
+constexpr int kPbrMinb = 2;
+// r > 64 pass-B h3 kernels: the split P two cb at a time, two waves per SIMD
+constexpr int kH3Pairs = 1;
 template <int RB, int NW, int CT>
-__global__ void __launch_bounds__(64 * NW, (RB >= 8 && !DION_H3_PAIRS) ? 1 : 2) colproj_h3_kernel(const ProjArgs a) {
+__global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colproj_h3_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int NQ = RB * 2 * 64;  // f16x8 units of one K-step's P split
   __shared__ f16x8 tq[2][NQ];
@@ -3493,9 +2731,9 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !DION_H3_PAIRS) ? 1 : 2) 
         const int i = i0 + 32 * k;
         if (i >= i_end) break;
         const bool more = i + 32 < i_end;
-        if (DION_SPLIT_FIRST_B && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
+        if (kSplitFirstB && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
         if (i + 32 * (PD - 1) < i_end) cpx_load<CT>(S[(k + PD - 1) % PD], M, a.ld_m, i + 32 * (PD - 1));
-        if (!DION_SPLIT_FIRST_B && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
+        if (!kSplitFirstB && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
         {
           const ColStepX6<CT>& X = S[k];
           Split2h B[CT];
@@ -3505,12 +2743,7 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !DION_H3_PAIRS) ? 1 : 2) 
             const f32x4 lo4{X.x[0][c], X.x[1][c], X.x[2][c], X.x[3][c]};
             const f32x4 hi4{X.x[4][c], X.x[5][c], X.x[6][c], X.x[7][c]};
             if constexpr (FIX) {
-#if DION_PBX == 2 || DION_PBX == 3  // dev experiment: no split (raw bits)
-              B[c].hi = __builtin_bit_cast(f16x8, lo4);
-              B[c].lo = __builtin_bit_cast(f16x8, hi4);
-#else
               split2h(lo4, hi4, fs, B[c]);
-#endif
             } else {
               float m8 = max8abs(lo4, hi4);
               m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
@@ -3519,7 +2752,7 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !DION_H3_PAIRS) ? 1 : 2) 
               split2h(lo4, hi4, sc, B[c]);
             }
           }
-          if constexpr (FIX && RB >= 8 && DION_H3_PAIRS) {
+          if constexpr (FIX && RB >= 8 && kH3Pairs) {
             // r > 64: the split P of two cb at a time (all RB of them would need 64 VGPRs
             // and push the kernel to one wave per SIMD); term by term over (c, cb pair)
 #pragma unroll
@@ -3554,13 +2787,6 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !DION_H3_PAIRS) ? 1 : 2) 
               A[cb].hi = tq[cur][(cb * 2 + 0) * 64 + lane];
               A[cb].lo = tq[cur][(cb * 2 + 1) * 64 + lane];
             }
-#if DION_PBX == 1 || DION_PBX == 3  // dev experiment: no MFMA (every split value stays live)
-#pragma unroll
-            for (int c = 0; c < CT; ++c) {
-              const u32x4 hb = __builtin_bit_cast(u32x4, B[c].hi) ^ __builtin_bit_cast(u32x4, B[c].lo);
-              acc[c][0] = __builtin_bit_cast(f32x4, __builtin_bit_cast(u32x4, acc[c][0]) ^ hb);
-            }
-#else
 #pragma unroll
             for (int c = 0; c < CT; ++c)
 #pragma unroll
@@ -3576,7 +2802,6 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !DION_H3_PAIRS) ? 1 : 2) 
 #pragma unroll
               for (int cb = 0; cb < RB; ++cb)
                 acc[c][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].hi, B[c].hi, acc[c][cb], 0, 0, 0);
-#endif
           } else {
 #pragma unroll
             for (int cb = 0; cb < RB; ++cb) {
@@ -3800,12 +3025,12 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
       const int j = j0 + 32 * k;
       if (j >= j_end) break;
       const bool more = j + 32 < j_end;
-      if (!DION_SPLIT_FIRST && j + 32 * (PD - 1) < j_end) xload(S[(k + PD - 1) % PD], j + 32 * (PD - 1));
+      if (!kSplitFirst && j + 32 * (PD - 1) < j_end) xload(S[(k + PD - 1) % PD], j + 32 * (PD - 1));
       if (more) {
         split_copy_load_n(TA, qs + static_cast<long>((j + 32) / 32) * NQ, tid);
         if (has_ef) split_copy_load_n(EA, rsp + static_cast<long>((j + 32) / 32) * NR, tid);
       }
-      if (DION_SPLIT_FIRST && j + 32 * (PD - 1) < j_end) xload(S[(k + PD - 1) % PD], j + 32 * (PD - 1));
+      if (kSplitFirst && j + 32 * (PD - 1) < j_end) xload(S[(k + PD - 1) % PD], j + 32 * (PD - 1));
       xpose(S[k]);
       compute(S[k], tq[cur], rs[cur]);
       xstore(S[k], j);
@@ -3844,7 +3069,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
 // four lanes (t, g = 0..3)), Q the A operand: D[16 cb + 4 g + q][col 2t + c] is added as
 // acc += D / s_col.  The matrix's max |M| goes into the flag for a fixed-scale pass B.
 template <int RB, int GDT>
-__global__ void __launch_bounds__(256, RB >= 8 ? DION_CPEH3_MINB8 : 2) colproj_efh3_kernel(const EfProjArgs e) {
+__global__ void __launch_bounds__(256, RB >= 8 ? kCpeh3Minb8 : 2) colproj_efh3_kernel(const EfProjArgs e) {
   constexpr int R = 16 * RB;
   constexpr int KK = RB / 2;
   constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;  // f16x8 units of one K-step's splits
@@ -3979,10 +3204,10 @@ __global__ void __launch_bounds__(256, RB >= 8 ? DION_CPEH3_MINB8 : 2) colproj_e
   for (int i0 = i_begin; i0 < i_end; i0 += 64) {
     const bool more = i0 + 32 < i_end;
     if (more) {
-      if (!DION_SPLIT_FIRST) cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
+      if (!kSplitFirst) cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
       split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 1) * NQ, tid);
       if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 1) * NR, tid);
-      if (DION_SPLIT_FIRST) cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
+      if (kSplitFirst) cpe_load<GDT>(SB, M, G, a.ld_m, a.ld_g, i0 + 32);
     }
     compute(SA, tq[cur], rs[cur], i0);
     if (!more) break;
@@ -3992,10 +3217,10 @@ __global__ void __launch_bounds__(256, RB >= 8 ? DION_CPEH3_MINB8 : 2) colproj_e
     cur ^= 1;
     const bool more2 = i0 + 64 < i_end;
     if (more2) {
-      if (!DION_SPLIT_FIRST) cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
+      if (!kSplitFirst) cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
       split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 2) * NQ, tid);
       if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 2) * NR, tid);
-      if (DION_SPLIT_FIRST) cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
+      if (kSplitFirst) cpe_load<GDT>(SA, M, G, a.ld_m, a.ld_g, i0 + 64);
     }
     compute(SB, tq[cur], rs[cur], i0 + 32);
     if (!more2) break;
@@ -4027,7 +3252,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? DION_CPEH3_MINB8 : 2) colproj_e
 // (one scale per matrix); with pass A's max |M| the step's products accumulate in place
 // under one scale for the matrix, else each row gets a per-step scale (as in pass A).
 template <int RB, int NW>
-__global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >= 8) ? 1 : (RB <= 4 ? DION_PBR_MINB : 2))
+__global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ? 1 : (RB <= 4 ? kPbrMinb : 2))
     rowproj_h3_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int NQ = RB * 2 * 64;
@@ -4044,9 +3269,8 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >=
   const int row_base = blk.x * (16 * kRBE * NW) + wave * (16 * kRBE);
   const int j_begin = kc * a.kchunk;
   const int j_end = min(a.cols, j_begin + a.kchunk);
-  const int j_len = j_end - j_begin;
-  const int j_rot = walk_rotation(blk, j_len);
-  auto cj = [&](int j) { const int x = j - j_begin + j_rot; return j_begin + (x >= j_len ? x - j_len : x); };
+
+  auto cj = [](int j) { return j; };
   const float* __restrict__ Mw = a.m[b] + static_cast<long>(row_base + (lane >> 3)) * a.ld_m + 4 * (lane & 7);
   auto xload = [&](RowStepE<DION_DTYPE_NONE>& T, int j) {
 #pragma unroll
@@ -4098,7 +3322,7 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >=
           split2h(X.x[rb][0], X.x[rb][1], sx, Bx[rb]);
         }
       }
-      if constexpr (FIX && RB >= 8 && DION_H3_PAIRS) {
+      if constexpr (FIX && RB >= 8 && kH3Pairs) {
         // r > 64: two cb of the split P at a time (see colproj_h3_kernel)
 #pragma unroll
         for (int cp = 0; cp < RB; cp += 2) {
@@ -4169,9 +3393,9 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >=
     for (int j0 = j_begin; j0 < j_end; j0 += 64) {
       const bool more = j0 + 32 < j_end;
       if (more) {
-        if (!DION_SPLIT_FIRST_B) xload(SB, cj(j0 + 32));
+        if (!kSplitFirstB) xload(SB, cj(j0 + 32));
         split_copy_load_n(TA, qs + static_cast<long>(cj(j0 + 32) / 32) * NQ, tid);
-        if (DION_SPLIT_FIRST_B) xload(SB, cj(j0 + 32));
+        if (kSplitFirstB) xload(SB, cj(j0 + 32));
       }
       xpose(SA);
       compute(SA, tq[cur]);
@@ -4181,9 +3405,9 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !DION_H3_PAIRS) || NW >=
       cur ^= 1;
       const bool more2 = j0 + 64 < j_end;
       if (more2) {
-        if (!DION_SPLIT_FIRST_B) xload(SA, cj(j0 + 64));
+        if (!kSplitFirstB) xload(SA, cj(j0 + 64));
         split_copy_load_n(TA, qs + static_cast<long>(cj(j0 + 64) / 32) * NQ, tid);
-        if (DION_SPLIT_FIRST_B) xload(SA, cj(j0 + 64));
+        if (kSplitFirstB) xload(SA, cj(j0 + 64));
       }
       xpose(SB);
       compute(SB, tq[cur]);
@@ -4284,7 +3508,7 @@ Geo colproj_geo(int rows, int cols, int batch, bool panel, int kalign = 16) {
 }
 
 // colproj_x6_kernel: NW waves of 16 CT columns per block (CT = 2 for r >= 64, else 4), 32-row K-steps
-constexpr int kColX6NW = DION_COLX6_NW;
+constexpr int kColX6NW = 4;
 Geo colx6_geo(int rows, int cols, int batch, int r) {
   Geo g;
   g.gx = static_cast<int>(ceil_div(cols, (r >= 64 ? 32 : 64) * kColX6NW));
@@ -4301,61 +3525,28 @@ Geo colx6_geo(int rows, int cols, int batch, int r) {
 bool rowproj_fast_ok(int rows, int cols, int r) { return rows % (64 * kRB) == 0 && cols % 32 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
 bool colproj_fast_ok(int rows, int cols, int r) { return cols % 256 == 0 && rows % 16 == 0 && r % 16 == 0 && r <= 128 && r != 48 && r != 80 && r != 96 && r != 112; }
 
-// rows (or columns) one rank-update block streams; DION_RANK_STREAM overrides (tuning)
-int rank_stream_len() {
-  static const int v = [] {
-    const char* e = getenv("DION_RANK_STREAM");
-    const int x = e ? atoi(e) : 0;
-    return (x >= 64 && x % 64 == 0) ? x : 512;
-  }();
-  return v;
-}
-
-// rank-update kernel choice: 0 = per-wave factor (rank_update_kernel), 1..4 =
-// rank_stream_kernel with (NW, D) = (4, 2), (4, 3), (8, 2), (8, 3); DION_RANK_VARIANT overrides
-int rank_stream_variant() {
-  static const int v = [] {
-    const char* e = getenv("DION_RANK_VARIANT");
-    const int x = e ? atoi(e) : 3;
-    return (x >= 0 && x <= 4) ? x : 3;
-  }();
-  return v;
-}
+// rank_stream_kernel: rows (or columns) one block streams, waves per block, X tiles in flight
+// (measured fastest of (NW, D) in {4, 8} x {2, 3} on the Llama set, round 2)
+constexpr int kRankStreamLen = 512;
+constexpr int kRankNW = 8;
+constexpr int kRankD = 2;
 
 // pre-split thin operand of the x6 projections (rows = the contraction index)
 size_t thin_presplit_bytes(int rows, int r, int batch) { return static_cast<size_t>(rows) * r * 6 * batch + 1024; }
 
-// pass A (not transposed) through the fp16x3 row kernel (rowproj_efh3_kernel; tuning knob)
-#ifndef DION_PA_H3
-#define DION_PA_H3 1
-#endif
-// pass A, transposed, through the fp16x3 column kernel (colproj_efh3_kernel; tuning knob)
-#ifndef DION_PA_H3T
-#define DION_PA_H3T 1
-#endif
-// pass B through the fp16x3 column kernel (colproj_h3_kernel) instead of bf16x6 (tuning knob)
-#ifndef DION_PB_H3
-#define DION_PB_H3 1
-#endif
-// pass B, transposed, through the fp16x3 row kernel (rowproj_h3_kernel) instead of bf16x6 (tuning knob)
-#ifndef DION_PB_H3R
-#define DION_PB_H3R 1
-#endif
+// pass B through the fp16x3 column kernel (colproj_h3_kernel) instead of bf16x6 (measured default)
+constexpr int kPbH3 = 1;
+// pass B, transposed, through the fp16x3 row kernel (rowproj_h3_kernel) instead of bf16x6 (measured default)
+constexpr int kPbH3r = 1;
 // waves per block of rowproj_h3_kernel: one LDS copy of the step's P split serves 32 NW rows
-// of M (tuning knob)
-#ifndef DION_PBR_NW
-#define DION_PBR_NW 4
-#endif
-constexpr int kPbRNW = DION_PBR_NW;
-// columns per lane of colproj_h3_kernel (2: 8-byte loads, 4: 16-byte loads; tuning knob)
-#ifndef DION_COLH3_CT
-#define DION_COLH3_CT 4
-#endif
-constexpr int kColH3CT = DION_COLH3_CT;
+// of M (measured default)
+constexpr int kPbRNW = 4;
+// columns per lane of colproj_h3_kernel (2: 8-byte loads, 4: 16-byte loads)
+constexpr int kColH3CT = 4;
 // r > 64 (RB = 8) keeps 2 columns per lane: 4 would need 256+ VGPRs (one wave per SIMD)
 constexpr int colh3_ct(int r) { return r > 64 ? 2 : kColH3CT; }
 bool colh3_ok(int rows, int cols, int r) {
-  return DION_PB_H3 && rows % 32 == 0 && cols % (16 * colh3_ct(r) * kColX6NW) == 0;
+  return kPbH3 && rows % 32 == 0 && cols % (16 * colh3_ct(r) * kColX6NW) == 0;
 }
 Geo colh3_geo(int rows, int cols, int batch, int r) {
   Geo g;
@@ -4383,13 +3574,9 @@ float h3_scale_host(float amax) {
 }
 
 // the weight update's rank_stream_kernel on h3 products (3 fp16 MFMAs per product instead
-// of bf16x6's 6; tuning knob)
-#ifndef DION_RANK_H3
-#define DION_RANK_H3 1
-#endif
-constexpr bool kRankH3 = DION_RANK_H3 != 0;
+// of bf16x6's 6)
+constexpr bool kRankH3 = (1) != 0;
 
-size_t ef_presplit_bytes(int mp, int r, int batch) { return static_cast<size_t>(mp) * r * 6 * batch; }
 
 // two pre-split operand buffers (Q and R', n_Q x r each) of dion_project_p_ef, after the slabs
 size_t presplit_stride(int nq, int r) { return static_cast<size_t>(nq) * r * 3 / 8; }  // uint4 per matrix
@@ -4401,18 +3588,8 @@ int pa_row_block(int r) { return 16 * (r > 64 ? kKR8 : kRBE) * kPaNW; }
 
 bool proj_ef_ok(int m, int n, int r, bool transposed) {
   // r = 128 (the Mixtral config) only through the h3 kernels
-  if (r != 32 && r != 64 && !(r == 128 && (transposed ? DION_PA_H3T : DION_PA_H3))) return false;
+  if (r != 32 && r != 64 && r != 128) return false;
   return transposed ? (n % 128 == 0 && m % 32 == 0) : (m % pa_row_block(r) == 0 && n % 32 == 0);
-}
-
-// rowproj_ef_kernel loads M in whole lines (TJ, default) or in the MFMA layout directly
-// (DION_PA_LINES=0); measured 1 % apart on the Llama fc1 batch
-bool pa_lines() {
-  static const bool v = [] {
-    const char* e = getenv("DION_PA_LINES");
-    return e == nullptr || atoi(e) != 0;
-  }();
-  return v;
 }
 
 Geo proj_ef_geo(int m, int n, int batch, bool transposed, int r) {
@@ -4552,7 +3729,7 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
                   (row_mode ? rows % (64 * kRBE) == 0
                             : (rows % 32 == 0 && cols % ((r >= 64 ? 32 : 64) * kColX6NW) == 0));
   const bool h3 = fast && gdt == DION_DTYPE_NONE &&
-                  (row_mode ? (DION_PB_H3R && rows % (16 * kRBE * kPbRNW) == 0) : colh3_ok(rows, cols, r));
+                  (row_mode ? (kPbH3r && rows % (16 * kRBE * kPbRNW) == 0) : colh3_ok(rows, cols, r));
   const Geo geo = row_mode ? rowproj_geo(rows, cols, batch,
                                          h3 ? 16 * kRBE * kPbRNW : x6 ? 64 * kRBE : (fast ? 64 * kRB : 128))
                  : h3      ? colh3_geo(rows, cols, batch, r)
@@ -4645,8 +3822,6 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
       constexpr int GD = decltype(Gc)::value;
       if (h3 && row_mode)
         hipLaunchKernelGGL((rowproj_h3_kernel<RB, kPbRNW>), grid, dim3(64 * kPbRNW), 0, st, a);
-      else if (x6 && row_mode)
-        hipLaunchKernelGGL((rowproj_x6_kernel<RB>), grid, dim3(256), 0, st, a);
       else if (h3)
         hipLaunchKernelGGL((colproj_h3_kernel<RB, kColX6NW, colh3_ct(16 * RB)>), grid, dim3(64 * kColX6NW), 0, st, a);
       else if (x6)
@@ -4973,7 +4148,7 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
         break;
       }
       case DION_OP_EF_APPLY:
-        n = ef_presplit_bytes(mp, d->r, chunk);
+        n = 0;  // the update splits its factors in-kernel
         break;
       case DION_OP_ORTHONORMALIZE: {
         if (d->r > d->m || d->r > d->n)
@@ -5061,13 +4236,12 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
     const size_t need = slab + presplit_bytes(nq, d->r, nb);
     if (need > ws_bytes || ws == nullptr)
       return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
-    const bool h3 = tr ? DION_PA_H3T != 0 : DION_PA_H3 != 0;
-    const long sstride = h3 ? static_cast<long>(nq) * d->r / 4 : static_cast<long>(presplit_stride(nq, d->r));
+    const long sstride = static_cast<long>(nq) * d->r / 4;
     u32x4* qsplit = reinterpret_cast<u32x4*>(static_cast<char*>(ws) + slab);
     u32x4* rsplit = qsplit + sstride * nb;
     uint32_t* amax = nullptr;
     float* inv = nullptr;
-    if (h3) {
+    {
       // fp16x3: per-matrix |max| of Q, R' and P', then the two fp16 limbs of Q and R'
       char* tail = reinterpret_cast<char*>(rsplit + sstride * nb);
       amax = reinterpret_cast<uint32_t*>(tail);
@@ -5108,25 +4282,6 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
       hipLaunchKernelGGL(presplit16_kernel, pgrid, dim3(256), 0, st, pa);
       rc = check_launch("presplit16");
       if (rc != DION_OK) return rc;
-    } else {
-      PresplitArgs pa;
-      memset(&pa, 0, sizeof(pa));
-      pa.rows = nq;
-      pa.r = d->r;
-      pa.stride = sstride;
-      const dim3 pgrid(static_cast<unsigned>(ceil_div(static_cast<long>(nq) * d->r / 8, 256)), nb);
-      for (int b = 0; b < nb; ++b) pa.src[b] = Q[b0 + b];
-      pa.dst = qsplit;
-      pa.layout = 0;
-      pa.kmap = 1;
-      hipLaunchKernelGGL(presplit_kernel, pgrid, dim3(256), 0, st, pa);
-      for (int b = 0; b < nb; ++b) pa.src[b] = ef->R[b0 + b];
-      pa.dst = rsplit;
-      pa.layout = 1;
-      pa.kmap = 0;
-      hipLaunchKernelGGL(presplit_kernel, pgrid, dim3(256), 0, st, pa);
-      rc = check_launch("presplit");
-      if (rc != DION_OK) return rc;
     }
     float* out = P + static_cast<long>(b0) * mp * d->r;
     EfProjArgs e;
@@ -5161,23 +4316,10 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
       constexpr int RB = decltype(RBc)::value;
       return dispatch_gdt(d->g_dtype, [&](auto Gc) {
         constexpr int GD = decltype(Gc)::value;
-        if constexpr (RB == 8) {  // r = 128: the h3 kernels only (proj_ef_ok)
-          if (tr)
-            hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
-          else
-            hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, DION_PA_PD8, kKR8>), grid, dim3(64 * kPaNW), 0, st, e);
-        } else {
-          if (tr && h3)
-            hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
-          else if (tr)
-            hipLaunchKernelGGL((colproj_ef_kernel<RB, GD>), grid, dim3(256), 0, st, e);
-          else if (h3)
-            hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, DION_PA_PD>), grid, dim3(64 * kPaNW), 0, st, e);
-          else if (pa_lines())
-            hipLaunchKernelGGL((rowproj_ef_kernel<RB, GD, 2, true>), grid, dim3(64 * kPaNW), 0, st, e);
-          else
-            hipLaunchKernelGGL((rowproj_ef_kernel<RB, GD, 2, false>), grid, dim3(64 * kPaNW), 0, st, e);
-        }
+        if (tr)
+          hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
+        else  // r = 128: one-step pipeline (register budget)
+          hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, RB >= 8 ? 1 : 2>), grid, dim3(64 * kPaNW), 0, st, e);
         return check_launch(tr ? "colproj_ef" : "rowproj_ef");
       });
     };
@@ -5571,7 +4713,6 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
     const int flen = d->transposed ? d->m : d->n;
     const int slen = d->transposed ? d->n : d->m;
     const dim3 grid(static_cast<unsigned>(ceil_div(flen, 128)), static_cast<unsigned>(ceil_div(slen, kEfStream)), nb);
-    const int rh = rpad / 2;
     bool split_ok = (d->m % 32 == 0) && (d->n % 32 == 0) && (r % 16 == 0) && r <= 128 &&
                     aligned16(a.P) && aligned16(a.R) && (ldv(d->ld_m, d->n) % 4 == 0) &&
                     (W == nullptr || ldv(d->ld_w, d->n) % 4 == 0);
@@ -5579,29 +4720,7 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
     if (M == nullptr && !split_ok)
       return fail(DION_E_UNSUPPORTED, "weight-only update needs the rank-update kernel (%dx%d r=%d)", d->m, d->n, r);
     if (split_ok) {
-      const int flen = d->transposed ? d->m : d->n;
-      const int slen = d->transposed ? d->n : d->m;
-      const int s_len = rank_stream_len();
-      const dim3 grid(static_cast<unsigned>(ceil_div(flen, 128)), static_cast<unsigned>(ceil_div(slen, s_len)), nb);
-      // the streamed factor P split once per call (instead of once per tile per wave) when the
-      // caller gave the workspace dion_workspace_bytes(DION_OP_EF_APPLY) asks for
-      const long sstride = static_cast<long>(mp) * r * 3 / 8;
-      const bool pre = ws != nullptr && ws_bytes >= ef_presplit_bytes(mp, r, nb) && (mp % 32 == 0);
-      u32x4* ssplit = static_cast<u32x4*>(ws);
-      if (pre) {
-        PresplitArgs pa;
-        memset(&pa, 0, sizeof(pa));
-        for (int b = 0; b < nb; ++b) pa.src[b] = a.P + static_cast<long>(b) * mp * r;
-        pa.dst = ssplit;
-        pa.stride = sstride;
-        pa.rows = mp;
-        pa.r = r;
-        pa.layout = 2;
-        const dim3 pgrid(static_cast<unsigned>(ceil_div(static_cast<long>(mp) * r / 8, 256)), nb);
-        hipLaunchKernelGGL(presplit_kernel, pgrid, dim3(256), 0, st, pa);
-        rc = check_launch("presplit(P)");
-        if (rc != DION_OK) return rc;
-      }
+      const int s_len = kRankStreamLen;
       for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1 && W == nullptr) break;
         if (pass == 0 && M == nullptr) continue;
@@ -5613,9 +4732,7 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
         }
         ra.S = a.P;
         ra.s_stride = static_cast<long>(mp) * r;
-        ra.Ssplit = pre ? ssplit : nullptr;
         ra.s_len = s_len;
-        ra.ss_stride = sstride;
         ra.nonzero = a.nonzero;
         ra.rows = d->m;
         ra.cols = d->n;
@@ -5640,8 +4757,7 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
         }
         auto launch = [&](auto RUc) {
           constexpr int RUv = decltype(RUc)::value;
-          const int variant = pre ? 0 : rank_stream_variant();
-          if (variant != 0) {
+          {
             // rank_stream_kernel: NW-wave blocks share the split streamed factor through LDS
             ra.s_len = s_len;
             // Both orientations run with the 32-wide strips across X's columns and the
@@ -5664,26 +4780,8 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
               else
                 hipLaunchKernelGGL((rank_stream_kernel<RUv, false, NWv, Dv>), g2, dim3(64 * NWv), 0, st, ra);
             };
-            using I4 = std::integral_constant<int, 4>;
-            using I8 = std::integral_constant<int, 8>;
-            using I2 = std::integral_constant<int, 2>;
-            using I3 = std::integral_constant<int, 3>;
-            switch (variant) {
-              case 1: go(I4{}, I2{}); break;
-              case 2: go(I4{}, I3{}); break;
-              case 3: go(I8{}, I2{}); break;
-              default: go(I8{}, I3{}); break;
-            }
-            return;
+            go(std::integral_constant<int, kRankNW>{}, std::integral_constant<int, kRankD>{});
           }
-          if (pre && d->transposed)
-            hipLaunchKernelGGL((rank_update_kernel<RUv, true, true>), grid, dim3(256), 0, st, ra);
-          else if (pre)
-            hipLaunchKernelGGL((rank_update_kernel<RUv, false, true>), grid, dim3(256), 0, st, ra);
-          else if (d->transposed)
-            hipLaunchKernelGGL((rank_update_kernel<RUv, true, false>), grid, dim3(256), 0, st, ra);
-          else
-            hipLaunchKernelGGL((rank_update_kernel<RUv, false, false>), grid, dim3(256), 0, st, ra);
         };
         switch (r / 16) {
           case 1: launch(std::integral_constant<int, 1>{}); break;

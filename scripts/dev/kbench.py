@@ -11,7 +11,6 @@ B, r = 16 if not T else 16, int(os.environ.get("KB_R", "64"))  # KB_R=128: Mixtr
 mp, nq = (n, m) if T else (m, n)
 dev = torch.device("cuda", 0)
 codec = HipDionCodec(dev)
-codec.ef_presplit = op.endswith("_pre")
 torch.manual_seed(0)
 Ms = [torch.randn(m, n, device=dev) * 1e-3 for _ in range(B)]
 Gs = [(torch.randn(m, n, device=dev) * 1e-3).to(torch.bfloat16) for _ in range(B)]
@@ -42,8 +41,7 @@ variants = [op] if len(sys.argv) <= 3 else sys.argv[3].split(",")
 for rnd in range(3):
     for v in variants:
         op = v
-        codec.ef_presplit = op.endswith("_pre")
-        torch.cuda.synchronize()
+                torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
             run()
