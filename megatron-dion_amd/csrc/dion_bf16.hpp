@@ -809,11 +809,8 @@ __global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) b16_stream_kernel(co
 // ----------------------------------------------------------------------------- host side
 namespace b16 {
 
-// the update on b16_stream_kernel (rank-stream geometry) where the shapes allow (tuning knob)
-#ifndef DION_B16_STREAM
-#define DION_B16_STREAM 1
-#endif
-constexpr bool kB16Stream = DION_B16_STREAM != 0;
+// the update on b16_stream_kernel (rank-stream geometry) where the shapes allow
+constexpr bool kB16Stream = true;
 
 
 int rpad_of(int r) { return (r + 15) / 16 * 16; }
@@ -833,12 +830,12 @@ Geo geo(int out_rows, int K, int batch) {
 }
 
 // the streaming kernels (b16_row_kernel / b16_col_kernel): whole blocks, r a multiple of 16,
-// bf16 or no gradient (shape rules here; pointer alignment is checked at launch)
-#ifndef DION_B16_FAST
-#define DION_B16_FAST 1
-#endif
+// bf16 or no gradient (shape rules here; pointer alignment is checked at launch).  Measured
+// and not kept: 8-wave blocks for the read-only pass B (column 0.42 -> 0.49 ms, row equal),
+// and dword-paired bf16 M accesses in b16_stream_kernel (2.15 -> 2.28 ms; round 3)
+constexpr bool kB16Fast = true;
 bool fast_ok(bool row_mode, int m, int n, int r, int gdt) {
-  if (!DION_B16_FAST || r % 16 != 0 || r > 128 || (gdt != DION_DTYPE_NONE && gdt != DION_DTYPE_BF16)) return false;
+  if (!kB16Fast || r % 16 != 0 || r > 128 || (gdt != DION_DTYPE_NONE && gdt != DION_DTYPE_BF16)) return false;
   return row_mode ? (m % kB16RowBlk == 0 && n % 64 == 0) : (n % kB16ColBlk == 0 && m % 32 == 0);
 }
 
