@@ -2674,9 +2674,16 @@ __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a)
 // pre-split P is the A operand (A[row j = 16 cb + t'][k]), one scale per matrix.  Each
 // step's product lands in a fresh accumulator D[j][col] (lane (t, g): R rows CT t + c,
 // r columns 16 cb + 4 g + q) and is added as acc += D / s_col.
-// 16-row blocks per wave of the r = 128 fused pass A row kernel (16-row waves with a prefetch
-// stage measured slower, 5.33 vs 4.60 ms, round 2); it runs with a one-step pipeline
+// the r = 128 fused pass A row kernel: 32-row waves in 4-wave blocks, one-step pipeline (324
+// VGPRs with the EF operand: one wave per SIMD).  Measured slower: 16-row waves in 4-wave
+// blocks with a prefetch stage (5.33 vs 4.60 ms, round 2: twice the staging traffic), and
+// 16-row waves in 8-wave blocks (184 VGPRs, two waves per SIMD, the same 128 rows per staged
+// step: 5.84 vs 4.79 ms, round 3) -- each wave reads the whole staged Q and R' splits (32 KB
+// per 32-column step at r = 128) for its rows, so halving the rows per wave doubles the LDS
+// operand reads per HBM byte (6.4x), and LDS bandwidth, not occupancy, bounds the kernel.
 constexpr int kKR8 = 2;
+constexpr int kNW8 = 4;
+constexpr int kPD8 = 1;
 // blocks per CU the r = 128 transposed fused pass A is compiled for
 constexpr int kCpeh3Minb8 = 1;
 // blocks per CU the r <= 64 pass-B row kernel is compiled for
@@ -2847,14 +2854,14 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colpr
 // holds row 16 rb + t, k-run KMAP 1) with a per-step scale per row (max over the lanes
 // (t, g = 0..3)), Q the A operand: each step lands in a fresh accumulator
 // D[16 cb + 4 g + q][row t] and is added as acc += D / s_row.
-template <int RB, int GDT, int PD, int KR = kRBE>
-__global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(const EfProjArgs e) {
+template <int RB, int GDT, int PD, int KR = kRBE, int NW = kPaNW>
+__global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : 8 / NW) rowproj_efh3_kernel(const EfProjArgs e) {
   constexpr int R = 16 * RB;
   constexpr int KK = RB / 2;
   constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;  // f16x8 units of one K-step's splits
   __shared__ f16x8 tq[2][NQ];
   __shared__ f16x8 rs[2][NR];
-  __shared__ f32x4 xt[kPaNW][16 * KR * 8];
+  __shared__ f32x4 xt[NW][16 * KR * 8];
   const ProjArgs& a = e.p;
   const BlockXYZ blk = xcd_block();
   const int b = blk.z;
@@ -2865,7 +2872,7 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
-  const int row_base = blk.x * (16 * KR * kPaNW) + wave * (16 * KR);
+  const int row_base = blk.x * (16 * KR * NW) + wave * (16 * KR);
   const int j_begin = kc * a.kchunk;
   const int j_end = min(a.cols, j_begin + a.kchunk);
   const void* G = nullptr;
@@ -3006,8 +3013,8 @@ __global__ void __launch_bounds__(64 * kPaNW, 8 / kPaNW) rowproj_efh3_kernel(con
     }
   };
 
-  SplitCopyN<NQ, 64 * kPaNW> TA;
-  SplitCopyN<NR, 64 * kPaNW> EA;
+  SplitCopyN<NQ, 64 * NW> TA;
+  SplitCopyN<NR, 64 * NW> EA;
 #pragma unroll
   for (int k = 0; k < PD - 1; ++k)
     if (j_begin + 32 * k < j_end) xload(S[k], j_begin + 32 * k);
@@ -3584,7 +3591,7 @@ size_t presplit_bytes(int nq, int r, int batch) { return 2 * 16 * presplit_strid
 
 // deferred-EF pass A (rowproj_ef_kernel / colproj_ef_kernel)
 // rows per block of the fused pass A row kernel (r = 128 may run 16-row waves)
-int pa_row_block(int r) { return 16 * (r > 64 ? kKR8 : kRBE) * kPaNW; }
+int pa_row_block(int r) { return r > 64 ? 16 * kKR8 * kNW8 : 16 * kRBE * kPaNW; }
 
 bool proj_ef_ok(int m, int n, int r, bool transposed) {
   // r = 128 (the Mixtral config) only through the h3 kernels
@@ -4319,7 +4326,8 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
         if (tr)
           hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
         else  // r = 128: one-step pipeline (register budget)
-          hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, RB >= 8 ? 1 : 2>), grid, dim3(64 * kPaNW), 0, st, e);
+          hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, RB >= 8 ? kPD8 : 2, RB >= 8 ? kKR8 : kRBE, RB >= 8 ? kNW8 : kPaNW>),
+                             grid, dim3(64 * (RB >= 8 ? kNW8 : kPaNW)), 0, st, e);
         return check_launch(tr ? "colproj_ef" : "rowproj_ef");
       });
     };
