@@ -75,7 +75,7 @@ WORKLOADS = {
 # ef_apply is two launches of the same instance (M, then W), each streaming 8 B per element
 KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("project_p", True): ("colproj_fast_kernel<4, 2>", 1),
-             ("project_p_ef", False): ("rowproj_efh3_kernel<4, 2, 2, 2>", 1),
+             ("project_p_ef", False): ("rowproj_efh3_kernel<4, 2, 2, 2, 4>", 1),
              ("project_p_ef", True): ("colproj_efh3_kernel<4, 2>", 1),
              ("ef_apply_w", False): ("rank_stream_kernel<4, false, 8, 2, true>", 1),
              ("ef_apply_w", True): ("rank_stream_kernel<4, false, 8, 2, true>", 1),
@@ -285,7 +285,7 @@ def kernel_names(r):
         out[("project_r", False)] = (f"colproj_h3_kernel<{rb}, 4, 2>", 1)
     if r > 64 and ("project_p_ef", False) in out:
         # r = 128: the h3 row kernel runs with pipeline depth 1 (register budget)
-        out[("project_p_ef", False)] = (f"rowproj_efh3_kernel<{rb}, 2, 1, 2>", 1)
+        out[("project_p_ef", False)] = (f"rowproj_efh3_kernel<{rb}, 2, 1, 2, 4>", 1)
     return out
 
 
