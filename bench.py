@@ -305,8 +305,8 @@ def launch_ranks(args) -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="llama3-8b-2d-grad-set-r64", choices=sorted(WORKLOADS))
     ap.add_argument("--layers", type=int, default=0, help="layers of the workload (0 = its default); "
                                                           "fewer only for debugging")

@@ -202,17 +202,29 @@ struct B16ThinArgs {
   int K, Kp, r, rpad, src_bf16;
 };
 
+// one 64 (k) x 64 (c) tile per block through LDS: coalesced row reads of T (c contiguous),
+// coalesced row writes of tt (k contiguous)
 __global__ void __launch_bounds__(256) b16_thin_kernel(const B16ThinArgs a) {
-  const int b = blockIdx.y;
-  const long total = static_cast<long>(a.rpad) * a.Kp;
-  for (long i = static_cast<long>(blockIdx.x) * 256 + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
-    const int c = static_cast<int>(i / a.Kp), k = static_cast<int>(i - static_cast<long>(c) * a.Kp);
+  __shared__ uint16_t tile[64][66];
+  const int b = blockIdx.z;
+  const int k0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+#pragma unroll 4
+  for (int i = tid; i < 64 * 64; i += 256) {
+    const int kk = i >> 6, cc = i & 63, k = k0 + kk, c = c0 + cc;
     uint16_t v = 0;
     if (c < a.r && k < a.K) {
       const long s = static_cast<long>(k) * a.r + c;
       v = a.src_bf16 ? static_cast<const uint16_t*>(a.src[b])[s] : f32_to_bf16_rne(static_cast<const float*>(a.src[b])[s]);
     }
-    a.tt[static_cast<long>(b) * total + i] = v;
+    tile[kk][cc] = v;
+  }
+  __syncthreads();
+  uint16_t* tt = a.tt + static_cast<long>(b) * a.rpad * a.Kp;
+#pragma unroll 4
+  for (int i = tid; i < 64 * 64; i += 256) {
+    const int cc = i >> 6, kk = i & 63, c = c0 + cc, k = k0 + kk;
+    if (c < a.rpad && k < a.Kp) tt[static_cast<long>(c) * a.Kp + k] = tile[kk][cc];
   }
 }
 
@@ -887,9 +899,8 @@ int project(bool row_mode, int m, int n, int r, int nb, const void* const* G, in
     ta.r = r;
     ta.rpad = rp;
     ta.src_bf16 = thin_bf16 ? 1 : 0;
-    long blocks = ceil_div(static_cast<long>(rp) * Kp, 256);
-    if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(b16_thin_kernel, dim3(static_cast<unsigned>(blocks), nb), dim3(256), 0, st, ta);
+    const dim3 tgrid(static_cast<unsigned>(ceil_div(Kp, 64)), static_cast<unsigned>(ceil_div(rp, 64)), nb);
+    hipLaunchKernelGGL(b16_thin_kernel, tgrid, dim3(256), 0, st, ta);
     int rc = check_launch("b16_thin");
     if (rc != DION_OK) return rc;
   }
