@@ -2019,10 +2019,10 @@ __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_st
 // turns their P columns into NaN (cholesky_ex does not raise; the fix-up's nan_to_num zeroes
 // them, ortho.py:113 / kernels.py:157-204).
 // ============================================================================
-template <int RP>
-__global__ void __launch_bounds__(256) chol_reg_kernel(const float* __restrict__ G_in, float* __restrict__ Fout,
-                                                       int r) {
-  constexpr int NG = 256 / RP, RPT = RP / NG;
+template <int RP, int NT = 256>
+__global__ void __launch_bounds__(NT) chol_reg_kernel(const float* __restrict__ G_in, float* __restrict__ Fout,
+                                                      int r) {
+  constexpr int NG = NT / RP, RPT = RP / NG;
   __shared__ float row[2][RP];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -2061,11 +2061,11 @@ __global__ void __launch_bounds__(256) chol_reg_kernel(const float* __restrict__
       if (i > j) a[q] -= (row[buf][i] * inv) * uc;
     }
   }
-  for (int idx = tid; idx < (RP - jf) * RP; idx += 256) {
+  for (int idx = tid; idx < (RP - jf) * RP; idx += NT) {
     const int i = jf + idx / RP, cc = idx % RP;
     O[i * RP + cc] = (i == cc) ? __builtin_nanf("") : 0.f;
   }
-  for (int j = jf + tid; j < RP; j += 256) O[RP * RP + j] = __builtin_nanf("");
+  for (int j = jf + tid; j < RP; j += NT) O[RP * RP + j] = __builtin_nanf("");
 }
 
 // ============================================================================
@@ -2075,16 +2075,26 @@ __global__ void __launch_bounds__(256) chol_reg_kernel(const float* __restrict__
 //   x_j = (p_j - sum_{k<j} R_kj x_k) * (1 / R_jj)
 // with the subtractions in k order (right-looking: once x_k is final, every later x_j takes
 // its fused term).  R (the factor kernels' padded RT x RT layout plus reciprocal diagonal)
-// is read with uniform loads, so the vector traffic is the row in and out; columns past r
-// are zero and stay zero.  In place (src == dst) is allowed.
+// is read with wave-uniform addresses: from global memory for RT <= 64 (the scalar cache
+// holds it), from a per-block LDS copy for RT = 128 (uniform global loads of the 64 KB factor
+// thrash the scalar cache: 361 us per 16-matrix group); the vector traffic is the row in and out.  Columns past r are zero and
+// stay zero.  In place (src == dst) is allowed.
 // ============================================================================
 template <int RT>
 __global__ void __launch_bounds__(256) trsm_right_kernel(const float* __restrict__ src, float* __restrict__ dst,
                                                          const float* __restrict__ Rf, int mp, int r) {
+  constexpr bool kLds = RT >= 128;  // RT <= 64: the 16 KB factor stays in the scalar cache
+  __shared__ f32x4 Rs4[kLds ? (RT * RT + RT) / 4 : 1];
   const int b = blockIdx.y;
+  const float* R = Rf + static_cast<long>(b) * (RT * RT + RT);
+  if constexpr (kLds) {
+    const f32x4* Rg = reinterpret_cast<const f32x4*>(R);
+    for (int i = threadIdx.x; i < (RT * RT + RT) / 4; i += 256) Rs4[i] = Rg[i];
+    __syncthreads();
+    R = reinterpret_cast<const float*>(Rs4);
+  }
   const long row = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
   if (row >= mp) return;
-  const float* __restrict__ R = Rf + static_cast<long>(b) * (RT * RT + RT);
   const float* p = src + (static_cast<long>(b) * mp + row) * r;
   float x[RT];
   if ((r & 3) == 0) {
@@ -3945,7 +3955,7 @@ int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t s
     switch (trsm_rt(r)) {
       case 32: hipLaunchKernelGGL((chol_reg_kernel<32>), dim3(batch), dim3(256), 0, st, G, Uinv, r); break;
       case 64: hipLaunchKernelGGL((chol_reg_kernel<64>), dim3(batch), dim3(256), 0, st, G, Uinv, r); break;
-      default: hipLaunchKernelGGL((chol_reg_kernel<128>), dim3(batch), dim3(256), 0, st, G, Uinv, r); break;
+      default: hipLaunchKernelGGL((chol_reg_kernel<128, 1024>), dim3(batch), dim3(1024), 0, st, G, Uinv, r); break;
     }
     return check_launch("chol");
   }
