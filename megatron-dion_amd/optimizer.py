@@ -475,7 +475,8 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
             pstate["momentum"] = torch.zeros_like(p, dtype=_as_dtype(getattr(mpc, "momentum_dtype", None)) or p.dtype)
             tp_world = int(dist.get_world_size(tp_group)) if tspec is not None else 1
             tp_rank = int(dist.get_rank(tp_group)) if tspec is not None else 0
-            layout = split_child_layouts(p, plan, fs_spec=spec, tp_spec=tspec, fs_group=fs_group,
+            layout = split_child_layouts(p, plan, fs_spec=spec, tp_spec=tspec, fs_world=fs_world,
+                                         fs_rank=int(dist.get_rank(fs_group)) if fs_world > 1 else 0,
                                          tp_world=tp_world, tp_rank=tp_rank)
             for kind in kinds:
                 lay = layout[kind]

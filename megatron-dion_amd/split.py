@@ -201,8 +201,8 @@ def split_plan(param: torch.Tensor, defaults: dict, global_rows: Optional[int] =
     return None
 
 
-def split_child_layouts(param: torch.Tensor, plan, *, fs_spec=None, tp_spec=None, fs_group=None,
-                        tp_world: int = 1, tp_rank: int = 0) -> dict:
+def split_child_layouts(param: torch.Tensor, plan, *, fs_spec=None, tp_spec=None, fs_world: int = 1,
+                        fs_rank: int = 0, tp_world: int = 1, tp_rank: int = 0) -> dict:
     """Per child kind: this rank's rows of the child and its FS / TP shard specs.
 
     `param` is the whole fused matrix or this rank's shard of it: `fs_spec` / `tp_spec` =
@@ -218,8 +218,6 @@ def split_child_layouts(param: torch.Tensor, plan, *, fs_spec=None, tp_spec=None
 
     Returns {kind: dict(local_rows, segments (local source rows), fs, tp (child specs or
     None), row_sizes (every member's child rows, or None), row_axis ("tp" | "fs" | None))}."""
-    import torch.distributed as dist
-
     family, kinds, _, flags = plan
     split = tuple(flags[f"{family}_split_shapes"] if family != "linear" else flags["linear_split_rows"])
     local_rows = int(param.shape[0])
@@ -234,10 +232,10 @@ def split_child_layouts(param: torch.Tensor, plan, *, fs_spec=None, tp_spec=None
         if (int(tp_spec[2]), int(tp_spec[3])) != ranges[me]:
             raise RuntimeError(f"[DION_{family.upper()}_LOCAL_ROW_RANGE_MISMATCH] local_rows={local_rows} "
                                f"parent_row_range={ranges[me]} tp_spec=({tp_spec[2]}, {tp_spec[3]})")
-    elif fs_spec is not None and int(fs_spec[1]) == 0 and fs_group is not None and dist.get_world_size(fs_group) > 1:
+    elif fs_spec is not None and int(fs_spec[1]) == 0 and fs_world > 1:
         row_axis = "fs"  # the members' canonical FS ranges (compute_fs_shard_range, sharding.py:44-61)
-        ranges = [_split_range(gm, dist.get_world_size(fs_group), k) for k in range(dist.get_world_size(fs_group))]
-        me = dist.get_rank(fs_group)
+        ranges = [_split_range(gm, fs_world, k) for k in range(fs_world)]
+        me = fs_rank
         if (int(fs_spec[2]), int(fs_spec[3])) != ranges[me]:
             raise RuntimeError(f"[DION_{family.upper()}_MISSING_FS_RANGE] fs_spec=({fs_spec[2]}, {fs_spec[3]}) is "
                                f"not the canonical FS range {ranges[me]}")
