@@ -2384,7 +2384,13 @@ __device__ __forceinline__ int kmap(int g, int e) {
 // swizzle of the 32 x 8 (16-byte unit) LDS transpose tile: chunk k of row r is stored at
 // k ^ ((r >> 1) & 7), conflict-free for 16 consecutive lanes on 64 banks (the alternative
 // 5 (r >> 1) & 7 measured twice the bank conflicts, round 2)
-__device__ __forceinline__ int xt_swz(int r) { return (r >> 1) & 7; }
+// slot swizzle of the [rows][8 x 16 B] transpose tiles: row r's slot k sits at k ^ (r & 7).
+// Conflict-free for every access the row kernels make (cdna_hip_programming.md section 2 bank
+// rules): row-wise ds_write_b128 (8 lanes = one row) and ds_read_b128, and lane (t, g) =
+// (row t, slot 4c + g) ds_read_b128 AND ds_write_b128 -- the earlier (r >> 1) & 7 put rows
+// 2i, 2i + 1 of an 8-lane write group on one 16-B slot (2-way, rowproj_efh3_kernel's
+// write-back: 32 extra LDS cycles per wave-step)
+__device__ __forceinline__ int xt_swz(int r) { return r & 7; }
 
 constexpr int kRBE = 2;   // 16-row blocks per wave in the fused row kernel (measured default)
 
