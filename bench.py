@@ -75,7 +75,7 @@ WORKLOADS = {
 # ef_apply is two launches of the same instance (M, then W), each streaming 8 B per element
 KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("project_p", True): ("colproj_fast_kernel<4, 2>", 1),
-             ("project_p_ef", False): ("rowproj_efh3_kernel<4, 2, 2, 2, 4>", 1),
+             ("project_p_ef", False): ("rowproj_efh3_kernel<4, 2, 1, 2, 4>", 1),
              ("project_p_ef", True): ("colproj_efh3_kernel<4, 2>", 1),
              ("ef_apply_w", False): ("rank_stream_kernel<4, false, 8, 2, true>", 1),
              ("ef_apply_w", True): ("rank_stream_kernel<4, false, 8, 2, true>", 1),

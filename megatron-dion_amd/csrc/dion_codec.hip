@@ -615,6 +615,11 @@ __device__ __forceinline__ void rp_compute(RowStep<GDT>& S, f32x4 (&acc)[kRB][RB
 // row blocks of one matrix that read the same thin rows at the same time.
 // waves per block of the fused pass-A row kernel (rowproj_efh3_kernel; 8 measured slower)
 constexpr int kPaNW = 4;
+// r <= 64 pass-A row kernel: no register prefetch ring (PD 1) and 3 blocks per CU (166
+// VGPRs, 3 waves per SIMD, 144 KB LDS) -- the PD-2 ring needs 228 VGPRs (2 waves per SIMD;
+// at 3 it spills 113).  Measured on the Llama set: kernel 5307 vs 5165 GB/s (3-round A/B)
+constexpr int kPaPD = 1;
+constexpr int kPaMinb = 3;
 
 constexpr int kXcdRemap = 1;
 struct BlockXYZ {
@@ -2871,7 +2876,7 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colpr
 // (t, g = 0..3)), Q the A operand: each step lands in a fresh accumulator
 // D[16 cb + 4 g + q][row t] and is added as acc += D / s_row.
 template <int RB, int GDT, int PD, int KR = kRBE, int NW = kPaNW>
-__global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : 8 / NW) rowproj_efh3_kernel(const EfProjArgs e) {
+__global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : (RB >= 8 ? 8 / NW : kPaMinb)) rowproj_efh3_kernel(const EfProjArgs e) {
   constexpr int R = 16 * RB;
   constexpr int KK = RB / 2;
   constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;  // f16x8 units of one K-step's splits
@@ -4342,7 +4347,7 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
         if (tr)
           hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
         else  // r = 128: one-step pipeline (register budget)
-          hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, RB >= 8 ? kPD8 : 2, RB >= 8 ? kKR8 : kRBE, RB >= 8 ? kNW8 : kPaNW>),
+          hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, RB >= 8 ? kPD8 : kPaPD, RB >= 8 ? kKR8 : kRBE, RB >= 8 ? kNW8 : kPaNW>),
                              grid, dim3(64 * (RB >= 8 ? kNW8 : kPaNW)), 0, st, e);
         return check_launch(tr ? "colproj_ef" : "rowproj_ef");
       });
