@@ -2707,6 +2707,15 @@ constexpr int kNW8 = 4;
 constexpr int kPD8 = 1;
 // blocks per CU the r = 128 transposed fused pass A is compiled for
 constexpr int kCpeh3Minb8 = 1;
+// transposed pass-A kernel (colproj_efh3_kernel): 0 = no register ring, the step's M/G
+// loads issued right before use and the CU's other blocks covering their latency (r <= 64:
+// 162 VGPRs, 3 blocks per CU; r = 128: 252 VGPRs, 2 waves per SIMD); 1 = the two-step SA/SB
+// ring (r <= 64: 234 VGPRs, 2 per SIMD, spills at 3; r = 128: 256 VGPRs + 103 AGPRs, 1)
+constexpr int kCpeRing = 1;
+// transposed pass-B row kernel (rowproj_h3_kernel): the same choice (ring-free r <= 64: 114
+// VGPRs, 4 waves per SIMD; r = 128: 153, 3 per SIMD.  Ring: 188 (2 per SIMD) and 256 with
+// 10 spilled)
+constexpr int kPbrRing = 1;
 // blocks per CU the r <= 64 pass-B row kernel is compiled for
 constexpr int kPbrMinb = 2;
 // r > 64 pass-B h3 kernels: the split P two cb at a time, two waves per SIMD
@@ -3097,7 +3106,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : (RB >= 8 ? 8 / NW : kPa
 // four lanes (t, g = 0..3)), Q the A operand: D[16 cb + 4 g + q][col 2t + c] is added as
 // acc += D / s_col.  The matrix's max |M| goes into the flag for a fixed-scale pass B.
 template <int RB, int GDT>
-__global__ void __launch_bounds__(256, RB >= 8 ? kCpeh3Minb8 : 2) colproj_efh3_kernel(const EfProjArgs e) {
+__global__ void __launch_bounds__(256, kCpeRing ? (RB >= 8 ? kCpeh3Minb8 : 2) : (RB >= 8 ? 2 : 3)) colproj_efh3_kernel(const EfProjArgs e) {
   constexpr int R = 16 * RB;
   constexpr int KK = RB / 2;
   constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;  // f16x8 units of one K-step's splits
@@ -3217,6 +3226,35 @@ __global__ void __launch_bounds__(256, RB >= 8 ? kCpeh3Minb8 : 2) colproj_efh3_k
 
   const u32x4* qs = e.qsplit + b * e.split_stride;
   const u32x4* rsp = e.rsplit + b * e.split_stride;
+  if constexpr (!kCpeRing) {
+    // no register ring: the step's M/G load is issued right before its use, the other
+    // blocks of the CU (3 per CU at this register count) cover its latency
+    ColStepE<GDT> S;
+    SplitCopy<NQ> TA;
+    SplitCopy<NR> EA;
+    split_copy_load<NQ>(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
+    split_copy_store<NQ>(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
+    if (has_ef) {
+      split_copy_load<NR>(EA, rsp + static_cast<long>(i_begin / 32) * NR, tid);
+      split_copy_store<NR>(EA, reinterpret_cast<bf16x8*>(rs[0]), tid);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int i0 = i_begin; i0 < i_end; i0 += 32) {
+      const bool more = i0 + 32 < i_end;
+      cpe_load<GDT>(S, M, G, a.ld_m, a.ld_g, i0);
+      if (more) {
+        split_copy_load<NQ>(TA, qs + static_cast<long>(i0 / 32 + 1) * NQ, tid);
+        if (has_ef) split_copy_load<NR>(EA, rsp + static_cast<long>(i0 / 32 + 1) * NR, tid);
+      }
+      compute(S, tq[cur], rs[cur], i0);
+      if (!more) break;
+      split_copy_store<NQ>(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+      if (has_ef) split_copy_store<NR>(EA, reinterpret_cast<bf16x8*>(rs[cur ^ 1]), tid);
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
   ColStepE<GDT> SA, SB;
   SplitCopy<NQ> TA;
   SplitCopy<NR> EA;
@@ -3257,6 +3295,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? kCpeh3Minb8 : 2) colproj_efh3_k
     __syncthreads();
     cur ^= 1;
   }
+  }
 
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
 #pragma unroll
@@ -3280,7 +3319,7 @@ __global__ void __launch_bounds__(256, RB >= 8 ? kCpeh3Minb8 : 2) colproj_efh3_k
 // (one scale per matrix); with pass A's max |M| the step's products accumulate in place
 // under one scale for the matrix, else each row gets a per-step scale (as in pass A).
 template <int RB, int NW>
-__global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ? 1 : (RB <= 4 ? kPbrMinb : 2))
+__global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ? 1 : (kPbrRing ? (RB <= 4 ? kPbrMinb : 2) : 3))
     rowproj_h3_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int NQ = RB * 2 * 64;
@@ -3413,6 +3452,24 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ?
         }
       }
     };
+    if constexpr (!kPbrRing) {
+      split_copy_load_n(TA, qs + static_cast<long>(cj(j_begin) / 32) * NQ, tid);
+      split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
+      __syncthreads();
+      int cur = 0;
+      for (int j0 = j_begin; j0 < j_end; j0 += 32) {
+        const bool more = j0 + 32 < j_end;
+        xload(SA, cj(j0));
+        if (more) split_copy_load_n(TA, qs + static_cast<long>(cj(j0 + 32) / 32) * NQ, tid);
+        xpose(SA);
+        compute(SA, tq[cur]);
+        if (!more) break;
+        split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+        __syncthreads();
+        cur ^= 1;
+      }
+      return;
+    }
     xload(SA, cj(j_begin));
     split_copy_load_n(TA, qs + static_cast<long>(cj(j_begin) / 32) * NQ, tid);
     split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
