@@ -2706,16 +2706,17 @@ constexpr int kKR8 = 2;
 constexpr int kNW8 = 4;
 constexpr int kPD8 = 1;
 // blocks per CU the r = 128 transposed fused pass A is compiled for
-constexpr int kCpeh3Minb8 = 1;
-// transposed pass-A kernel (colproj_efh3_kernel): 0 = no register ring, the step's M/G
-// loads issued right before use and the CU's other blocks covering their latency (r <= 64:
-// 162 VGPRs, 3 blocks per CU; r = 128: 252 VGPRs, 2 waves per SIMD); 1 = the two-step SA/SB
-// ring (r <= 64: 234 VGPRs, 2 per SIMD, spills at 3; r = 128: 256 VGPRs + 103 AGPRs, 1)
+// transposed pass-A kernel (colproj_efh3_kernel) at r <= 64: 1 = the two-step SA/SB register
+// ring (234 VGPRs, 2 waves per SIMD; it spills at 3), 0 = no ring, the step's M/G loads
+// issued right before use and the CU's other blocks covering their latency (162 VGPRs, 3
+// blocks per CU).  Measured (Llama set, 3-round A/B): ring 5459 vs 5313 GB/s.  r = 128 always
+// runs ring-free: 252 VGPRs at 2 waves per SIMD against the ring's 256 + 103 AGPRs at 1,
+// 3098 -> 3888 GB/s (Mixtral set)
 constexpr int kCpeRing = 1;
-// transposed pass-B row kernel (rowproj_h3_kernel): the same choice (ring-free r <= 64: 114
-// VGPRs, 4 waves per SIMD; r = 128: 153, 3 per SIMD.  Ring: 188 (2 per SIMD) and 256 with
-// 10 spilled)
-constexpr int kPbrRing = 1;
+// transposed pass-B row kernel (rowproj_h3_kernel): ring-free (r <= 64: 114 VGPRs, 4 waves per
+// SIMD; r = 128: 153, 3) -- the ring needs 188 (2 per SIMD) and 256 with 10 spilled.
+// Measured: Llama 4593 -> 4831 GB/s, Mixtral 3730 -> 3954 GB/s
+constexpr int kPbrRing = 0;
 // blocks per CU the r <= 64 pass-B row kernel is compiled for
 constexpr int kPbrMinb = 2;
 // r > 64 pass-B h3 kernels: the split P two cb at a time, two waves per SIMD
@@ -3106,7 +3107,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : (RB >= 8 ? 8 / NW : kPa
 // four lanes (t, g = 0..3)), Q the A operand: D[16 cb + 4 g + q][col 2t + c] is added as
 // acc += D / s_col.  The matrix's max |M| goes into the flag for a fixed-scale pass B.
 template <int RB, int GDT>
-__global__ void __launch_bounds__(256, kCpeRing ? (RB >= 8 ? kCpeh3Minb8 : 2) : (RB >= 8 ? 2 : 3)) colproj_efh3_kernel(const EfProjArgs e) {
+__global__ void __launch_bounds__(256, (RB >= 8 || kCpeRing) ? 2 : 3) colproj_efh3_kernel(const EfProjArgs e) {
   constexpr int R = 16 * RB;
   constexpr int KK = RB / 2;
   constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;  // f16x8 units of one K-step's splits
@@ -3226,7 +3227,7 @@ __global__ void __launch_bounds__(256, kCpeRing ? (RB >= 8 ? kCpeh3Minb8 : 2) : 
 
   const u32x4* qs = e.qsplit + b * e.split_stride;
   const u32x4* rsp = e.rsplit + b * e.split_stride;
-  if constexpr (!kCpeRing) {
+  if constexpr (RB >= 8 || !kCpeRing) {
     // no register ring: the step's M/G load is issued right before its use, the other
     // blocks of the CU (3 per CU at this register count) cover its latency
     ColStepE<GDT> S;
@@ -3615,6 +3616,10 @@ bool colproj_fast_ok(int rows, int cols, int r) { return cols % 256 == 0 && rows
 constexpr int kRankStreamLen = 512;
 constexpr int kRankNW = 8;
 constexpr int kRankD = 2;
+// r = 128 (RU 8): one X tile in flight -- 135 VGPRs, 3 waves per SIMD, against D 2's 202 at 2.
+// Measured on the Mixtral set 5050 -> 5332 GB/s; at r = 64 D 1 (102 VGPRs, 4 per SIMD) is
+// slower, 5970 -> 5716
+constexpr int kRankD8 = 1;
 
 // pre-split thin operand of the x6 projections (rows = the contraction index)
 size_t thin_presplit_bytes(int rows, int r, int batch) { return static_cast<size_t>(rows) * r * 6 * batch + 1024; }
@@ -4866,7 +4871,7 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
               else
                 hipLaunchKernelGGL((rank_stream_kernel<RUv, false, NWv, Dv>), g2, dim3(64 * NWv), 0, st, ra);
             };
-            go(std::integral_constant<int, kRankNW>{}, std::integral_constant<int, kRankD>{});
+            go(std::integral_constant<int, kRankNW>{}, std::integral_constant<int, (RUv >= 8 ? kRankD8 : kRankD)>{});
           }
         };
         switch (r / 16) {
