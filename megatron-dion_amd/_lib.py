@@ -8,10 +8,30 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# DION_LIB_PATH: load another build of the same ABI (kernel-variant A/B runs during tuning)
-LIB_PATH = os.environ.get("DION_LIB_PATH") or os.path.join(HERE, "csrc", "libdion_codec.so")
+DEFAULT_LIB_PATH = os.path.join(HERE, "csrc", "libdion_codec.so")
+
+
+def _lib_path() -> str:
+    """The in-tree library, unless a kernel-variant A/B run names another build of the same ABI.
+
+    A variant needs BOTH `DION_LIB_PATH` and `DION_DEV_ALLOW_LIB_PATH=1` (a dev-only switch
+    that no product path, test, smoke() or bench.py sets), and its use is announced on
+    stderr: an environment variable alone can never swap the product's kernels silently."""
+    alt = os.environ.get("DION_LIB_PATH")
+    if not alt:
+        return DEFAULT_LIB_PATH
+    if os.environ.get("DION_DEV_ALLOW_LIB_PATH") != "1":
+        raise RuntimeError(f"[DION_LIB_PATH_NOT_ALLOWED] DION_LIB_PATH={alt!r} is a dev-only override; "
+                           "set DION_DEV_ALLOW_LIB_PATH=1 to load a variant build, or unset DION_LIB_PATH")
+    print(f"[dion] WARNING: loading codec variant {alt} (DION_LIB_PATH), not {DEFAULT_LIB_PATH}",
+          file=sys.stderr, flush=True)
+    return alt
+
+
+LIB_PATH = _lib_path()
 ABI_VERSION = 12
 
 DION_OK = 0

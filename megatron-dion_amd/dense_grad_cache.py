@@ -15,6 +15,13 @@ The record lives on the optimizer (attribute `_dion_dense_grad_reduction_cache`)
 Lookups answer "match" (a mark for this region, step, group and op), "mismatch" (a mark
 that covers the region but for another group / op: an error, the gradient was reduced
 differently) or "missing".  Stale marks (another step) are dropped on lookup.
+
+A mark says nothing about the bytes: if the step is skipped after the norm (an AMP loss
+scaler finding an inf) and the next iteration's gradients land in the same storage, a mark
+keyed on (storage, region, step) would still "match" and the new gradients would never be
+exchanged.  `invalidate` drops every mark; `MegatronDion.zero_grad()` calls it, and a
+caller that skips a step without zeroing through the optimizer calls it itself.  (Megatron's
+own loop cannot hit this: it checks for infs before the norm and returns without one.)
 """
 from __future__ import annotations
 
@@ -113,6 +120,12 @@ def consume_if_reduced(owner, grads: Sequence[torch.Tensor], *, group, op) -> bo
     if not cache["entries"]:
         delattr(owner, CACHE_ATTR)
     return True
+
+
+def invalidate(owner) -> None:
+    """Forget every reduction mark (gradients repopulated or a step skipped after the norm)."""
+    if getattr(owner, CACHE_ATTR, None) is not None:
+        delattr(owner, CACHE_ATTR)
 
 
 def can_reuse_dense_grad(dist_meta) -> bool:

@@ -116,6 +116,14 @@ class MegatronDion(Optimizer):
         does so itself."""
         return flush_pending_error_feedback(self, lambda: self.codec)
 
+    def zero_grad(self, set_to_none: bool = True):
+        """torch's zero_grad, plus: the gradients about to be repopulated invalidate the
+        grad norm's dense-reduction marks (dense_grad_cache.invalidate), so a norm computed
+        before a skipped step can never vouch for the next iteration's gradients."""
+        from .dense_grad_cache import invalidate
+        invalidate(self)
+        return super().zero_grad(set_to_none=set_to_none)
+
     def state_dict(self):
         self.flush_error_feedback()
         return super().state_dict()

@@ -1,4 +1,5 @@
 # A/B of codec kernel variants on Llama-size batches: bash scripts/dev/ab_kernels.sh variant1 [variant2 ...]
+export DION_DEV_ALLOW_LIB_PATH=1
 # ("default" = the in-tree library); ops: pa_ef pa_ef_T pb pb_T w w_T
 set -o pipefail
 mkdir -p gpurun_out

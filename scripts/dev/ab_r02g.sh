@@ -1,4 +1,5 @@
 # bf16 state mode: the update on b16_stream_kernel vs b16_update_kernel (b16old): GPU bf16
+export DION_DEV_ALLOW_LIB_PATH=1
 # tests, then the bf16-state bench line with each library
 set -o pipefail
 mkdir -p gpurun_out

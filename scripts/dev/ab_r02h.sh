@@ -1,4 +1,5 @@
 # r = 128 fused pass A row kernel with 16-row waves and a prefetch stage (kr1) vs 32-row
+export DION_DEV_ALLOW_LIB_PATH=1
 # waves without (default): parity (full-size Mixtral shapes and the r = 128 seeded cases
 # through kr1), kbench, Mixtral bench lines with each, stream counts
 set -o pipefail

@@ -1,4 +1,5 @@
 # one call: r = 128 16-row pass A (kr1 variant) parity + A/B; then the default build's GPU
+export DION_DEV_ALLOW_LIB_PATH=1
 # suite, smoke, bench line and the round's committed profiles (rocprof stats, PMC traffic,
 # SQ counters)
 set -o pipefail

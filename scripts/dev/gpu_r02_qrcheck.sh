@@ -1,4 +1,5 @@
 # the bf16 three-step test with the batched-reduction sketch QR (default) and the previous
+export DION_DEV_ALLOW_LIB_PATH=1
 # library (qrold), twice each
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,4 +1,5 @@
 # dev: accuracy (vs fp64) and speed of pass-B variants
+export DION_DEV_ALLOW_LIB_PATH=1
 set -o pipefail
 mkdir -p gpurun_out
 for v in ${VARIANTS:-default pbh3}; do

@@ -1,4 +1,5 @@
 # HBM bytes per kernel of one kbench op: bash scripts/dev/pmc_traffic_op.sh <op> [lib variant]
+export DION_DEV_ALLOW_LIB_PATH=1
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,4 +1,5 @@
 # dev: SQ counter groups of one kbench op for a library variant: VARIANT=name OPS="pb pb_T" bash scripts/dev/pmc_variant.sh
+export DION_DEV_ALLOW_LIB_PATH=1
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,4 +1,5 @@
 set -o pipefail
+export DION_DEV_ALLOW_LIB_PATH=1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 120 python scripts/dev/diag_h3t2.py > gpurun_out/diag_h3t.log 2>&1 && \

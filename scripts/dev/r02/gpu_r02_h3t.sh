@@ -1,4 +1,5 @@
 # one GPU box call: the transposed-h3 change -- the parity tests that touch it, the gpu
+export DION_DEV_ALLOW_LIB_PATH=1
 # suite, then the Llama bench A/B against the bf16x6 transposed kernels (variant x6t)
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,4 +1,5 @@
 # dev: same-box A/B of two codec builds on the Llama bench (default lib vs $AB_LIB)
+export DION_DEV_ALLOW_LIB_PATH=1
 mkdir -p gpurun_out
 for i in 1 2; do
   for lib in default "$AB_LIB"; do

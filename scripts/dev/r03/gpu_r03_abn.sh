@@ -1,4 +1,5 @@
 # same-box A/B of the default library against the variant libraries named in $LIBS (Llama bench)
+export DION_DEV_ALLOW_LIB_PATH=1
 set -o pipefail
 mkdir -p gpurun_out
 for i in 1 2; do

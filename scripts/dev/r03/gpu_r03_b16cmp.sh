@@ -1,4 +1,5 @@
 # bf16-state: GPU tests of the bf16 mode, then per-kernel bench comparison new lib vs HEAD lib
+export DION_DEV_ALLOW_LIB_PATH=1
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

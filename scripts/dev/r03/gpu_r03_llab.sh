@@ -1,4 +1,5 @@
 # bench A/B, alternating new / $OLD_LIB, three rounds (BENCH_ARGS picks the workload)
+export DION_DEV_ALLOW_LIB_PATH=1
 set -o pipefail
 mkdir -p gpurun_out
 for i in 1 2 3; do

@@ -1,4 +1,5 @@
 # r = 128 (Mixtral experts): r = 128 GPU parity tests, then Mixtral bench A/B (new lib vs $OLD_LIB)
+export DION_DEV_ALLOW_LIB_PATH=1
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,4 +1,5 @@
 # dev: ortho kernel variants (build/libdion_*.so) under rocprofv3 --stats
+export DION_DEV_ALLOW_LIB_PATH=1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for v in inv0 inv1 inv2 fact0; do

@@ -1,4 +1,5 @@
 # ortho chain (trsm factor in LDS, 1024-thread r = 128 Cholesky): parity tests, Mixtral + Llama A/B vs $OLD_LIB
+export DION_DEV_ALLOW_LIB_PATH=1
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,4 +1,5 @@
 # parity of the ring-free + rank-depth-1 build, then bench A/B of the in-tree build against
+export DION_DEV_ALLOW_LIB_PATH=1
 # the two variants on the Llama and Mixtral sets
 set -o pipefail
 mkdir -p gpurun_out

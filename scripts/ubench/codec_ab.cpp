@@ -1,0 +1,287 @@
+// Dev tool (not product): A/B of codec library builds on the Llama-3-8B launch groups, through the
+// C ABI, without torch.  Each library is dlopen'ed; for every (op, shape) the libraries run on
+// identical inputs once for a result check against the first library, then round-robin timing.
+//   build: hipcc -O3 --offload-arch=gfx950 -I include -o scripts/ubench/codec_ab scripts/ubench/codec_ab.cpp -ldl
+//   run:   scripts/ubench/codec_ab "pa,pb,upd" "o,qkv,fc1,fc2" lib1.so [lib2.so ...]
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "dion_codec.h"
+
+#define CK(x)                                                                          \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(2);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+struct Lib {
+  std::string path;
+  void* h;
+  decltype(&dion_workspace_bytes) ws;
+  decltype(&dion_project_p_ef) pa;
+  decltype(&dion_project_r) pb;
+  decltype(&dion_ef_apply) upd;
+  decltype(&dion_last_error) err;
+};
+
+static Lib open_lib(const char* p) {
+  Lib L;
+  L.path = p;
+  L.h = dlopen(p, RTLD_NOW | RTLD_LOCAL);
+  if (!L.h) {
+    fprintf(stderr, "dlopen %s: %s\n", p, dlerror());
+    exit(2);
+  }
+  L.ws = (decltype(L.ws))dlsym(L.h, "dion_workspace_bytes");
+  L.pa = (decltype(L.pa))dlsym(L.h, "dion_project_p_ef");
+  L.pb = (decltype(L.pb))dlsym(L.h, "dion_project_r");
+  L.upd = (decltype(L.upd))dlsym(L.h, "dion_ef_apply");
+  L.err = (decltype(L.err))dlsym(L.h, "dion_last_error");
+  return L;
+}
+
+__global__ void fill_f32(float* x, long n, uint32_t seed, float scale) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    h *= 3266489917u;
+    h ^= h >> 16;
+    x[i] = ((float)(h & 0xFFFFFF) / 16777216.f - 0.5f) * scale;
+  }
+}
+__global__ void fill_bf16(uint16_t* x, long n, uint32_t seed, float scale) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    h *= 3266489917u;
+    h ^= h >> 16;
+    float v = ((float)(h & 0xFFFFFF) / 16777216.f - 0.5f) * scale;
+    x[i] = (uint16_t)(__float_as_uint(v) >> 16);
+  }
+}
+// max |a - b| and max |b| (as uint bits of non-negative floats), one atomic per block
+__global__ void diff_max(const float* a, const float* b, long n, uint32_t* out) {
+  uint32_t d = 0, m = 0;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float x = a[i], y = b[i];
+    float dd = fabsf(x - y);
+    if (!(dd == dd)) dd = INFINITY;
+    d = max(d, __float_as_uint(dd));
+    m = max(m, __float_as_uint(fabsf(y)));
+  }
+  atomicMax(out, d);
+  atomicMax(out + 1, m);
+}
+
+static void fill(float* x, long n, uint32_t seed, float scale) {
+  hipLaunchKernelGGL(fill_f32, dim3(2048), dim3(256), 0, 0, x, n, seed, scale);
+}
+static void fillb(uint16_t* x, long n, uint32_t seed, float scale) {
+  hipLaunchKernelGGL(fill_bf16, dim3(2048), dim3(256), 0, 0, x, n, seed, scale);
+}
+static double rel_diff(const float* a, const float* b, long n) {
+  uint32_t* o;
+  CK(hipMalloc(&o, 8));
+  CK(hipMemset(o, 0, 8));
+  hipLaunchKernelGGL(diff_max, dim3(1024), dim3(256), 0, 0, a, b, n, o);
+  uint32_t h[2];
+  CK(hipMemcpy(h, o, 8, hipMemcpyDeviceToHost));
+  CK(hipFree(o));
+  float d, m;
+  memcpy(&d, &h[0], 4);
+  memcpy(&m, &h[1], 4);
+  return m > 0 ? d / m : d;
+}
+
+struct Shape {
+  const char* name;
+  int m, n;
+  bool tr;
+};
+
+int main(int argc, char** argv) {
+  if (argc < 4) {
+    fprintf(stderr, "usage: %s ops shapes lib.so [lib.so ...]\n", argv[0]);
+    return 2;
+  }
+  const std::string ops = argv[1], shapes_s = argv[2];
+  std::vector<Lib> libs;
+  for (int i = 3; i < argc; ++i) libs.push_back(open_lib(argv[i]));
+  const int reps = getenv("AB_REPS") ? atoi(getenv("AB_REPS")) : 5;
+  const int rounds = getenv("AB_ROUNDS") ? atoi(getenv("AB_ROUNDS")) : 3;
+  const int r = getenv("AB_R") ? atoi(getenv("AB_R")) : 64;
+  const int B = 16;
+  const Shape all[] = {{"o", 4096, 4096, false}, {"qkv", 6144, 4096, false}, {"fc1", 28672, 4096, false},
+                       {"fc2", 4096, 14336, true}, {"exp", 14336, 4096, false}, {"expT", 4096, 14336, true}};
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (const Shape& sh : all) {
+    if (("," + shapes_s + ",").find(std::string(",") + sh.name + ",") == std::string::npos) continue;
+    const long mn = (long)sh.m * sh.n;
+    const int mp = sh.tr ? sh.n : sh.m, nq = sh.tr ? sh.m : sh.n;
+    float *M, *Mref, *W, *Q, *P, *Pe, *Re, *R, *Pout, *Pout0, *Rout0, *Qn;
+    uint16_t* G;
+    uint32_t* nz;
+    CK(hipMalloc(&M, mn * 4 * B));
+    CK(hipMalloc(&Mref, mn * 4 * B));
+    CK(hipMalloc(&W, mn * 4 * B));
+    CK(hipMalloc(&G, mn * 2 * B));
+    CK(hipMalloc(&Q, (long)nq * r * 4 * B));
+    CK(hipMalloc(&Qn, (long)nq * r * 4 * B));
+    CK(hipMalloc(&P, (long)mp * r * 4 * B));
+    CK(hipMalloc(&Pout, (long)mp * r * 4 * B));
+    CK(hipMalloc(&Pout0, (long)mp * r * 4 * B));
+    CK(hipMalloc(&Pe, (long)mp * r * 4 * B));
+    CK(hipMalloc(&Re, (long)nq * r * 4 * B));
+    CK(hipMalloc(&R, (long)nq * r * 4 * B));
+    CK(hipMalloc(&Rout0, (long)nq * r * 4 * B));
+    CK(hipMalloc(&nz, 4 * B));
+    fillb(G, mn * B, 11, 2e-3f);
+    fill(W, mn * B, 12, 0.04f);
+    fill(Q, (long)nq * r * B, 13, 1.f);
+    fill(Qn, (long)nq * r * B, 14, 0.02f);
+    fill(P, (long)mp * r * B, 15, 0.01f);
+    fill(Pe, (long)mp * r * B, 16, 0.01f);
+    fill(Re, (long)nq * r * B, 17, 0.01f);
+    CK(hipDeviceSynchronize());
+    std::vector<float*> Mv(B), Wv(B), Qv(B), Qnv(B), Pev(B), Rev(B);
+    std::vector<const void*> Gv(B);
+    for (int b = 0; b < B; ++b) {
+      Mv[b] = M + mn * b;
+      Wv[b] = W + mn * b;
+      Gv[b] = G + mn * b;
+      Qv[b] = Q + (long)nq * r * b;
+      Qnv[b] = Qn + (long)nq * r * b;
+      Pev[b] = Pe + (long)mp * r * b;
+      Rev[b] = Re + (long)nq * r * b;
+    }
+    DionBatchDesc d;
+    memset(&d, 0, sizeof(d));
+    d.batch = B;
+    d.m = sh.m;
+    d.n = sh.n;
+    d.r = r;
+    d.transposed = sh.tr;
+    d.g_dtype = DION_DTYPE_BF16;
+    d.m_dtype = DION_DTYPE_F32;
+    d.w_dtype = DION_DTYPE_F32;
+    DionPendingEF ef;
+    ef.P = Pev.data();
+    ef.R = Rev.data();
+    ef.alpha = -0.05f;
+    size_t wsb = 0;
+    for (auto& L : libs)
+      for (int op : {DION_OP_PROJECT_P_EF, DION_OP_PROJECT_R, DION_OP_EF_APPLY}) {
+        size_t x = 0;
+        if (L.ws(&d, op, &x) == DION_OK && x > wsb) wsb = x;
+      }
+    void* ws;
+    CK(hipMalloc(&ws, wsb + 256));
+    struct OpDef {
+      const char* name;
+      double bytes_per_elem;
+    };
+    for (const char* opn : {"pa", "pb", "upd"}) {
+      if (("," + ops + ",").find(std::string(",") + opn + ",") == std::string::npos) continue;
+      const std::string op = opn;
+      auto reset_inputs = [&] {
+        fill(M, mn * B, 10, 2e-3f);
+        CK(hipMemset(nz, 0, 4 * B));
+        CK(hipDeviceSynchronize());
+      };
+      auto call = [&](Lib& L) -> int {
+        if (op == "pa") {
+          return L.pa(&d, Gv.data(), Mv.data(), (const float* const*)Qv.data(), Pout, nz, &ef, ws, wsb, st);
+        } else if (op == "pb") {
+          return L.pb(&d, (const float* const*)Mv.data(), P, R, nz, ws, wsb, st);
+        } else {
+          return L.upd(&d, nullptr, Wv.data(), P, R, (const float* const*)Qnv.data(), nz, 0.95, 0.01, 0.01, 0.5, ws,
+                       wsb, st);
+        }
+      };
+      const double bpe = op == "pa" ? 10.0 : op == "pb" ? 4.0 : 8.0;
+      // result check: every library on the same inputs, compared with the first
+      for (size_t li = 0; li < libs.size(); ++li) {
+        reset_inputs();
+        if (op == "pb") {
+          // pass B's flags: max |M| bits from a pass A of library 0 is overkill; use inf (per-step scales)
+          // unless AB_PB_FIXED: then the true max of the filled M (|M| <= 1e-3)
+          uint32_t fl[16];
+          float mx = 1e-3f;
+          for (int b = 0; b < B; ++b) memcpy(&fl[b], &mx, 4);
+          if (!getenv("AB_PB_FIXED"))
+            for (int b = 0; b < B; ++b) fl[b] = 0x7F800000u;
+          CK(hipMemcpy(nz, fl, 4 * B, hipMemcpyHostToDevice));
+        }
+        if (op == "upd") {
+          uint32_t fl[16];
+          for (int b = 0; b < B; ++b) fl[b] = 1;
+          CK(hipMemcpy(nz, fl, 4 * B, hipMemcpyHostToDevice));
+          fill(W, mn * B, 12, 0.04f);
+          CK(hipDeviceSynchronize());
+        }
+        int rc = call(libs[li]);
+        CK(hipStreamSynchronize(st));
+        if (rc != DION_OK) {
+          printf("%s %s %s: rc=%d %s\n", op.c_str(), sh.name, libs[li].path.c_str(), rc, libs[li].err());
+          continue;
+        }
+        float* out = op == "pa" ? Pout : op == "pb" ? R : W;
+        const long n_out = op == "pa" ? (long)mp * r * B : op == "pb" ? (long)nq * r * B : mn * B;
+        if (li == 0) {
+          CK(hipMemcpy(op == "upd" ? Mref : (op == "pa" ? Pout0 : Rout0), out, n_out * 4, hipMemcpyDeviceToDevice));
+          if (op == "pa") CK(hipMemcpy(Mref, M, mn * 4 * B, hipMemcpyDeviceToDevice));
+        } else {
+          const float* ref = op == "upd" ? Mref : (op == "pa" ? Pout0 : Rout0);
+          double e = rel_diff(out, ref, n_out);
+          double em = op == "pa" ? rel_diff(M, Mref, mn * B) : 0.0;
+          printf("check %-4s %-5s %s: out maxrel %.3g%s", op.c_str(), sh.name, libs[li].path.c_str(), e,
+                 op == "pa" ? "" : "\n");
+          if (op == "pa") printf("  M maxrel %.3g\n", em);
+        }
+      }
+      // timing: round robin
+      std::vector<double> best(libs.size(), 1e30), sum(libs.size(), 0);
+      for (int rd = 0; rd < rounds; ++rd)
+        for (size_t li = 0; li < libs.size(); ++li) {
+          call(libs[li]);
+          CK(hipStreamSynchronize(st));
+          CK(hipEventRecord(e0, st));
+          for (int i = 0; i < reps; ++i) call(libs[li]);
+          CK(hipEventRecord(e1, st));
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          ms /= reps;
+          best[li] = std::min(best[li], (double)ms);
+          sum[li] += ms;
+        }
+      for (size_t li = 0; li < libs.size(); ++li)
+        printf("time %-4s %-5s %8.3f ms (best %8.3f)  %6.3f TB/s  %s\n", op.c_str(), sh.name, sum[li] / rounds,
+               best[li], bpe * mn * B / (sum[li] / rounds) / 1e9, libs[li].path.c_str());
+      fflush(stdout);
+    }
+    CK(hipFree(ws));
+    for (void* p : {(void*)M, (void*)Mref, (void*)W, (void*)G, (void*)Q, (void*)Qn, (void*)P, (void*)Pout, (void*)Pout0,
+                    (void*)Pe, (void*)Re, (void*)R, (void*)Rout0, (void*)nz})
+      CK(hipFree(p));
+  }
+  return 0;
+}

@@ -163,3 +163,50 @@ def test_w2_clip_then_step_exchanges_each_dense_gradient_once():
             for n, _, _ in SHAPES:
                 for key in ("W", "M"):
                     assert torch.equal(res[r][f"1_s{s}_{n}_{key}"], res[r][f"0_s{s}_{n}_{key}"]), (r, s, n, key)
+
+
+def _skip_worker(rank, world, port, out_dir):
+    """norm on persistent gradient buffers, the step skipped (an AMP-style inf), the
+    next iteration's gradients written into the SAME buffers after zero_grad(), then norm + step.
+    The second norm must exchange the new gradients (not trust the first norm's marks)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    import megatron_dion_amd.grad_norm as gn
+    from tests._cpu_codec import OracleCodec
+
+    opt, params = _make(OracleCodec(sketch_lookup=lambda P: _sketch(P, 0)), dist.group.WORLD)
+    plist = list(params.values())
+    for n, g in _grads(rank, 0).items():
+        params[n].grad = g.clone()  # persistent buffers from here on
+    flags = gn.dense_reuse_flags(opt, plist)
+    out = {"norm0": gn.dion_grad_norm_sq(opt, [p.grad for p in plist], replica_group=dist.group.WORLD,
+                                         dense_reuse=flags)}
+    # the step is skipped; the next iteration zeroes and refills the same storage
+    opt.zero_grad(set_to_none=False)
+    for n, g in _grads(rank, 1).items():
+        params[n].grad.add_(g)
+    out["norm1"] = gn.dion_grad_norm_sq(opt, [p.grad for p in plist], replica_group=dist.group.WORLD,
+                                        dense_reuse=flags)
+    opt.step()
+    for n, p in params.items():
+        out[f"{n}_W"] = p.detach().clone()
+        out[f"{n}_G"] = p.grad.detach().clone()
+    torch.save(out, os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_w2_skipped_step_then_refilled_buffers_are_exchanged_again():
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_skip_worker, args=(2, _free_port(), tmp), nprocs=2, join=True, start_method="spawn")
+        res = [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+    g0, g1 = _grads(0, 1), _grads(1, 1)
+    ref = sum(((g0[n].double() + g1[n].double()) / 2).square().sum().item() for n in g0)
+    for r in range(2):
+        assert res[r]["norm1"].item() == pytest.approx(ref, rel=1e-6), r
+        for n, _, _ in SHAPES:
+            # the gradients the step consumed are the replica average, identical on both ranks
+            avg = (g0[n] + g1[n]) / 2
+            assert torch.allclose(res[r][f"{n}_G"], avg, rtol=0, atol=1e-9), (r, n)
+            assert torch.equal(res[0][f"{n}_W"], res[1][f"{n}_W"]), n
