@@ -355,13 +355,48 @@ class MegatronDion(Optimizer):
         if not self.is_distributed_mode:
             raise RuntimeError(f"[DION_STEP_REQUIRES_DISTRIBUTED_MODE] step={self._step_count}")
         profile = os.environ.get("DION_PROFILE_SPLIT", "").lower() in ("1", "true", "yes")
+        self._profile_enabled = profile
+        self._phase_records = [] if profile else None
+        if profile and torch.cuda.is_available():
+            torch.cuda.synchronize()
         t0 = time.perf_counter() if profile else None
         self._dion_in_step = True
         try:
             self._step_batches(profile, t0)
         finally:
             self._dion_in_step = False
+            if profile:
+                self._report_profile(t0)
         return loss
+
+    # phases the fused kernels fold into another phase's record (PhaseClock)
+    _FUSED_PHASES = {"grad_momentum": "p_matmul", "error_feedback": "apply_update or the next p_matmul"}
+
+    def _report_profile(self, t0) -> None:
+        """algorithm.py:170-218 with HIP-event phase times: one synchronise, then the per-label sums
+        (the reference's [DION_PROFILE] line) and the slowest batches ([DION_PROFILE_BATCH]).
+        Phase times of batches on concurrent streams overlap, so their sum can exceed `total`."""
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        from .runtime import phase_seconds
+        self._profile_records = [(label, phase_seconds(a, b), desc) for label, a, b, desc in
+                                 (self._phase_records or [])]
+        self._phase_records = None
+        if self._global_rank != 0:
+            return
+        by_label, by_desc = OrderedDict(), {}
+        for label in ("grad_momentum", "q_unshard", "p_matmul", "p_reduce", "ortho_r", "error_feedback",
+                      "q_normalize", "apply_update"):
+            by_label[label] = 0.0
+        for label, sec, desc in self._profile_records:
+            by_label[label] = by_label.get(label, 0.0) + sec
+            by_desc[desc] = by_desc.get(desc, 0.0) + sec
+        summary = ", ".join(f"{k}={v:.3f}s" + (f" (fused: {self._FUSED_PHASES[k]})" if k in self._FUSED_PHASES and
+                                              v == 0.0 else "") for k, v in by_label.items())
+        print(f"[DION_PROFILE] step={self._step_count} total={elapsed:.3f}s {summary}", flush=True)
+        for desc, sec in sorted(by_desc.items(), key=lambda kv: kv[1], reverse=True)[:12]:
+            print(f"[DION_PROFILE_BATCH] step={self._step_count} time={sec:.3f}s {desc}", flush=True)
 
     def _step_batches(self, profile, t0):
         width = 3 if self.max_concurrent_tasks is None else int(self.max_concurrent_tasks)
@@ -380,9 +415,6 @@ class MegatronDion(Optimizer):
             # runtime.py:314-315: the elementwise task runs after the Dion batches
             self._apply_elementwise_batches(elementwise)
         self._buffer_cache.clear()  # algorithm.py:219
-        if profile:
-            torch.cuda.synchronize()
-            self._profile_records.append(("step", time.perf_counter() - t0))
 
 
 def _elementwise_moment(state, param, key, legacy, dtype):

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import collections
 import math
+import time
 import weakref
 from typing import Callable, Generator, Iterable, List, Optional
 
@@ -25,6 +26,51 @@ import torch.distributed as dist
 from .codec import factor_rows
 from .dense_grad_cache import consume_if_reduced
 from .kernels import scaled_lr_for_shape
+
+
+class PhaseClock:
+    """DION_PROFILE_SPLIT: the reference's per-phase step profile (dion/runtime.py:67-99,
+    dion/algorithm.py:170-218), timed with HIP events instead of a device synchronise at every
+    mark (which would serialise the streams).  `mark(label)` charges the time since the
+    previous mark of this batch to `label`; MegatronDion.step sums the records per label after
+    one synchronise.  Labels are the reference's: grad_momentum, q_unshard, p_matmul, p_reduce,
+    ortho_r, error_feedback, q_normalize, apply_update.  Fused kernels charge their phase
+    where they end: M += G (and a deferred error feedback) to p_matmul (pass A), the fix-up to
+    q_normalize, an eager error feedback to apply_update; the fused phases are listed with 0 s."""
+
+    def __init__(self, optimizer, device, desc: str):
+        self.records = getattr(optimizer, "_phase_records", None)
+        self.cuda = self.records is not None and getattr(device, "type", "cpu") == "cuda"
+        self.desc = desc
+        self.last = self._now() if self.records is not None else None
+
+    def _now(self):
+        if self.cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        return time.perf_counter()
+
+    def mark(self, label: str) -> None:
+        if self.records is None:
+            return
+        now = self._now()
+        self.records.append((label, self.last, now, self.desc))
+        self.last = now
+
+
+def phase_seconds(start, end) -> float:
+    """Seconds between two PhaseClock stamps (HIP events after a synchronise, or host times)."""
+    if isinstance(start, float):
+        return float(end) - start
+    return start.elapsed_time(end) / 1e3
+
+
+def _batch_desc(batch_group, dist_metas, real, shape) -> str:
+    """runtime.py:48-64 (_profile_desc)."""
+    meta = dist_metas[0] if dist_metas else None
+    return (f"kernel={getattr(batch_group, 'kernel_kind', '')} real={int(real)} shape={tuple(shape)} "
+            f"name={getattr(meta, 'param_name', '')}")
 
 
 class AsyncRuntime:
@@ -328,6 +374,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
              and (commit_updates is None or all(c is None for c in commit_updates[:real]))
              and not bf16_state and codec.supports_deferred_ef(m, n, r, transposed))
+    clock = PhaseClock(optimizer, dev, _batch_desc(batch_group, dist_metas, real, (m, n)))
     pending = [_take_pending(optimizer_states[i]) for i in range(real)]
     if any(p is not None for p in pending):
         alphas = {p[2] for p in pending if p is not None}
@@ -342,6 +389,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
             codec.project_p(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed)
     else:
         codec.project_p(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed)
+    clock.mark("p_matmul")
 
     def ortho(P_slice, entry):
         S = None if sketches is None else sketches.get(entry)
@@ -361,6 +409,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
                 codec.round_bf16(P_own)
         else:
             P_own.copy_(mine)
+        clock.mark("p_reduce")
         if sketches is None:
             codec.orthonormalize(P_own, m, n, transposed,
                                  _sketch_seed(optimizer, batch_cache_key, rank * kch), oversample, state_dtype=sdt)
@@ -431,8 +480,10 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         R = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
         codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero)
 
+    clock.mark("ortho_r")
     eps = float(optimizer.defaults["epsilon"])
     codec.fixup_colnorm(P, R, list(Qs[:real]), nonzero, eps, m, n, transposed)
+    clock.mark("q_normalize")
 
     grp = optim_groups[0] or {}
     st0 = optimizer_states[0] or {}
@@ -454,6 +505,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     else:
         codec.ef_apply(list(momentums[:real]), list(params[:real]), P, R, list(Qs[:real]), nonzero, mu, lr, wd,
                        scaled, transposed)
+    clock.mark("apply_update")
     commit_qs()
     if commit_updates is not None:
         for i in range(real):
@@ -511,8 +563,10 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
              and (commit_updates is None or all(c is None for c in commit_updates[:real]))
              and not bf16_state and codec.supports_deferred_ef(m, n, r, transposed))
+    clock = PhaseClock(optimizer, dev, _batch_desc(batch_group, dist_metas, real, (m, n)))
     _project_with_pending(codec, real_grads, momentums, Qs, P, nonzero, optimizer_states, real, m, n, transposed,
                           defer)
+    clock.mark("p_matmul")
     # reduce-scatter(sum): this rank receives entry fs_rank summed over the FS shards
     P_own = torch.empty((1, mp, r), dtype=torch.float32, device=dev)
     work = dist.reduce_scatter_tensor(P_own, P, op=dist.ReduceOp.SUM, group=fs_group, async_op=True)
@@ -526,6 +580,7 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         work.wait()
         if bf16_state:
             codec.round_bf16(P_own)
+    clock.mark("p_reduce")
     own = indices[fs_rank]
     if own >= real or dist_metas[own] is None:
         P_own.zero_()  # a padded entry stays inert (runtime.py:1242-1248)
@@ -551,6 +606,7 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         work.wait()
         if bf16_state:
             codec.round_bf16(R)
+    clock.mark("ortho_r")
     colsum = torch.empty((real, r), dtype=torch.float32, device=dev)
     codec.fixup_colsum(P, R, list(Qs[:real]), nonzero, colsum, m, n, transposed)
     qgroup = getattr(batch_group, "q_norm_group", None)
@@ -559,8 +615,10 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         yield
         work.wait()
     codec.colnorm_apply(R, list(Qs[:real]), colsum, float(optimizer.defaults["epsilon"]), m, n, transposed)
+    clock.mark("q_normalize")
     _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim_groups, optimizer_states,
                    dist_metas, real, m, n, transposed, defer, commit_updates, commit_qs)
+    clock.mark("apply_update")
 
 
 def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, optim_groups, real_grads,
@@ -607,6 +665,7 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         if tuple(Qs[i].shape) != (nq, c1 - c0):
             raise RuntimeError(f"[DION_Q_UNSHARD_LOCAL_RANK_MISMATCH] step={optimizer._step_count} entry={i} "
                                f"local_shape={tuple(Qs[i].shape)} expected={(nq, c1 - c0)} r={r} tp={T}")
+    clock = PhaseClock(optimizer, dev, _batch_desc(batch_group, dist_metas, real, (m, n)))
     local = torch.zeros((B, nq, widest), dtype=qdt, device=dev)
     for i in range(B):
         local[i, :, :c1 - c0].copy_(Qs[i])
@@ -620,6 +679,7 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         Qfull[:, :, a:b].copy_(gathered[k, :, :, :b - a])
     del local, gathered
     qviews = [Qfull[i] for i in range(B)]
+    clock.mark("q_unshard")
     P = torch.zeros((B, mp, r), dtype=torch.float32, device=dev)
     nonzero = torch.zeros((B,), dtype=torch.int32, device=dev)
     defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
@@ -627,6 +687,7 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
              and not bf16_state and codec.supports_deferred_ef(m, n, r, transposed))
     _project_with_pending(codec, real_grads, momentums, qviews, P, nonzero, optimizer_states, real, m, n, transposed,
                           defer)
+    clock.mark("p_matmul")
     for coll in tuple(getattr(batch_collectives, "fs_p_collectives", None) or ()):
         if coll.process_group is not None and int(coll.world_size) > 1:
             idx = [int(i) for i in coll.indices]
@@ -644,6 +705,7 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         work.wait()
         if bf16_state:
             codec.round_bf16(P)
+    clock.mark("p_reduce")
     yield from distributed_orthonormalize(optimizer, P, real, m, n, transposed, batch_group.ortho_group, dist_metas,
                                           batch_cache_key, sketches)
     if bf16_state:
@@ -664,6 +726,7 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         work.wait()
         if bf16_state:
             codec.round_bf16(R)
+    clock.mark("ortho_r")
     eps = float(optimizer.defaults["epsilon"])
     qgroup = getattr(batch_group, "q_norm_group", None)
     if qgroup is not None and _group_world(qgroup) > 1:
@@ -675,8 +738,10 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
         codec.colnorm_apply(R, qviews[:real], colsum, eps, m, n, transposed)
     else:
         codec.fixup_colnorm(P, R, qviews[:real], nonzero, eps, m, n, transposed)
+    clock.mark("q_normalize")
     _apply_updates(optimizer, codec, params, momentums, qviews, P, R, nonzero, optim_groups, optimizer_states,
                    dist_metas, real, m, n, transposed, defer, commit_updates)
+    clock.mark("apply_update")
     for i in range(real):  # reshard_q_along_tp: keep this rank's columns
         Qs[i].copy_(Qfull[i][:, c0:c1])
 
