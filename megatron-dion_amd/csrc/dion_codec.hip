@@ -3564,12 +3564,28 @@ struct Geo {
 };
 
 constexpr int kTargetBlocks = 2048;
+#ifndef DION_TB_PA
+#define DION_TB_PA 2048
+#endif
+#ifndef DION_TB_PBC
+#define DION_TB_PBC 512
+#endif
+#ifndef DION_TB_PBR
+#define DION_TB_PBR 1024
+#endif
+#ifndef DION_TB_PAT
+#define DION_TB_PAT 1024
+#endif
+#ifndef DION_RSL
+#define DION_RSL 256
+#endif
+constexpr int kTbPa = DION_TB_PA, kTbPbc = DION_TB_PBC, kTbPbr = DION_TB_PBR, kTbPat = DION_TB_PAT;
 
 // row projection: X rows x cols, reduce over cols (block_rows 128 generic, 256 fast)
-Geo rowproj_geo(int rows, int cols, int batch, int block_rows = 128) {
+Geo rowproj_geo(int rows, int cols, int batch, int block_rows = 128, int target = kTargetBlocks) {
   Geo g;
   g.gx = static_cast<int>(ceil_div(rows, block_rows));
-  long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
+  long want = ceil_div(target, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
   long maxc = ceil_div(cols, 256);
   long nc = want < maxc ? want : maxc;
   if (nc < 1) nc = 1;
@@ -3613,7 +3629,7 @@ bool colproj_fast_ok(int rows, int cols, int r) { return cols % 256 == 0 && rows
 
 // rank_stream_kernel: rows (or columns) one block streams, waves per block, X tiles in flight
 // (measured fastest of (NW, D) in {4, 8} x {2, 3} on the Llama set, round 2)
-constexpr int kRankStreamLen = 512;
+constexpr int kRankStreamLen = DION_RSL;
 constexpr int kRankNW = 8;
 constexpr int kRankD = 2;
 // r = 128 (RU 8): one X tile in flight -- 135 VGPRs, 3 waves per SIMD, against D 2's 202 at 2.
@@ -3641,7 +3657,7 @@ bool colh3_ok(int rows, int cols, int r) {
 Geo colh3_geo(int rows, int cols, int batch, int r) {
   Geo g;
   g.gx = static_cast<int>(ceil_div(cols, 16 * colh3_ct(r) * kColX6NW));
-  long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
+  long want = ceil_div(kTbPbc, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
   long maxc = ceil_div(rows, 256);
   long nc = want < maxc ? want : maxc;
   if (nc < 1) nc = 1;
@@ -3683,10 +3699,10 @@ bool proj_ef_ok(int m, int n, int r, bool transposed) {
 }
 
 Geo proj_ef_geo(int m, int n, int batch, bool transposed, int r) {
-  if (!transposed) return rowproj_geo(m, n, batch, pa_row_block(r));
+  if (!transposed) return rowproj_geo(m, n, batch, pa_row_block(r), kTbPa);
   Geo g;
   g.gx = static_cast<int>(ceil_div(n, 128));
-  long want = ceil_div(kTargetBlocks, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
+  long want = ceil_div(kTbPat, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
   long maxc = ceil_div(m, 256);
   long nc = want < maxc ? want : maxc;
   if (nc < 1) nc = 1;
@@ -3821,7 +3837,8 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
   const bool h3 = fast && gdt == DION_DTYPE_NONE &&
                   (row_mode ? (kPbH3r && rows % (16 * kRBE * kPbRNW) == 0) : colh3_ok(rows, cols, r));
   const Geo geo = row_mode ? rowproj_geo(rows, cols, batch,
-                                         h3 ? 16 * kRBE * kPbRNW : x6 ? 64 * kRBE : (fast ? 64 * kRB : 128))
+                                         h3 ? 16 * kRBE * kPbRNW : x6 ? 64 * kRBE : (fast ? 64 * kRB : 128),
+                                         h3 ? kTbPbr : kTargetBlocks)
                  : h3      ? colh3_geo(rows, cols, batch, r)
                  : x6      ? colx6_geo(rows, cols, batch, r)
                            : colproj_geo(rows, cols, batch, false);
@@ -4218,7 +4235,7 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
           if (nf > n) n = nf;
           const size_t ne = slab_bytes(rowproj_geo(d->m, d->n, chunk, 64 * kRBE), chunk, d->r);
           if (ne > n) n = ne;
-          const size_t nh = slab_bytes(rowproj_geo(d->m, d->n, chunk, 16 * kRBE * kPbRNW), chunk, d->r);
+          const size_t nh = slab_bytes(rowproj_geo(d->m, d->n, chunk, 16 * kRBE * kPbRNW, kTbPbr), chunk, d->r);
           if (nh > n) n = nh;
         } else {
           const size_t nx = slab_bytes(colx6_geo(d->m, d->n, chunk, d->r), chunk, d->r);
