@@ -136,6 +136,7 @@ def build_dion_batches(*, dion_params: Sequence, get_replicate_group: Callable,
     replicate_group = get_replicate_group()
     grouped: Dict[tuple, list] = {}
     groups: Dict[tuple, DionBatchGroup] = {}
+    sync_of: Dict[tuple, list] = {}
     for sp in dion_params:
         state = sp.optimizer_state
         meta = sp.dist_meta
@@ -160,10 +161,24 @@ def build_dion_batches(*, dion_params: Sequence, get_replicate_group: Callable,
                _contract_key(sp.optim_group, state), _group_key(bg))
         grouped.setdefault(key, []).append(sp)
         groups.setdefault(key, bg)
+        if key not in sync_of:  # resolve_batch_group's sync groups (batches.py:519-551)
+            sync = []
+            for g, on in ((replicate_group, cfg.use_low_rank_sync), (tp_group, getattr(cfg, "use_tp_shard", False)),
+                          (fs_group, getattr(cfg, "use_fs_shard", False))):
+                if on and g is not None and group_size(g) > 1 and all(g is not x for x in sync):
+                    sync.append(g)
+            sync_of[key] = sync
 
+    # batches.py:855-884: keys listed per sync group in first-seen group order (keys with no sync
+    # group form one more group), each group's keys sorted by repr, a key's first listing wins
+    per_group: Dict[object, list] = {}
+    for key in grouped:
+        for g in sync_of[key] or [None]:
+            per_group.setdefault(None if g is None else id(g), []).append(key)
+    ordered = list(dict.fromkeys(k for keys in per_group.values() for k in sorted(keys, key=repr)))
     batches: List[DionBatch] = []
     cache_key = 0
-    for key in sorted(grouped, key=repr):
+    for key in ordered:
         items = grouped[key]
         bg = groups[key]
         size = max(1, int(bg.batch_world_size))

@@ -454,6 +454,50 @@ def is_dion_param(param: torch.Tensor, name: str = "") -> bool:
     return not any(k in name for k in ("embedding", "output_layer", "lm_head"))
 
 
+_CHILD_ROW_GROUPS: Dict[Tuple[int, ...], object] = {}
+
+
+def _child_ranks(parent_group, members: Sequence[int]) -> Tuple[int, ...]:
+    ranks = tuple(int(r) for r in dist.get_process_group_ranks(parent_group))
+    return tuple(ranks[k] for k in members)
+
+
+def _prepare_child_row_groups(needed: Sequence[Tuple[int, ...]]) -> None:
+    """Create every split child's owner group on every rank, in one order (row_child.py:94-101,
+    dion_distrib_optimizer.py:260-284 _ensure_child_group).  The ranks of the job exchange the
+    owner sets they need (another FS group's children have other global ranks) and all create
+    the union, sorted, so each new_group call is matched on every rank; the reference's
+    group-local creation is not used because gloo's group-local rendezvous does not line up when
+    ranks create different groups."""
+    want = sorted(set(tuple(int(r) for r in t) for t in needed))
+    if dist.get_world_size() > 1:
+        every = [None] * dist.get_world_size()
+        dist.all_gather_object(every, want)
+        want = sorted(set(t for lst in every for t in lst))
+    for ranks in want:
+        if ranks not in _CHILD_ROW_GROUPS:
+            _CHILD_ROW_GROUPS[ranks] = dist.new_group(list(ranks))
+
+
+def _child_row_group(parent_group, members: Sequence[int]):
+    """The prepared process group of a split child's owners; one owner needs none."""
+    child = _child_ranks(parent_group, members)
+    if len(child) <= 1:
+        return None
+    if child not in _CHILD_ROW_GROUPS:
+        raise RuntimeError(f"[DION_SPLIT_CHILD_GROUP_NOT_PREPARED] ranks={child}")
+    return _CHILD_ROW_GROUPS[child]
+
+
+def _row_axis_group(spec, tspec, fs_group, tp_group, fs_world: int, tp_world: int):
+    """The group a split parent's rows are sharded over (TP on dim 0, else FS on dim 0)."""
+    if tspec is not None and int(tspec[1]) == 0 and tp_world > 1:
+        return tp_group
+    if spec is not None and int(spec[1]) == 0 and fs_world > 1:
+        return fs_group
+    return None
+
+
 def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str, torch.Tensor]],
                       replicate_group=None, base_seed: int = 0, dion_predicate=None, fs_group=None,
                       fs_shards: Optional[Dict[str, tuple]] = None, tp_group=None,
@@ -495,6 +539,34 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
     dist_metas = optimizer.__dict__.setdefault("dist_metas", {})
     group_of = {id(p): g for g in optimizer.param_groups for p in g["params"]}
     dion_named, ew_named = [], []
+    # split children owned by part of their parent's row group need owner groups, created on every
+    # rank before any state (row_child.py:94-101); all ranks hold the same split parents, so they
+    # agree on whether to exchange
+    layouts, needed, sharded_split = {}, [], False
+    for name, p in named_params:
+        spec, tspec = (fs_shards or {}).get(name), (tp_shards or {}).get(name)
+        if not pred(p, name) or (spec is None and tspec is None):
+            continue
+        plan = split_plan(p, optimizer.defaults, global_rows=int((tspec or spec)[0][0]))
+        if plan is None:
+            continue
+        if tspec is not None and tp_group is None:
+            raise RuntimeError(f"[DION_MISSING_BATCH_TP_GROUP] {name}: tp_shards given without tp_group")
+        fs_world = int(dist.get_world_size(fs_group)) if (spec is not None and fs_group is not None) else 1
+        tp_world = int(dist.get_world_size(tp_group)) if tspec is not None else 1
+        tp_rank = int(dist.get_rank(tp_group)) if tspec is not None else 0
+        layout = split_child_layouts(p, plan, fs_spec=spec, tp_spec=tspec, fs_world=fs_world,
+                                     fs_rank=int(dist.get_rank(fs_group)) if fs_world > 1 else 0,
+                                     tp_world=tp_world, tp_rank=tp_rank)
+        row_group = _row_axis_group(spec, tspec, fs_group, tp_group, fs_world, tp_world)
+        layouts[name] = layout
+        if row_group is not None:
+            sharded_split = True
+            size = int(dist.get_world_size(row_group))
+            needed += [_child_ranks(row_group, lay["members"]) for lay in layout.values()
+                       if 1 < len(lay["members"]) < size]
+    if sharded_split:
+        _prepare_child_row_groups(needed)
     for name, p in named_params:
         if not pred(p, name):
             ew_named.append((name, p))
@@ -515,11 +587,21 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
             pstate["momentum"] = torch.zeros_like(p, dtype=_as_dtype(getattr(mpc, "momentum_dtype", None)) or p.dtype)
             tp_world = int(dist.get_world_size(tp_group)) if tspec is not None else 1
             tp_rank = int(dist.get_rank(tp_group)) if tspec is not None else 0
-            layout = split_child_layouts(p, plan, fs_spec=spec, tp_spec=tspec, fs_world=fs_world,
-                                         fs_rank=int(dist.get_rank(fs_group)) if fs_world > 1 else 0,
-                                         tp_world=tp_world, tp_rank=tp_rank)
+            layout = layouts.get(name) or split_child_layouts(p, plan, fs_spec=spec, tp_spec=tspec)
+            row_axis_group = _row_axis_group(spec, tspec, fs_group, tp_group, fs_world, tp_world)
             for kind in kinds:
                 lay = layout[kind]
+                c_fs_group, c_fs_world, c_tp_group, c_tp_world, c_tp_rank = fs_group, fs_world, tp_group, tp_world, tp_rank
+                if row_axis_group is not None and len(lay["members"]) < dist.get_world_size(row_axis_group):
+                    # owners short of the whole row group: the child's own owner group
+                    sub = _child_row_group(row_axis_group, lay["members"])
+                    if row_axis_group is tp_group and tspec is not None and int(tspec[1]) == 0:
+                        c_tp_group, c_tp_world, c_tp_rank = sub, lay["child_world"], max(lay["child_rank"], 0)
+                    else:
+                        c_fs_group, c_fs_world = sub, lay["child_world"]
+                if lay["child_rank"] < 0:
+                    metas[(name, kind)] = None  # no rows of this child here (row_child.py:105-106)
+                    continue
                 rows = lay["local_rows"]
                 cname = f"{name}::{kind}"
                 cuid = child_uid((name,), family, kind)
@@ -527,8 +609,9 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
                                                base_seed=base_seed, param_uid=cuid, param_name=cname,
                                                q_dtype=_as_dtype(getattr(mpc, "q_dtype", None)),
                                                use_low_rank_sync=optimizer.use_low_rank_sync, with_momentum=False,
-                                               fs_shard=None if lay["fs"] is None else (*lay["fs"], fs_world),
-                                               tp_shard=None if lay["tp"] is None else (*lay["tp"], tp_world, tp_rank),
+                                               fs_shard=None if lay["fs"] is None else (*lay["fs"], c_fs_world),
+                                               tp_shard=None if lay["tp"] is None else (*lay["tp"], c_tp_world,
+                                                                                        c_tp_rank),
                                                q_stream=q_stream)
                 for field in ("Q", "r", "local_shape", "global_shape"):
                     pstate[state_key(family, field, kind)] = cstate[field]
@@ -539,13 +622,13 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
                                      tensor_row_shard_sizes=lay["row_sizes"],
                                      row_shard_sizes=lay["row_sizes"] if lay["row_axis"] == "tp" else None)
                 if lay["fs"] is not None:
-                    cmeta.extra.update(fs_group=fs_group, fs_shard_dim=int(lay["fs"][1]),
+                    cmeta.extra.update(fs_group=c_fs_group, fs_shard_dim=int(lay["fs"][1]),
                                        fs_start_idx=int(lay["fs"][2]), fs_end_idx=int(lay["fs"][3]),
-                                       fs_world_size=fs_world)
+                                       fs_world_size=c_fs_world)
                 if lay["tp"] is not None:
-                    cmeta.extra.update(tp_group=tp_group, tp_shard_dim=int(lay["tp"][1]),
+                    cmeta.extra.update(tp_group=c_tp_group, tp_shard_dim=int(lay["tp"][1]),
                                        tp_start_idx=int(lay["tp"][2]), tp_end_idx=int(lay["tp"][3]),
-                                       tp_world_size=tp_world)
+                                       tp_world_size=c_tp_world)
                 metas[(name, kind)] = (ccfg, cmeta, lay["segments"])
             metas[name] = (None, plan)
             continue
@@ -590,6 +673,8 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
                 pstate = optimizer.state[p]
                 M = dict.__getitem__(pstate, "momentum")
                 for kind in kinds:
+                    if metas[(name, kind)] is None:
+                        continue
                     ccfg, cmeta, segs = metas[(name, kind)]
                     cstate = {"momentum": gather_rows(M, segs)}
                     for field in ("Q", "r", "local_shape", "global_shape"):

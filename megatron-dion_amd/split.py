@@ -213,11 +213,15 @@ def split_child_layouts(param: torch.Tensor, plan, *, fs_spec=None, tp_spec=None
     shard, `partition_stride` 2), and the child is sharded over the same group with those
     child rows (resolve_row_child_layout, distrib_dion/row_child.py:30-117; uneven members
     give explicit row sizes, split_child.py:10-52).  The columns keep the parent's shard.  A
-    child whose rows miss a member of the group would need a sub-group (row_child.py:94-106):
-    refused with [DION_SPLIT_CHILD_PARTIAL_OWNERS].
+    child whose rows miss members of the group is owned by the members that hold some of its
+    rows (row_child.py:62-106): it is sharded over their sub-group (the caller builds it from
+    `members`, row_child.py:94-101), a single owner holds it whole (no row shard, world 1), and
+    a rank outside `members` has no rows of it (local_rows 0, no step param, :105-106).
 
     Returns {kind: dict(local_rows, segments (local source rows), fs, tp (child specs or
-    None), row_sizes (every member's child rows, or None), row_axis ("tp" | "fs" | None))}."""
+    None), row_sizes (every owner's child rows, or None), row_axis ("tp" | "fs" | None),
+    members (indices in the parent's row group of the child's owners), child_rank (this rank's
+    index among them, -1 outside), child_world)}."""
     family, kinds, _, flags = plan
     split = tuple(flags[f"{family}_split_shapes"] if family != "linear" else flags["linear_split_rows"])
     local_rows = int(param.shape[0])
@@ -255,27 +259,40 @@ def split_child_layouts(param: torch.Tensor, plan, *, fs_spec=None, tp_spec=None
                                                           tp=(tp_world, k) if row_axis == "tp" else None))
             else:
                 per.append(grouped_child_segments_in_range(a, b, split, kind, kinds_all, family.upper()))
-        if any(not s for s in per):
-            raise RuntimeError(f"[DION_SPLIT_CHILD_PARTIAL_OWNERS] {family} child {kind}: rows owned by "
-                               f"{sum(bool(s) for s in per)} of {len(per)} {row_axis} ranks (the reference "
-                               "builds a child sub-group, row_child.py:94-106; not built)")
-        child_ranges = [(s[0][2], s[-1][3]) for s in per]
+        members = tuple(k for k, s in enumerate(per) if s)
+        if not members:
+            raise RuntimeError(f"[DION_{family.upper()}_NO_{(row_axis or 'ROW').upper()}_OWNERS] child {kind}")
+        child_ranges = [(per[k][0][2], per[k][-1][3]) for k in members]
         child_rows = (split[LINEAR_CHILD_KINDS.index(kind)] if family == "linear"
                       else split[kinds_all.index(kind)] * (gm // sum(split)))
         if child_ranges[0][0] != 0 or child_ranges[-1][1] != child_rows or any(
                 x[1] != y[0] for x, y in zip(child_ranges, child_ranges[1:])):
             raise RuntimeError(f"[DION_{family.upper()}_{(row_axis or 'ROW').upper()}_COVERAGE_MISMATCH] child {kind} "
                                f"child_global_rows={child_rows} member_ranges={child_ranges}")
-        c0, c1 = child_ranges[me]
+        sizes = None if row_axis is None else tuple(b - a for a, b in child_ranges)
+        if me not in members:
+            out[kind] = dict(local_rows=0, segments=[], fs=None, tp=None, row_sizes=sizes, row_axis=row_axis,
+                             members=members, child_rank=-1, child_world=len(members))
+            continue
+        crank = members.index(me)
+        c0, c1 = child_ranges[crank]
         cg = (child_rows, gshape[1])
+        # a single owner holds the child whole: no shard on the row axis (row_child.py:102, world 1)
+        sharded = len(members) > 1
         fs = tp = None
         if fs_spec is not None:
-            fs = (cg, 0, c0, c1) if int(fs_spec[1]) == 0 else (cg, 1, int(fs_spec[2]), int(fs_spec[3]))
+            if int(fs_spec[1]) != 0:
+                fs = (cg, 1, int(fs_spec[2]), int(fs_spec[3]))
+            elif sharded or row_axis != "fs":
+                fs = (cg, 0, c0, c1)
         if tp_spec is not None:
-            tp = (cg, 0, c0, c1) if int(tp_spec[1]) == 0 else (cg, 1, int(tp_spec[2]), int(tp_spec[3]))
+            if int(tp_spec[1]) != 0:
+                tp = (cg, 1, int(tp_spec[2]), int(tp_spec[3]))
+            elif sharded or row_axis != "tp":
+                tp = (cg, 0, c0, c1)
         out[kind] = dict(local_rows=c1 - c0, segments=[(a, b) for a, b, _, _ in per[me]], fs=fs, tp=tp,
-                         row_sizes=None if row_axis is None else tuple(b - a for a, b in child_ranges),
-                         row_axis=row_axis)
+                         row_sizes=sizes if sharded else None, row_axis=row_axis if sharded else None,
+                         members=members, child_rank=crank, child_world=len(members))
     return out
 
 
