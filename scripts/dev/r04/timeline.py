@@ -50,3 +50,13 @@ for q, lst in qs.items():
     print(f"queue {q}: " + " ".join(
         f"{r['Kernel_Name'].split('(')[0].split('<')[0].replace('void ', '')[:14]}@{(int(r['Start_Timestamp'])-t0)/1e3:.0f}+{(int(r['End_Timestamp'])-int(r['Start_Timestamp']))/1e3:.0f}"
         for r in lst if any(k in r["Kernel_Name"] for k in STREAM)))
+# per-family duration sums over the step (non-streaming families are the ortho chain and glue)
+fam = defaultdict(lambda: [0, 0.0])
+for r in step:
+    n = r["Kernel_Name"].split("(")[0].replace("void ", "")
+    n = n.split("<")[0] + ("<" + n.split("<")[1][:12] if "<" in n else "")
+    fam[n][0] += 1
+    fam[n][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+print("per-kernel sums over the step:")
+for n, (c, d) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
+    print(f"  {d:9.1f} us  n={c:3d}  {n}")

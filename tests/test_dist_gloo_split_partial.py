@@ -188,5 +188,5 @@ def test_gloo_split_linear_partial_owners_match_reference(name, deferred):
 @pytest.mark.parametrize("name", CASES)
 @pytest.mark.parametrize("deferred", [False, True], ids=["eager_ef", "deferred_ef"])
 def test_hip_split_linear_partial_owners_match_reference(name, deferred):
-    res = run_split_partial(name, deferred=deferred, device="cuda")
+    res = run_split_partial(name, deferred=deferred, device="cuda:0")
     check_split_partial(res, name, deferred, 2e-5)
