@@ -2721,22 +2721,11 @@ constexpr int kPbrRing = 0;
 constexpr int kPbrMinb = 2;
 // r > 64 pass-B h3 kernels: the split P two cb at a time, two waves per SIMD
 constexpr int kH3Pairs = 1;
-// pass-B h3 kernels at r <= 64 with the pre-split P read by every wave straight from memory
-// (L2: the step's split is 8 KB, read by every wave of every block on those rows) into registers
-// one step ahead, instead of one LDS copy per block and a block barrier per step: the waves of
-// a block stream independently.  Measured slower (round 4, 16 Llama matrices, TB/s LDS ->
-// direct): o 4.66 -> 4.12, qkv 5.33 -> 4.45, fc1 5.89 -> 4.89, fc2 4.74 -> 4.04 -- the
-// per-wave operand reads cost more than the barrier
-#ifndef DION_PB_DIRECT
-#define DION_PB_DIRECT 0
-#endif
-constexpr int kPbDirect = DION_PB_DIRECT;
-template <int RB, int NW, int CT, bool DIRECT = false>
+template <int RB, int NW, int CT>
 __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colproj_h3_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int NQ = RB * 2 * 64;  // f16x8 units of one K-step's P split
-  static_assert(!DIRECT || (RB <= 4 && kColX6PD == 2), "direct operands: r <= 64, two-step ring");
-  __shared__ f16x8 tq[DIRECT ? 1 : 2][DIRECT ? 1 : NQ];
+  __shared__ f16x8 tq[2][NQ];
   const BlockXYZ blk = xcd_block_col();
   const int b = blk.z;
   const int kc = blk.y;
@@ -2767,23 +2756,12 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colpr
     SplitCopyN<NQ, 64 * NW> TA;
     constexpr int PD = kColX6PD;
     ColStepX6<CT> S[PD];
-    // DIRECT: this wave's copy of the step's split P, two steps in registers (parity k)
-    f16x8 AQ[2][DIRECT ? 2 * RB : 1];
-    const f16x8* __restrict__ qd = reinterpret_cast<const f16x8*>(qs) + lane;
-    auto aq_load = [&](f16x8 (&dst)[DIRECT ? 2 * RB : 1], int i) {
-#pragma unroll
-      for (int u = 0; u < 2 * RB; ++u) dst[u] = qd[static_cast<long>(i / 32) * NQ + u * 64];
-    };
 #pragma unroll
     for (int k = 0; k < PD - 1; ++k)
       if (i_begin + 32 * k < i_end) cpx_load<CT>(S[k], M, a.ld_m, i_begin + 32 * k);
-    if constexpr (DIRECT) {
-      aq_load(AQ[0], i_begin);
-    } else {
-      split_copy_load_n(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
-      split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
-      __syncthreads();
-    }
+    split_copy_load_n(TA, qs + static_cast<long>(i_begin / 32) * NQ, tid);
+    split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
+    __syncthreads();
     int cur = 0;
     for (int i0 = i_begin; i0 < i_end; i0 += 32 * PD) {
 #pragma unroll
@@ -2791,19 +2769,9 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colpr
         const int i = i0 + 32 * k;
         if (i >= i_end) break;
         const bool more = i + 32 < i_end;
-        if constexpr (DIRECT) {
-          if (i + 32 * (PD - 1) < i_end) cpx_load<CT>(S[(k + PD - 1) % PD], M, a.ld_m, i + 32 * (PD - 1));
-          if (more) aq_load(AQ[(k + 1) & 1], i + 32);
-        } else {
-          if (kSplitFirstB && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
-          if (i + 32 * (PD - 1) < i_end) cpx_load<CT>(S[(k + PD - 1) % PD], M, a.ld_m, i + 32 * (PD - 1));
-          if (!kSplitFirstB && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
-        }
-        // the step's split P, unit u = 2 cb + (0 hi, 1 lo)
-        auto tqv = [&](int u) -> f16x8 {
-          if constexpr (DIRECT) return AQ[k & 1][u];
-          else return tq[cur][u * 64 + lane];
-        };
+        if (kSplitFirstB && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
+        if (i + 32 * (PD - 1) < i_end) cpx_load<CT>(S[(k + PD - 1) % PD], M, a.ld_m, i + 32 * (PD - 1));
+        if (!kSplitFirstB && more) split_copy_load_n(TA, qs + static_cast<long>(i / 32 + 1) * NQ, tid);
         {
           const ColStepX6<CT>& X = S[k];
           Split2h B[CT];
@@ -2828,10 +2796,10 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colpr
 #pragma unroll
             for (int cp = 0; cp < RB; cp += 2) {
               Split2h A0, A1;
-              A0.hi = tqv(cp * 2 + 0);
-              A0.lo = tqv(cp * 2 + 1);
-              A1.hi = tqv(cp * 2 + 2);
-              A1.lo = tqv(cp * 2 + 3);
+              A0.hi = tq[cur][(cp * 2 + 0) * 64 + lane];
+              A0.lo = tq[cur][(cp * 2 + 1) * 64 + lane];
+              A1.hi = tq[cur][(cp * 2 + 2) * 64 + lane];
+              A1.lo = tq[cur][(cp * 2 + 3) * 64 + lane];
 #pragma unroll
               for (int c = 0; c < CT; ++c) {
                 acc[c][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.lo, B[c].hi, acc[c][cp], 0, 0, 0);
@@ -2854,8 +2822,8 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colpr
             Split2h A[RB];
 #pragma unroll
             for (int cb = 0; cb < RB; ++cb) {
-              A[cb].hi = tqv(cb * 2 + 0);
-              A[cb].lo = tqv(cb * 2 + 1);
+              A[cb].hi = tq[cur][(cb * 2 + 0) * 64 + lane];
+              A[cb].lo = tq[cur][(cb * 2 + 1) * 64 + lane];
             }
 #pragma unroll
             for (int c = 0; c < CT; ++c)
@@ -2876,8 +2844,8 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colpr
 #pragma unroll
             for (int cb = 0; cb < RB; ++cb) {
               Split2h A;
-              A.hi = tqv(cb * 2 + 0);
-              A.lo = tqv(cb * 2 + 1);
+              A.hi = tq[cur][(cb * 2 + 0) * 64 + lane];
+              A.lo = tq[cur][(cb * 2 + 1) * 64 + lane];
 #pragma unroll
               for (int c = 0; c < CT; ++c) {
                 const f32x4 d = mfma3h(A, B[c], f32x4{0.f, 0.f, 0.f, 0.f});
@@ -2888,11 +2856,9 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colpr
           }
         }
         if (!more) break;
-        if constexpr (!DIRECT) {
-          split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
-          __syncthreads();
-          cur ^= 1;
-        }
+        split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
+        __syncthreads();
+        cur ^= 1;
       }
     }
   };
@@ -3353,13 +3319,12 @@ __global__ void __launch_bounds__(256, (RB >= 8 || kCpeRing) ? 2 : 3) colproj_ef
 // 16 c + 4 g .. + 3).  The streamed M is the B operand, the pre-split P the A operand
 // (one scale per matrix); with pass A's max |M| the step's products accumulate in place
 // under one scale for the matrix, else each row gets a per-step scale (as in pass A).
-template <int RB, int NW, bool DIRECT = false>
+template <int RB, int NW>
 __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ? 1 : (kPbrRing ? (RB <= 4 ? kPbrMinb : 2) : 3))
     rowproj_h3_kernel(const ProjArgs a) {
   constexpr int R = 16 * RB;
   constexpr int NQ = RB * 2 * 64;
-  static_assert(!DIRECT || (RB <= 4 && !kPbrRing), "direct operands: r <= 64, ring-free");
-  __shared__ f16x8 tq[DIRECT ? 1 : 2][DIRECT ? 1 : NQ];
+  __shared__ f16x8 tq[2][NQ];
   __shared__ f32x4 xt[NW][32 * 8];
   const BlockXYZ blk = xcd_block();
   const int b = blk.z;
@@ -3410,7 +3375,7 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ?
     constexpr bool FIX = decltype(FIXc)::value;
     RowStepE<DION_DTYPE_NONE> SA, SB;
     SplitCopyN<NQ, 64 * NW> TA;
-    auto compute = [&](RowStepE<DION_DTYPE_NONE>& X, auto qv) {  // qv(u): split P unit u = 2 cb + (0 hi, 1 lo)
+    auto compute = [&](RowStepE<DION_DTYPE_NONE>& X, const f16x8* tqc) {
       Split2h Bx[kRBE];
       float invx[kRBE];
 #pragma unroll
@@ -3430,10 +3395,10 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ?
 #pragma unroll
         for (int cp = 0; cp < RB; cp += 2) {
           Split2h A0, A1;
-          A0.hi = qv(cp * 2 + 0);
-          A0.lo = qv(cp * 2 + 1);
-          A1.hi = qv(cp * 2 + 2);
-          A1.lo = qv(cp * 2 + 3);
+          A0.hi = tqc[(cp * 2 + 0) * 64 + lane];
+          A0.lo = tqc[(cp * 2 + 1) * 64 + lane];
+          A1.hi = tqc[(cp * 2 + 2) * 64 + lane];
+          A1.lo = tqc[(cp * 2 + 3) * 64 + lane];
 #pragma unroll
           for (int rb = 0; rb < kRBE; ++rb) {
             acc[rb][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.lo, Bx[rb].hi, acc[rb][cp], 0, 0, 0);
@@ -3455,8 +3420,8 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ?
         Split2h A[RB];
 #pragma unroll
         for (int cb = 0; cb < RB; ++cb) {
-          A[cb].hi = qv(cb * 2 + 0);
-          A[cb].lo = qv(cb * 2 + 1);
+          A[cb].hi = tqc[(cb * 2 + 0) * 64 + lane];
+          A[cb].lo = tqc[(cb * 2 + 1) * 64 + lane];
         }
 #pragma unroll
         for (int rb = 0; rb < kRBE; ++rb)
@@ -3477,8 +3442,8 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ?
 #pragma unroll
         for (int cb = 0; cb < RB; ++cb) {
           Split2h A;
-          A.hi = qv(cb * 2 + 0);
-          A.lo = qv(cb * 2 + 1);
+          A.hi = tqc[(cb * 2 + 0) * 64 + lane];
+          A.lo = tqc[(cb * 2 + 1) * 64 + lane];
 #pragma unroll
           for (int rb = 0; rb < kRBE; ++rb) {
             const f32x4 d = mfma3h(A, Bx[rb], f32x4{0.f, 0.f, 0.f, 0.f});
@@ -3488,20 +3453,6 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ?
         }
       }
     };
-    if constexpr (DIRECT) {
-      // each wave loads the step's split P with its M rows (no LDS copy, no block barrier)
-      const f16x8* __restrict__ qd = reinterpret_cast<const f16x8*>(qs) + lane;
-      f16x8 AQ[2 * RB];
-      for (int j0 = j_begin; j0 < j_end; j0 += 32) {
-        xload(SA, cj(j0));
-#pragma unroll
-        for (int u = 0; u < 2 * RB; ++u) AQ[u] = qd[static_cast<long>(cj(j0) / 32) * NQ + u * 64];
-        xpose(SA);
-        compute(SA, [&](int u) { return AQ[u]; });
-      }
-      return;
-    }
-    auto lds_q = [&](int c) { return [&, c](int u) { return tq[c][u * 64 + lane]; }; };
     if constexpr (!kPbrRing) {
       split_copy_load_n(TA, qs + static_cast<long>(cj(j_begin) / 32) * NQ, tid);
       split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[0]), tid);
@@ -3512,7 +3463,7 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ?
         xload(SA, cj(j0));
         if (more) split_copy_load_n(TA, qs + static_cast<long>(cj(j0 + 32) / 32) * NQ, tid);
         xpose(SA);
-        compute(SA, lds_q(cur));
+        compute(SA, tq[cur]);
         if (!more) break;
         split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
         __syncthreads();
@@ -3533,7 +3484,7 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ?
         if (kSplitFirstB) xload(SB, cj(j0 + 32));
       }
       xpose(SA);
-      compute(SA, lds_q(cur));
+      compute(SA, tq[cur]);
       if (!more) break;
       split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
       __syncthreads();
@@ -3545,7 +3496,7 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ?
         if (kSplitFirstB) xload(SA, cj(j0 + 64));
       }
       xpose(SB);
-      compute(SB, lds_q(cur));
+      compute(SB, tq[cur]);
       if (!more2) break;
       split_copy_store_n(TA, reinterpret_cast<bf16x8*>(tq[cur ^ 1]), tid);
       __syncthreads();
@@ -3976,12 +3927,10 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     constexpr int RB = decltype(RBc)::value;
     return dispatch_gdt(gdt, [&](auto Gc) {
       constexpr int GD = decltype(Gc)::value;
-      constexpr bool kDirect = kPbDirect && RB <= 4;
       if (h3 && row_mode)
-        hipLaunchKernelGGL((rowproj_h3_kernel<RB, kPbRNW, kDirect>), grid, dim3(64 * kPbRNW), 0, st, a);
+        hipLaunchKernelGGL((rowproj_h3_kernel<RB, kPbRNW>), grid, dim3(64 * kPbRNW), 0, st, a);
       else if (h3)
-        hipLaunchKernelGGL((colproj_h3_kernel<RB, kColX6NW, colh3_ct(16 * RB), kDirect>), grid, dim3(64 * kColX6NW),
-                           0, st, a);
+        hipLaunchKernelGGL((colproj_h3_kernel<RB, kColX6NW, colh3_ct(16 * RB)>), grid, dim3(64 * kColX6NW), 0, st, a);
       else if (x6)
         hipLaunchKernelGGL((colproj_x6_kernel<RB, kColX6NW>), grid, dim3(64 * kColX6NW), 0, st, a);
       else if (fast && row_mode)
