@@ -85,15 +85,21 @@ KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("ef_apply", True): ("rank_stream_kernel<4, false, 8, 2>", 2)}
 
 
-# --state-dtype bf16 (the speedrun's bf16 momentum and Q, SURVEY 8c case viii): eager EF,
-# bytes per element A: G 2 + M 2 + M 2, B: M 2, EF + weight update in one pass: M 4 + W 8
-BYTES_PER_ELEM_BF16 = {"project_p": 6.0, "project_r": 2.0, "ef_apply": 12.0}
+# --state-dtype bf16 (the speedrun's bf16 momentum and Q, SURVEY 8c case viii), bytes per
+# element: pass A G 2 + M 2 + M 2 (the deferred EF rides along), B: M 2, the weight update W 8
+# (16 per step); eager EF: the update pass also moves M (EF + weight update: M 4 + W 8, 20 per step)
+BYTES_PER_ELEM_BF16 = {"project_p": 6.0, "project_p_ef": 6.0, "project_r": 2.0, "ef_apply": 12.0,
+                       "ef_apply_w": 8.0}
 KERNEL_OF_BF16 = {("project_p", False): ("b16_row_kernel<4, 2>", 1),
                   ("project_p", True): ("b16_col_kernel<4, 2>", 1),
                   ("project_r", False): ("b16_col_kernel<4, 0>", 1),
                   ("project_r", True): ("b16_row_kernel<4, 0>", 1),
+                  ("project_p_ef", False): ("b16_row_ef_kernel<4, 2>", 1),
+                  ("project_p_ef", True): ("b16_col_ef_kernel<4, 2>", 1),
                   ("ef_apply", False): ("b16_stream_kernel<4, 8, false>", 1),
-                  ("ef_apply", True): ("b16_stream_kernel<4, 8, true>", 1)}
+                  ("ef_apply", True): ("b16_stream_kernel<4, 8, true>", 1),
+                  ("ef_apply_w", False): ("b16_stream_kernel<4, 8, false>", 1),
+                  ("ef_apply_w", True): ("b16_stream_kernel<4, 8, true>", 1)}
 
 
 class TimedCodec:
@@ -368,7 +374,6 @@ def main():
     if bf16_state:
         global BYTES_PER_ELEM
         BYTES_PER_ELEM = BYTES_PER_ELEM_BF16
-        args.eager_ef = True  # no deferred-EF pass A for a bf16 momentum
     mpc = mda.DionMixedPrecisionConfig(momentum_dtype=torch.bfloat16, q_dtype=torch.bfloat16) if bf16_state else None
     kw = {} if not args.eager_ef else {"defer_error_feedback": False}
     min_side = min(min(m, n) for _, m, n in shapes)
@@ -380,7 +385,10 @@ def main():
         group = install_loopback(args.simulate_world)
     attach_dp_routing(opt, named, replicate_group=group, q_stream="cpu")
     assert all(opt.state[p]["r"] == rank_r for _, p in named), "rank rule gave another r"
-    deferred = bool(opt._defer_ef) and codec.supports_deferred_ef(*shapes[0][1:], rank_r, shapes[0][1] < shapes[0][2])
+    sdt = torch.bfloat16 if bf16_state else torch.float32
+    deferred = bool(opt._defer_ef) and all(
+        codec.supports_deferred_ef(m, n, rank_r, m < n, state_dtype=sdt, grad_dtype=torch.bfloat16)
+        for _, m, n in shapes)
     elems = sum(m * n for _, m, n in shapes)
 
     for _ in range(args.warmup):
@@ -429,7 +437,7 @@ def main():
     roofline = None
     if per_kernel:
         roofline = kernel_roofline(per_kernel, elems, ms_per_step, args.probe_steps, deferred,
-                                   step_bpe=20.0 if bf16_state else None, r=rank_r)
+                                   step_bpe=(16.0 if deferred else 20.0) if bf16_state else None, r=rank_r)
 
     wl = args.workload if (args.layers or default_layers) == default_layers else \
         f"{args.workload} ({args.layers} layers, debug)"

@@ -23,7 +23,9 @@
  *    every M and Q pointer then addresses bf16 (uint16) data, W stays fp32, and the
  *    fp32 P / R buffers hold bf16-representable values, rounded (nearest even)
  *    wherever the reference's bf16 tensors round (runtime.py:1560-1616, ortho.py:123,
- *    kernels.py:54-83, 229-290).  dion_project_p_ef is DION_E_UNSUPPORTED in this mode;
+ *    kernels.py:54-83, 229-290).  dion_project_p_ef exists in this mode for r a multiple
+ *    of 32 and a bf16 (or no) gradient on whole streaming blocks (its workspace query
+ *    says which); elsewhere it is DION_E_UNSUPPORTED;
  *  - orientation follows the reference's DionParamConfig.is_transposed
  *    (dion/state.py:304-310): transposed == 0 => P has m rows (P = M Q),
  *    transposed == 1 => P has n rows (P = M^T Q).  m_P = transposed ? n : m,
@@ -112,7 +114,9 @@ typedef struct DionPendingEF {
  * for every entry whose pending factors are non-NULL (the rest as dion_project_p).
  * Same sums, same order as the eager schedule (error feedback of step t,
  * kernels.py:54-154, then M += G of step t+1, runtime.py:1560-1566), but the
- * momentum is read and written once instead of twice.  Returns
+ * momentum is read and written once instead of twice.  bf16 state: the eager
+ * update's M = rne(M + rne(alpha rne(P R^T))) on the same value (each element, before
+ * its gradient), the increment from fp32 sums of the exact bf16 products.  Returns
  * DION_E_UNSUPPORTED (and enqueues nothing) for shapes without the fused kernel
  * (query: dion_workspace_bytes(desc, DION_OP_PROJECT_P_EF, ...)); the caller then
  * applies the pending EF with dion_ef_apply(W = NULL) and calls dion_project_p.

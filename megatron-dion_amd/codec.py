@@ -132,12 +132,16 @@ class HipDionCodec:
                                      ws.numel(), self._stream())
         _lib.check(rc, "dion_project_p")
 
-    def supports_deferred_ef(self, m: int, n: int, r: int, transposed: bool, state_dtype=torch.float32) -> bool:
-        """True when the fused deferred-EF pass A exists for this shape (dion_project_p_ef)."""
-        key = (int(m), int(n), int(r), bool(transposed), state_dtype)
+    def supports_deferred_ef(self, m: int, n: int, r: int, transposed: bool, state_dtype=torch.float32,
+                             grad_dtype=None) -> bool:
+        """True when the fused deferred-EF pass A exists for this shape, state dtype and gradient
+        dtype (dion_project_p_ef)."""
+        key = (int(m), int(n), int(r), bool(transposed), state_dtype, grad_dtype)
         ok = self._ef_ok.get(key)
         if ok is None:
             d = self._desc(1, m, n, r, transposed, state_dtype=state_dtype)
+            if grad_dtype is not None:
+                d.g_dtype = _dtype_code(torch.empty(0, dtype=grad_dtype))
             nbytes = ctypes.c_size_t(0)
             ok = self.lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P_EF, ctypes.byref(nbytes)) == 0
             self._ef_ok[key] = ok
@@ -151,7 +155,7 @@ class HipDionCodec:
         B = len(momentums)
         if B == 0:
             return
-        m, n = self._check_batch(momentums)
+        m, n = self._check_batch(momentums, momentums[0].dtype)
         r = int(qs[0].shape[1])
         g0 = grads[0] if grads else None
         if grads:

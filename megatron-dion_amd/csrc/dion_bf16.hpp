@@ -488,6 +488,365 @@ __global__ void __launch_bounds__(256, 2) b16_col_kernel(const B16ProjArgs a) {
   if (a.nonzero != nullptr && __any(nz != 0u) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
 }
 
+// ----------------------------------------------------------------------------- deferred EF
+// The previous step's error feedback folded into this step's pass A (the fp32 mode's
+// schedule, dion_project_p_ef): for every element, before the gradient,
+//   M = rne(M + rne(alpha rne(u))),  u = sum_c P'[i][c] R'[j][c]   (R'[i] P'[j] transposed)
+// -- the eager update's formula (b16_ef, kernels.py:54-83) on the same M value, applied one
+// pass later -- then M = rne(M + rne(G)) and P = rne(X Q) as in b16_row_kernel / b16_col_kernel.
+// The step's u tile comes from v_mfma_f32_16x16x32_bf16 (exact bf16 products summed in fp32;
+// K = r in steps of 32), is rounded to the bf16 EF increment in the MFMA layout, and reaches
+// the load layout of M through the wave's LDS tile.  P' and R' are the bf16 panels the host
+// packs from the pending fp32 buffers (bf16 values).  Saves the eager update's M read + write
+// (4 of 20 bytes per element).
+struct B16EfArgs {
+  B16ProjArgs p;
+  const uint16_t* ep;  // (batch, m_P, r) bf16: P' of each entry's pending error feedback
+  const uint16_t* er;  // (batch, n_Q, r) bf16: R'
+  int has[MAXB];       // entry has a pending error feedback
+  float alpha;
+};
+
+// one step's R' fragments: item (nb, kk, lane) = er[(j0 + 16 nb + lane % 16) r + 32 kk + 8 (lane / 16) ..]
+template <int NB, int KK>
+struct B16EfStage {
+  static constexpr int kItems = NB * KK * 64;
+  static constexpr int kPer = (kItems + 255) / 256;
+  u32x4 v[kPer];
+  __device__ __forceinline__ void load(const uint16_t* er, int r, int j0, int tid) {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int item = tid + 256 * it;
+      if (kItems % 256 == 0 || item < kItems) {
+        const int nb = item / (KK * 64), rem = item - nb * (KK * 64), kk = rem >> 6, ln = rem & 63;
+        v[it] = *reinterpret_cast<const u32x4*>(er + static_cast<long>(j0 + 16 * nb + (ln & 15)) * r + 32 * kk +
+                                                8 * (ln >> 4));
+      }
+    }
+  }
+  __device__ __forceinline__ void store(u32x4* dst, int tid) const {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int item = tid + 256 * it;
+      if (kItems % 256 == 0 || item < kItems) dst[item] = v[it];
+    }
+  }
+};
+
+// the EF increments of four accumulator values, packed: rne(alpha rne(u))
+__device__ __forceinline__ u32x2_ b16_ef_pack(const f32x4& u, float alpha) {
+  uint32_t e[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) e[q] = f32_to_bf16_rne(alpha * bf16_round(u[q]));
+  return u32x2_{e[0] | (e[1] << 16), e[2] | (e[3] << 16)};
+}
+
+// row mode (not transposed): b16_row_kernel + the EF.  u's lane (t, g) of tile (rb, jb) is
+// row 16 rb + t, columns 16 jb + 4 g .. + 3 of the wave's 32 x 64 step (D = R'_tile P'_tile^T:
+// A = R' rows of the step's columns, staged per step; B = P' of the wave's rows, in registers);
+// it goes into the transpose tile xt (16-B slots, 8-B halves) and comes back in the load layout.
+template <int RB, int GDT>
+__global__ void __launch_bounds__(256, 2) b16_row_ef_kernel(const B16EfArgs e) {
+  const B16ProjArgs& a = e.p;
+  constexpr int KK = RB / 2;
+  constexpr int NI = 2 * RB * 64;
+  constexpr int NE = 4 * KK * 64;
+  __shared__ u32x4 tp[2][NI];
+  __shared__ u32x4 rs[2][NE];
+  __shared__ u32x4 xt[4][32 * 8];
+  const BlockXYZ blk = xcd_block();
+  const int b = blk.z, kc = blk.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int t = lane & 15, g = lane >> 4;
+  const int lr = lane >> 3, lc = lane & 7;
+  const int r0 = blk.x * kB16RowBlk + wave * 32;
+  const int k_begin = kc * a.kchunk, k_end = min(a.K, k_begin + a.kchunk);
+  uint16_t* X = a.x[b] + static_cast<long>(r0 + lr) * a.ld_x + 8 * lc;
+  const uint16_t* G = GDT == DION_DTYPE_BF16
+                          ? static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(r0 + lr) * a.ld_g + 8 * lc
+                          : nullptr;
+  const uint16_t* tt = a.tt + static_cast<long>(b) * a.rpad * a.Kp;
+  const bool ef_on = e.has[b] != 0;  // uniform over the block
+  const uint16_t* er = e.er + static_cast<long>(b) * a.cols * a.r;
+  bf16x8s Pf[2][KK];
+  if (ef_on) {
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+        Pf[rb][kk] = *reinterpret_cast<const bf16x8s*>(e.ep + (static_cast<long>(b) * a.rows + r0 + 16 * rb + t) * a.r +
+                                                       32 * kk + 8 * g);
+  }
+  u32x4 xs[2][4], gs[2][4];
+  auto load = [&](int s, int j) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xs[s][q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + static_cast<long>(8 * q) * a.ld_x + j));
+      if constexpr (GDT == DION_DTYPE_BF16)
+        gs[s][q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(G + static_cast<long>(8 * q) * a.ld_g + j));
+    }
+  };
+  f32x4 acc[2][RB];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t nz = 0;
+  B16Stage<2, RB> T;
+  B16EfStage<4, KK> RS;
+  if (k_begin < k_end) {
+    load(0, k_begin);
+    T.load(tt, a.Kp, k_begin, tid);
+    T.store(tp[0], tid);
+    if (ef_on) {
+      RS.load(er, a.r, k_begin, tid);
+      RS.store(rs[0], tid);
+    }
+  }
+  __syncthreads();
+  auto step = [&](auto Sc, int j, int cur) -> bool {
+    constexpr int S = decltype(Sc)::value;
+    const bool more = j + 64 < k_end;
+    if (more) {
+      T.load(tt, a.Kp, j + 64, tid);
+      if (ef_on) RS.load(er, a.r, j + 64, tid);
+      load(S ^ 1, j + 64);
+    }
+    u32x4* xw = xt[wave];
+    if (ef_on) {
+      u32x2_* xe = reinterpret_cast<u32x2_*>(xw);
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk)
+            u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8s, rs[cur][(jb * KK + kk) * 64 + lane]),
+                                                        Pf[rb][kk], u, 0, 0, 0);
+          const int row = 16 * rb + t, cg = 2 * jb + (g >> 1);
+          xe[(row * 8 + (cg ^ xt_swz(row))) * 2 + (g & 1)] = b16_ef_pack(u, e.alpha);
+        }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 8 * q + lr;
+        const u32x4 ev = xw[row * 8 + (lc ^ xt_swz(row))];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) xs[S][q][d] = b16_add2(xs[S][q][d], ev[d]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if constexpr (GDT == DION_DTYPE_BF16) {
+        u32x4 o;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] = b16_add2(xs[S][q][d], gs[S][q][d]);
+        xs[S][q] = o;
+      }
+      if (GDT == DION_DTYPE_BF16 || ef_on)
+        __builtin_nontemporal_store(xs[S][q], reinterpret_cast<u32x4*>(X + static_cast<long>(8 * q) * a.ld_x + j));
+      nz |= (xs[S][q][0] | xs[S][q][1] | xs[S][q][2] | xs[S][q][3]) & 0x7FFF7FFFu;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 8 * q + lr;
+      xw[row * 8 + (lc ^ xt_swz(row))] = xs[S][q];
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      bf16x8s B[2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int row = 16 * rb + t;
+        B[rb] = __builtin_bit_cast(bf16x8s, xw[row * 8 + ((4 * ss + g) ^ xt_swz(row))]);
+      }
+#pragma unroll
+      for (int cb = 0; cb < RB; ++cb) {
+        const bf16x8s A = __builtin_bit_cast(bf16x8s, tp[cur][(ss * RB + cb) * 64 + lane]);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[rb], acc[rb][cb], 0, 0, 0);
+      }
+    }
+    if (!more) return false;
+    T.store(tp[cur ^ 1], tid);
+    if (ef_on) RS.store(rs[cur ^ 1], tid);
+    __syncthreads();
+    return true;
+  };
+  for (int j = k_begin; j < k_end; j += 128) {
+    if (!step(std::integral_constant<int, 0>{}, j, 0)) break;
+    if (!step(std::integral_constant<int, 1>{}, j + 64, 1)) break;
+  }
+  float* out = a.slab + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * a.r;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(r0 + 16 * rb + t) * a.r + 16 * cb + 4 * g) = acc[rb][cb];
+  if (a.nonzero != nullptr && __any(nz != 0u) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
+}
+
+// column mode (transposed storage): b16_col_kernel + the EF.  u = R'[i] P'[j]: D = P'_tile
+// R'_tile^T (A = P' of the wave's 64 columns, in registers; B = R' rows of the step, staged);
+// lane (t, g) of tile (ib, jb) holds row 16 ib + t, columns 16 jb + 4 g .. + 3, written to the
+// wave's padded LDS tile and read back as the load layout's rows 8 g + e, columns 4 t .. + 3.
+constexpr int kB16EfLd = 17;  // u32x2 slots per row of the column kernel's EF tile (16 + 1 pad)
+template <int RB, int GDT>
+__global__ void __launch_bounds__(256, 2) b16_col_ef_kernel(const B16EfArgs e) {
+  const B16ProjArgs& a = e.p;
+  constexpr int KK = RB / 2;
+  constexpr int NI = RB * 64;
+  constexpr int NE = 2 * KK * 64;
+  __shared__ u32x4 tp[2][NI];
+  __shared__ u32x4 rs[2][NE];
+  __shared__ u32x2_ et[4][32 * kB16EfLd];
+  const BlockXYZ blk = xcd_block();
+  const int b = blk.z, kc = blk.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int t = lane & 15, g = lane >> 4;
+  const int wc = blk.x * kB16ColBlk + wave * 64;
+  const int c0 = wc + 4 * t;
+  const int k_begin = kc * a.kchunk, k_end = min(a.K, k_begin + a.kchunk);
+  uint16_t* X = a.x[b] + static_cast<long>(8 * g) * a.ld_x + c0;
+  const uint16_t* G = GDT == DION_DTYPE_BF16
+                          ? static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(8 * g) * a.ld_g + c0
+                          : nullptr;
+  const uint16_t* tt = a.tt + static_cast<long>(b) * a.rpad * a.Kp;
+  const bool ef_on = e.has[b] != 0;
+  const uint16_t* er = e.er + static_cast<long>(b) * a.rows * a.r;
+  bf16x8s Pf[4][KK];
+  if (ef_on) {
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+        Pf[jb][kk] = *reinterpret_cast<const bf16x8s*>(e.ep + (static_cast<long>(b) * a.cols + wc + 16 * jb + t) * a.r +
+                                                       32 * kk + 8 * g);
+  }
+  u32x2_ xs[2][8], gs[2][8];
+  auto load = [&](int s, int i) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      xs[s][q] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_*>(X + static_cast<long>(i + q) * a.ld_x));
+      if constexpr (GDT == DION_DTYPE_BF16)
+        gs[s][q] = __builtin_nontemporal_load(reinterpret_cast<const u32x2_*>(G + static_cast<long>(i + q) * a.ld_g));
+    }
+  };
+  f32x4 acc[4][RB];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t nz = 0;
+  B16Stage<1, RB> T;
+  B16EfStage<2, KK> RS;
+  if (k_begin < k_end) {
+    load(0, k_begin);
+    T.load(tt, a.Kp, k_begin, tid);
+    T.store(tp[0], tid);
+    if (ef_on) {
+      RS.load(er, a.r, k_begin, tid);
+      RS.store(rs[0], tid);
+    }
+  }
+  __syncthreads();
+  auto step = [&](auto Sc, int i, int cur) -> bool {
+    constexpr int S = decltype(Sc)::value;
+    const bool more = i + 32 < k_end;
+    if (more) {
+      T.load(tt, a.Kp, i + 32, tid);
+      if (ef_on) RS.load(er, a.r, i + 32, tid);
+      load(S ^ 1, i + 32);
+    }
+    if (ef_on) {
+      u32x2_* ew = et[wave];
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk)
+            u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Pf[jb][kk],
+                                                        __builtin_bit_cast(bf16x8s, rs[cur][(ib * KK + kk) * 64 + lane]), u,
+                                                        0, 0, 0);
+          ew[(16 * ib + t) * kB16EfLd + 4 * jb + g] = b16_ef_pack(u, e.alpha);
+        }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const u32x2_ ev = ew[(8 * g + q) * kB16EfLd + t];
+        xs[S][q] = u32x2_{b16_add2(xs[S][q][0], ev[0]), b16_add2(xs[S][q][1], ev[1])};
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if constexpr (GDT == DION_DTYPE_BF16)
+        xs[S][q] = u32x2_{b16_add2(xs[S][q][0], gs[S][q][0]), b16_add2(xs[S][q][1], gs[S][q][1])};
+      if (GDT == DION_DTYPE_BF16 || ef_on)
+        __builtin_nontemporal_store(xs[S][q], reinterpret_cast<u32x2_*>(X + static_cast<long>(i + q) * a.ld_x));
+      nz |= (xs[S][q][0] | xs[S][q][1]) & 0x7FFF7FFFu;
+    }
+    bf16x8s B[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      u32x4 v;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t x0 = xs[S][2 * d][c >> 1], x1 = xs[S][2 * d + 1][c >> 1];
+        v[d] = (c & 1) ? ((x0 >> 16) | (x1 & 0xFFFF0000u)) : ((x0 & 0xFFFFu) | (x1 << 16));
+      }
+      B[c] = __builtin_bit_cast(bf16x8s, v);
+    }
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      const bf16x8s A = __builtin_bit_cast(bf16x8s, tp[cur][cb * 64 + lane]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[c], acc[c][cb], 0, 0, 0);
+    }
+    if (!more) return false;
+    T.store(tp[cur ^ 1], tid);
+    if (ef_on) RS.store(rs[cur ^ 1], tid);
+    __syncthreads();
+    return true;
+  };
+  for (int i = k_begin; i < k_end; i += 64) {
+    if (!step(std::integral_constant<int, 0>{}, i, 0)) break;
+    if (!step(std::integral_constant<int, 1>{}, i + 32, 1)) break;
+  }
+  float* out = a.slab + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * a.r;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(c0 + c) * a.r + 16 * cb + 4 * g) = acc[c][cb];
+  if (a.nonzero != nullptr && __any(nz != 0u) && lane == 0) atomicMax(&a.nonzero[b], kAbsUnknown);
+}
+
+// fp32 buffers of bf16 values -> bf16 panels (exact), entries with a null source skipped
+struct B16PackArgs {
+  const float* src[2 * MAXB];
+  uint16_t* dst[2 * MAXB];
+  long count[2 * MAXB];
+};
+__global__ void __launch_bounds__(256) b16_pack_kernel(const B16PackArgs a) {
+  const int s = blockIdx.y;
+  const float* src = a.src[s];
+  if (src == nullptr) return;
+  uint16_t* dst = a.dst[s];
+  const long n8 = a.count[s] / 8;
+  for (long i = static_cast<long>(blockIdx.x) * 256 + threadIdx.x; i < n8; i += static_cast<long>(gridDim.x) * 256) {
+    const f32x4 x0 = reinterpret_cast<const f32x4*>(src)[2 * i];
+    const f32x4 x1 = reinterpret_cast<const f32x4*>(src)[2 * i + 1];
+    u32x4 o;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      o[d] = f32_to_bf16_rne(x0[2 * d]) | (static_cast<uint32_t>(f32_to_bf16_rne(x0[2 * d + 1])) << 16);
+      o[2 + d] = f32_to_bf16_rne(x1[2 * d]) | (static_cast<uint32_t>(f32_to_bf16_rne(x1[2 * d + 1])) << 16);
+    }
+    reinterpret_cast<u32x4*>(dst)[i] = o;
+  }
+}
+
 // ----------------------------------------------------------------------------- updates
 // For every element (i, j) of the m x n storage:
 //   u = sum_c RF_u[i][c] CF_u[j][c];   M = rne(M + rne(alpha rne(u)))      (error feedback)
@@ -866,23 +1225,39 @@ Geo fast_geo(bool row_mode, int out_rows, int K, int batch) {
   return g;
 }
 
-size_t proj_ws(int m, int n, int r, int batch, bool row_mode) {
+// the EF panels (P' and R' in bf16) after the thin panel, when the pass carries the error feedback
+size_t ef_panel_bytes(int m, int n, int r, int batch) {
+  return (sizeof(uint16_t) * static_cast<size_t>(batch) * (static_cast<size_t>(m) + n) * r + 255) / 256 * 256;
+}
+
+size_t proj_ws(int m, int n, int r, int batch, bool row_mode, bool with_ef = false) {
   const int out_rows = row_mode ? m : n, K = row_mode ? n : m;
   const Geo g = geo(out_rows, K, batch);
   const Geo f = fast_geo(row_mode, out_rows, K, batch);
   const int nchunk = g.nchunk > f.nchunk ? g.nchunk : f.nchunk;  // either kernel may run (alignment)
   const size_t slab = (sizeof(float) * static_cast<size_t>(batch) * nchunk * out_rows * r + 255) / 256 * 256;
-  return slab + sizeof(uint16_t) * static_cast<size_t>(batch) * rpad_of(r) * kpad_of(K);
+  const size_t thin = (sizeof(uint16_t) * static_cast<size_t>(batch) * rpad_of(r) * kpad_of(K) + 255) / 256 * 256;
+  return slab + thin + (with_ef ? ef_panel_bytes(m, n, r, batch) : 0);
 }
 
-// one projection of up to MAXB matrices: out (batch, out_rows, r) = rne(X T) or rne(X^T T)
+// the deferred-EF pass A exists for the streaming kernels' shapes with r = 32 or 64 (r = 96 / 128
+// spill past 256 VGPRs) and a bf16 (or no) gradient
+bool ef_ok(bool row_mode, int m, int n, int r, int gdt) {
+  return (r == 32 || r == 64) && fast_ok(row_mode, m, n, r, gdt);
+}
+
+// one projection of up to MAXB matrices: out (batch, out_rows, r) = rne(X T) or rne(X^T T); with
+// `efP` (pass A only) each entry whose efP[b] is set first takes its pending error feedback
+// M = rne(M + rne(alpha rne(P' R'^T)))
 int project(bool row_mode, int m, int n, int r, int nb, const void* const* G, int gdt, uint16_t* const* X, long ld_x,
             long ld_g, const void* const* thin, bool thin_bf16, float* out, uint32_t* nonzero, void* ws,
-            size_t ws_bytes, hipStream_t st) {
+            size_t ws_bytes, hipStream_t st, const float* const* efP = nullptr, const float* const* efR = nullptr,
+            float alpha = 0.f) {
   if (r > 128) return fail(DION_E_UNSUPPORTED, "bf16 path: r=%d > 128", r);
   const int out_rows = row_mode ? m : n, K = row_mode ? n : m;
   const Geo g = geo(out_rows, K, nb);
-  const size_t need = proj_ws(m, n, r, nb, row_mode);
+  const bool with_ef = efP != nullptr;
+  const size_t need = proj_ws(m, n, r, nb, row_mode, with_ef);
   if (ws == nullptr || ws_bytes < need) return fail(DION_E_WORKSPACE, "bf16 projection needs %zu workspace bytes, got %zu", need, ws_bytes);
   const size_t slab_b = (sizeof(float) * static_cast<size_t>(nb) * g.nchunk * out_rows * r + 255) / 256 * 256;
   float* slab = static_cast<float*>(ws);
@@ -939,10 +1314,54 @@ int project(bool row_mode, int m, int n, int r, int nb, const void* const* G, in
     a.nchunk = fg.nchunk;
   }
   const dim3 grid = fast ? dim3(fg.gx, fg.nchunk, nb) : dim3(g.gx, g.nchunk, nb);
+  B16EfArgs e;
+  if (with_ef) {
+    if (!fast || !ef_ok(row_mode, m, n, r, gdt))
+      return fail(DION_E_UNSUPPORTED, "no deferred-EF bf16 pass A for %dx%d r=%d", m, n, r);
+    const int mp = row_mode ? m : n, nq = row_mode ? n : m;
+    memset(&e, 0, sizeof(e));
+    e.p = a;
+    uint16_t* ep = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(tt) +
+                                               (sizeof(uint16_t) * static_cast<size_t>(nb) * rp * Kp + 255) / 256 * 256);
+    uint16_t* er = ep + static_cast<long>(nb) * mp * r;
+    B16PackArgs pk;
+    memset(&pk, 0, sizeof(pk));
+    for (int b = 0; b < nb; ++b) {
+      if ((efP[b] == nullptr) != (efR[b] == nullptr))
+        return fail(DION_E_INVALID, "pending EF of entry %d has only one factor", b);
+      if (efP[b] && ((reinterpret_cast<uintptr_t>(efP[b]) & 15u) || (reinterpret_cast<uintptr_t>(efR[b]) & 15u)))
+        return fail(DION_E_UNSUPPORTED, "deferred-EF pass A needs 16-byte aligned factors (entry %d)", b);
+      e.has[b] = efP[b] != nullptr;
+      pk.src[b] = efP[b];
+      pk.dst[b] = ep + static_cast<long>(b) * mp * r;
+      pk.count[b] = static_cast<long>(mp) * r;
+      pk.src[nb + b] = efR[b];
+      pk.dst[nb + b] = er + static_cast<long>(b) * nq * r;
+      pk.count[nb + b] = static_cast<long>(nq) * r;
+    }
+    long pblocks = ceil_div(static_cast<long>(mp > nq ? mp : nq) * r / 8, 256);
+    if (pblocks > 1024) pblocks = 1024;
+    hipLaunchKernelGGL(b16_pack_kernel, dim3(static_cast<unsigned>(pblocks), 2 * nb), dim3(256), 0, st, pk);
+    int rc = check_launch("b16_pack");
+    if (rc != DION_OK) return rc;
+    e.ep = ep;
+    e.er = er;
+    e.alpha = alpha;
+  }
   auto launch = [&](auto RBc) {
     constexpr int RB = decltype(RBc)::value;
     return dispatch_gdt(gdt, [&](auto Gc) {
       constexpr int GD = decltype(Gc)::value;
+      if constexpr (RB % 2 == 0 && GD != DION_DTYPE_F32) {
+        if (with_ef) {
+          if (row_mode)
+            hipLaunchKernelGGL((b16_row_ef_kernel<RB, GD>), grid, dim3(256), 0, st, e);
+          else
+            hipLaunchKernelGGL((b16_col_ef_kernel<RB, GD>), grid, dim3(256), 0, st, e);
+          return check_launch("b16_proj_ef");
+        }
+      }
+      if (with_ef) return fail(DION_E_UNSUPPORTED, "no deferred-EF bf16 pass A for r=%d", r);
       if constexpr (GD == DION_DTYPE_F32) {
         if (row_mode)
           hipLaunchKernelGGL((b16_proj_kernel<false, RB, GD>), grid, dim3(256), 0, st, a);

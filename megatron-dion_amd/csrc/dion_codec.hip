@@ -4203,8 +4203,18 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
   size_t need = 0;
   const int chunks[2] = {d->batch < MAXB ? d->batch : MAXB, d->batch % MAXB};
   if (d->m_dtype == DION_DTYPE_BF16) {
-    if (op == DION_OP_PROJECT_P_EF)
-      return fail(DION_E_UNSUPPORTED, "no deferred-EF pass A for bf16 momentum");
+    if (op == DION_OP_PROJECT_P_EF) {
+      const bool row_mode = !d->transposed;
+      if (!b16::ef_ok(row_mode, d->m, d->n, d->r, d->g_dtype))
+        return fail(DION_E_UNSUPPORTED, "no deferred-EF bf16 pass A for %dx%d r=%d", d->m, d->n, d->r);
+      for (int ci = 0; ci < 2; ++ci)
+        if (chunks[ci] > 0) {
+          const size_t n = b16::proj_ws(d->m, d->n, d->r, chunks[ci], row_mode, true);
+          if (n > need) need = n;
+        }
+      *bytes = need;
+      return DION_OK;
+    }
     if (op == DION_OP_PROJECT_P || op == DION_OP_PROJECT_R) {
       const bool row_mode = (op == DION_OP_PROJECT_P) ? !d->transposed : d->transposed;
       for (int ci = 0; ci < 2; ++ci)
@@ -4316,13 +4326,27 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
   if (ef == nullptr) return dion_project_p(d, G, M, Q, P, nonzero, ws, ws_bytes, stream);
   int rc = validate(d);
   if (rc != DION_OK) return rc;
-  if (d->m_dtype != DION_DTYPE_F32) return fail(DION_E_UNSUPPORTED, "no deferred-EF pass A for bf16 momentum");
   if (M == nullptr || Q == nullptr || P == nullptr || ef->P == nullptr || ef->R == nullptr)
     return fail(DION_E_INVALID, "null argument");
   if (d->g_dtype != DION_DTYPE_NONE && G == nullptr) return fail(DION_E_INVALID, "G is null");
   const bool tr = d->transposed != 0;
   const int mp = tr ? d->n : d->m;
   const long ld_m = ldv(d->ld_m, d->n), ld_g = ldv(d->ld_g, d->n);
+  if (d->m_dtype == DION_DTYPE_BF16) {
+    // bf16 momentum / Q: M = rne(M + rne(alpha rne(P' R'^T))), M = rne(M + rne(G)), P = rne(X Q)
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+      const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+      rc = b16::project(!tr, d->m, d->n, d->r, nb, G ? G + b0 : nullptr, d->g_dtype,
+                        reinterpret_cast<uint16_t* const*>(M + b0), ld_m, ld_g,
+                        reinterpret_cast<const void* const*>(Q + b0), true, P + static_cast<long>(b0) * mp * d->r,
+                        nonzero ? nonzero + b0 : nullptr, ws, ws_bytes, st,
+                        reinterpret_cast<const float* const*>(ef->P) + b0,
+                        reinterpret_cast<const float* const*>(ef->R) + b0, ef->alpha);
+      if (rc != DION_OK) return rc;
+    }
+    return DION_OK;
+  }
   if (!proj_ef_ok(d->m, d->n, d->r, tr) || ld_m % 8 != 0 || (d->g_dtype != DION_DTYPE_NONE && ld_g % 8 != 0))
     return fail(DION_E_UNSUPPORTED, "no deferred-EF pass A for %dx%d r=%d", d->m, d->n, d->r);
   for (int b = 0; b < d->batch; ++b) {

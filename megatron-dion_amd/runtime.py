@@ -373,7 +373,8 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     # deferred error feedback: the previous step's M += -(1-mu) P R^T rides on this pass A
     defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
              and (commit_updates is None or all(c is None for c in commit_updates[:real]))
-             and not bf16_state and codec.supports_deferred_ef(m, n, r, transposed))
+             and codec.supports_deferred_ef(m, n, r, transposed, state_dtype=momentums[0].dtype,
+                                           grad_dtype=real_grads[0].dtype if real_grads else None))
     clock = PhaseClock(optimizer, dev, _batch_desc(batch_group, dist_metas, real, (m, n)))
     pending = [_take_pending(optimizer_states[i]) for i in range(real)]
     if any(p is not None for p in pending):
@@ -562,7 +563,8 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     nonzero = torch.zeros((B,), dtype=torch.int32, device=dev)
     defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
              and (commit_updates is None or all(c is None for c in commit_updates[:real]))
-             and not bf16_state and codec.supports_deferred_ef(m, n, r, transposed))
+             and codec.supports_deferred_ef(m, n, r, transposed, state_dtype=momentums[0].dtype,
+                                           grad_dtype=real_grads[0].dtype if real_grads else None))
     clock = PhaseClock(optimizer, dev, _batch_desc(batch_group, dist_metas, real, (m, n)))
     _project_with_pending(codec, real_grads, momentums, Qs, P, nonzero, optimizer_states, real, m, n, transposed,
                           defer)
@@ -684,7 +686,8 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     nonzero = torch.zeros((B,), dtype=torch.int32, device=dev)
     defer = (getattr(optimizer, "_defer_ef", False) and hasattr(codec, "supports_deferred_ef")
              and (commit_updates is None or all(c is None for c in commit_updates[:real]))
-             and not bf16_state and codec.supports_deferred_ef(m, n, r, transposed))
+             and codec.supports_deferred_ef(m, n, r, transposed, state_dtype=momentums[0].dtype,
+                                           grad_dtype=real_grads[0].dtype if real_grads else None))
     _project_with_pending(codec, real_grads, momentums, qviews, P, nonzero, optimizer_states, real, m, n, transposed,
                           defer)
     clock.mark("p_matmul")

@@ -18,13 +18,15 @@ class OracleCodec:
         self.sketch_lookup = sketch_lookup  # fn(P (1, m_P, r)) -> sketch (1, k, m_P) or None
         self.deferred = deferred            # offer the deferred-EF pass A (host-logic tests)
 
-    def supports_deferred_ef(self, m, n, r, transposed, state_dtype=torch.float32):
+    def supports_deferred_ef(self, m, n, r, transposed, state_dtype=torch.float32, grad_dtype=None):
         return self.deferred
 
     def project_p_ef(self, grads, momentums, qs, P, nonzero, transposed, ef_P, ef_R, alpha):
         for b, M in enumerate(momentums):
             if ef_P[b] is not None:
-                upd = (ef_R[b] @ ef_P[b].mT) if transposed else (ef_P[b] @ ef_R[b].mT)
+                # the eager update's arithmetic in the state dtype (ef_apply below)
+                Pb, Rb = ef_P[b].to(M.dtype), ef_R[b].to(M.dtype)
+                upd = (Rb @ Pb.mT) if transposed else (Pb @ Rb.mT)
                 M.add_(upd * alpha)
         self.project_p(grads, momentums, qs, P, nonzero, transposed)
 

@@ -245,3 +245,53 @@ def test_bf16_llama_shape_properties(m, n):
     delta = (Q.float() @ Pb.t()) if transposed else (Pb @ Q.float().t())
     w_ref = W0 * (1 - 0.01 * 0.01) - s * delta.to(torch.bfloat16).float()
     assert maxrel(W, w_ref) <= 5e-3
+
+
+@pytest.mark.parametrize("shapes,r", [([(512, 384)] * 2, 64), ([(384, 1024)] * 2, 64), ([(1536, 4096)], 32),
+                                      ([(256, 512), (512, 256)], 32)],
+                         ids=["rows_r64", "cols_T_r64", "splitk_T_r32", "both_r32"])
+def test_bf16_deferred_ef_matches_eager(shapes, r):
+    """The bf16 deferred-EF pass A (b16_row_ef_kernel / b16_col_ef_kernel) against the eager
+    schedule (b16_stream_kernel EF + update) on the same inputs: same rounding points, the EF
+    increment's fp32 sums in another MFMA order, so the tolerance bars above."""
+    dev = _dev()
+    mats = _seeded(shapes, r, 5, torch.bfloat16)
+    runs = {}
+    for defer in (False, True):
+        names = [f"w{i}" for i in range(len(mats))]
+        params = {n: torch.nn.Parameter(W.to(dev)) for n, (W, _, _) in zip(names, mats)}
+        opt = mda.MegatronDion([params[n] for n in names], lr=0.01, mu=0.95, weight_decay=0.01,
+                               rank_fraction=r / min(min(s) for s in shapes), coalesce_local=False,
+                               mixed_precision_config=BF16, defer_error_feedback=defer)
+        attach_dp_routing(opt, [(n, params[n]) for n in names])
+        for n, (_, Q, _) in zip(names, mats):
+            opt.state[params[n]]["Q"].copy_(Q.to(dev))
+        m0, n0 = shapes[0]
+        assert opt.codec.supports_deferred_ef(m0, n0, r, m0 < n0, state_dtype=torch.bfloat16,
+                                              grad_dtype=torch.bfloat16)
+        name_of = {id(params[n]): n for n in names}
+        out = []
+        for step in range(3):
+            gen = torch.Generator().manual_seed(300 + step)
+            sk = {}
+            for n, (W, _, Gs) in zip(names, mats):
+                mm, kk_ = W.shape
+                mp = kk_ if mm < kk_ else mm
+                sk[n] = torch.randn(1, O.sketch_rows(r, 1.25), mp, generator=gen) * (1.0 / O.sketch_rows(r, 1.25)) ** 0.5
+                params[n].main_grad = Gs[step].to(dev)
+            opt._sketch_override = lambda batch, _sk=sk: {0: _sk[name_of[id(batch.params[0])]][0].to(dev)}
+            opt.step()
+            opt.flush_error_feedback()
+            torch.cuda.synchronize()
+            out.append({n: (params[n].detach().clone(), opt.state[params[n]]["momentum"].float().clone(),
+                            opt.state[params[n]]["Q"].float().clone()) for n in names})
+        runs[defer] = out
+    worst = {}
+    for step in range(3):
+        for n, (W, M, Q) in runs[True][step].items():
+            We, Me, Qe = runs[False][step][n]
+            errs = dict(W=maxrel(W, We), M=maxrel(M, Me), Q=maxrel(Q, Qe))
+            for k, v in errs.items():
+                worst[k] = max(worst.get(k, 0.0), v)
+            assert errs["W"] <= TOL_W and errs["M"] <= TOL_M and errs["Q"] <= TOL_Q, (step, n, errs)
+    print("bf16 deferred vs eager worst", worst)

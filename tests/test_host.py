@@ -35,20 +35,22 @@ def test_library_exports_every_header_symbol():
 def test_deferred_ef_query_names_the_fused_shapes():
     lib = _lib.load()
     nbytes = ctypes.c_size_t(0)
-    for (m, n, r, tr), ok in (((4096, 4096, 64, 0), True), ((28672, 4096, 64, 0), True),
-                              ((4096, 14336, 64, 1), True), ((6144, 4096, 32, 0), True),
-                              ((64, 48, 8, 0), False), ((4096, 4096, 128, 0), True), ((4096, 4096, 128, 1), True),
-                              ((4096, 14300, 64, 1), False)):
+    # (shape, fp32 momentum supported, bf16 momentum supported)
+    for (m, n, r, tr), ok, ok16 in (((4096, 4096, 64, 0), True, True), ((28672, 4096, 64, 0), True, True),
+                                    ((4096, 14336, 64, 1), True, True), ((6144, 4096, 32, 0), True, True),
+                                    ((64, 48, 8, 0), False, False), ((4096, 4096, 128, 0), True, False),
+                                    ((4096, 4096, 128, 1), True, False), ((4096, 14300, 64, 1), False, False)):
         d = _lib.DionBatchDesc(batch=16, m=m, n=n, r=r, transposed=tr, g_dtype=_lib.DTYPE_BF16,
                                m_dtype=_lib.DTYPE_F32, w_dtype=_lib.DTYPE_F32)
         rc = lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P_EF, ctypes.byref(nbytes))
         assert (rc == _lib.DION_OK) == ok, (m, n, r, tr, rc)
         if not ok:
             assert rc == _lib.DION_E_UNSUPPORTED
-        # bf16 momentum (case viii) has no fused deferred-EF pass A: the eager schedule runs
+        # bf16 momentum (case viii): the fused pass A of the bf16 streaming kernels (r = 32 / 64,
+        # whole blocks); elsewhere the eager schedule runs
         d.m_dtype = _lib.DTYPE_BF16
-        assert lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P_EF, ctypes.byref(nbytes)) \
-            == _lib.DION_E_UNSUPPORTED
+        rc16 = lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PROJECT_P_EF, ctypes.byref(nbytes))
+        assert rc16 == (_lib.DION_OK if ok16 else _lib.DION_E_UNSUPPORTED), (m, n, r, tr, rc16)
         for op in (_lib.OP_PROJECT_P, _lib.OP_PROJECT_R, _lib.OP_ORTHONORMALIZE, _lib.OP_FIXUP_COLNORM):
             assert lib.dion_workspace_bytes(ctypes.byref(d), op, ctypes.byref(nbytes)) == _lib.DION_OK
 
