@@ -41,7 +41,7 @@ variants = [op] if len(sys.argv) <= 3 else sys.argv[3].split(",")
 for rnd in range(3):
     for v in variants:
         op = v
-                torch.cuda.synchronize()
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
             run()
