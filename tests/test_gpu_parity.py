@@ -547,11 +547,13 @@ def test_pipelined_two_stream_schedule_is_bit_identical(deferred):
     shapes = [(512, 256)] * 5 + [(256, 768)] * 3 + [(384, 256)] * 4
     kw = dict(defer_error_feedback=deferred, coalesce_max_entries=2)
     ref = _run_schedule(shapes, 64, 3, local_streams=1, **kw)
-    for la in (2, 0):
-        got = _run_schedule(shapes, 64, 3, local_streams=2, pipeline_lookahead=la, **kw)
+    # (streams, lookahead): 3 and 4 streams put the pipelined schedule's groups on 2 and 3
+    # streaming streams (cross-stream hand-offs, per-stream workspaces)
+    for ns, la in ((2, 2), (2, 0), (3, 1), (4, 1), (3, 0), (4, 0)):
+        got = _run_schedule(shapes, 64, 3, local_streams=ns, pipeline_lookahead=la, **kw)
         for i, (a, b) in enumerate(zip(got, ref)):
             for k in range(3):
-                assert torch.equal(a[k], b[k]), (la, i, k)
+                assert torch.equal(a[k], b[k]), (ns, la, i, k)
 
 
 # ---------------------------------------------------------------------------------------------- split children
