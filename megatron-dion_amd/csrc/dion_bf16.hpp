@@ -25,10 +25,15 @@
 
 typedef short bf16x8s __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ uint16_t f32_to_bf16_rne(float x) {
-  const uint32_t u = __float_as_uint(x);
-  if ((u & 0x7FFFFFFFu) > 0x7F800000u) return static_cast<uint16_t>((u >> 16) | 0x0040u);  // quiet NaN
-  return static_cast<uint16_t>((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+// fp32 -> bf16, round to nearest even: v_cvt_pk_bf16_f32 (gfx950; fp32 denormals are kept,
+// .amdhsa_float_denorm_mode_32 3, and a NaN stays a quiet NaN -- MI355X_MICROARCH.md), one
+// instruction where the integer form takes five
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float x) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(x)); }
+// two values at once: (lo, hi) -> lo | hi << 16
+__device__ __forceinline__ uint32_t f32x2_to_bf16x2_rne(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v{lo, hi}), bf16x2v));
 }
 
 __device__ __forceinline__ float bf16_round(float x) { return bf16_to_f32(f32_to_bf16_rne(x)); }
@@ -261,9 +266,8 @@ constexpr int kB16RowBlk = 128;  // row mode: 4 waves x 32 rows per block, 64-co
 constexpr int kB16ColBlk = 256;  // column mode: 4 waves x 64 columns per block, 32-row steps
 
 __device__ __forceinline__ uint32_t b16_add2(uint32_t m, uint32_t g) {
-  const uint32_t lo = f32_to_bf16_rne(__uint_as_float(m << 16) + __uint_as_float(g << 16));
-  const uint32_t hi = f32_to_bf16_rne(__uint_as_float(m & 0xFFFF0000u) + __uint_as_float(g & 0xFFFF0000u));
-  return lo | (hi << 16);
+  return f32x2_to_bf16x2_rne(__uint_as_float(m << 16) + __uint_as_float(g << 16),
+                             __uint_as_float(m & 0xFFFF0000u) + __uint_as_float(g & 0xFFFF0000u));
 }
 
 // one step's thin-operand runs: item (s, cb, lane) = tt[16 cb + lane % 16][k0 + 32 s + 8 (lane / 16) ..]
@@ -535,10 +539,9 @@ struct B16EfStage {
 
 // the EF increments of four accumulator values, packed: rne(alpha rne(u))
 __device__ __forceinline__ u32x2_ b16_ef_pack(const f32x4& u, float alpha) {
-  uint32_t e[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) e[q] = f32_to_bf16_rne(alpha * bf16_round(u[q]));
-  return u32x2_{e[0] | (e[1] << 16), e[2] | (e[3] << 16)};
+  const uint32_t r01 = f32x2_to_bf16x2_rne(u[0], u[1]), r23 = f32x2_to_bf16x2_rne(u[2], u[3]);
+  return u32x2_{f32x2_to_bf16x2_rne(alpha * __uint_as_float(r01 << 16), alpha * __uint_as_float(r01 & 0xFFFF0000u)),
+                f32x2_to_bf16x2_rne(alpha * __uint_as_float(r23 << 16), alpha * __uint_as_float(r23 & 0xFFFF0000u))};
 }
 
 // row mode (not transposed): b16_row_kernel + the EF.  u's lane (t, g) of tile (rb, jb) is
