@@ -1788,17 +1788,22 @@ __device__ __forceinline__ float h3_scale(float amax, float& inv) {
 // same whether the compiler forms it from the product in one step (v_fma_mixlo_f16) or
 // from the fp32 product, and hi + lo represents x s.  With any other s the two roundings
 // differ now and then and the pair misses x s by an ulp of hi.
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split2h(const f32x4& a, const f32x4& b, float s, Split2h& o) {
   // x s is rounded to fp32 ONCE and both limbs come from that value: with contraction the
   // compiler fuses x s - hi into one mixed-precision FMA on the exact product, and where
-  // the rounded product is an fp16 tie, hi and lo then disagree by an ulp of hi
+  // the rounded product is an fp16 tie, hi and lo then disagree by an ulp of hi.  Two values
+  // per instruction (v_pk_mul_f32, v_cvt_pk_f16_f32, v_pk_add_f32): 3 VALU per value, not 5
 #pragma clang fp contract(off)
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float x = (j < 4 ? a[j] : b[j - 4]) * s;
-    const _Float16 h = static_cast<_Float16>(x);
-    o.hi[j] = h;
-    o.lo[j] = static_cast<_Float16>(x - static_cast<float>(h));
+  for (int j = 0; j < 4; ++j) {
+    const f32x2 x = f32x2{j < 2 ? a[2 * j] : b[2 * j - 4], j < 2 ? a[2 * j + 1] : b[2 * j - 3]} * s;
+    const f16x2v h = __builtin_convertvector(x, f16x2v);
+    const f16x2v l = __builtin_convertvector(x - __builtin_convertvector(h, f32x2), f16x2v);
+    o.hi[2 * j] = h[0];
+    o.hi[2 * j + 1] = h[1];
+    o.lo[2 * j] = l[0];
+    o.lo[2 * j + 1] = l[1];
   }
 }
 
