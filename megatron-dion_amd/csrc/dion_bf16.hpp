@@ -1148,12 +1148,19 @@ __global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) b16_stream_kernel(co
       for (int u = 0; u < RU; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
           __builtin_bit_cast(bf16x8, src[((TR ? 1 : 0) * RU + u) * 64 + lane]),
           __builtin_bit_cast(bf16x8, TR ? Fu[u] : Fw[TR ? 0 : u]), acc, 0, 0, 0);
+      // W = fma(beta, rne(d), W decay), two values per instruction (v_cvt_pk_bf16_f32,
+      // v_pk_mul_f32, v_pk_fma_f32): the same per-element operations
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float v = fmaf(a.beta, bf16_round(acc[q]), T.w[q] * a.decay);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rw,
-                                              static_cast<int>((static_cast<long>(s0 + vrow[q]) * a.ld_w + fbase + t) * 4), 0,
-                                              kStreamAux);
+      for (int q = 0; q < 16; q += 2) {
+        const uint32_t d2 = f32x2_to_bf16x2_rne(acc[q], acc[q + 1]);
+        const f32x2v dv{__uint_as_float(d2 << 16), __uint_as_float(d2 & 0xFFFF0000u)};
+        const f32x2v wd = f32x2v{T.w[q], T.w[q + 1]} * a.decay;
+        const f32x2v v = __builtin_elementwise_fma(f32x2v{a.beta, a.beta}, dv, wd);
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[e]), rw,
+                                                static_cast<int>((static_cast<long>(s0 + vrow[q + e]) * a.ld_w + fbase + t) * 4),
+                                                0, kStreamAux);
       }
     }
   };
