@@ -4,9 +4,11 @@ A fused SwiGLU fc1 (gate 24 + up 24 rows, `split_linear`) FS-sharded on its rows
 (16 rows each) has a gate child on ranks {0, 1} and an up child on ranks {1, 2}: each child is
 sharded over its own 2-rank sub-group (row_child.py:94-106, dion_distrib_optimizer.py:260-284),
 rank 1 belongs to both and ranks 2 / 0 hold nothing of gate / up.  Over 2 ranks (24 | 24) each
-child has one owner and is a whole matrix there ("ddp" with world 1).  The product's adapter
-(`attach_dp_routing(..., fs_group=, fs_shards=)` with `split_linear=True`) builds the layouts and
-the sub-groups; the batches, every shard of W and M and every Q on every rank are checked against
+child has one owner and is a whole matrix there ("ddp" with world 1).  TP-sharded rows over 3
+ranks (partition stride 1) give the same owners, each child a TP-sharded ("fsdp_tp") matrix over
+its 2-rank TP sub-group, replayed with the reference's seeded TP sketch slices.  The product's
+adapter (`attach_dp_routing(..., fs_group=, fs_shards=)` or `tp_group=, tp_shards=`, with
+`split_linear=True`) builds the layouts and the sub-groups; the batches, every shard of W and M and every Q on every rank are checked against
 the reference's own run (tests/golden/make_golden_split_partial.py), whose sketches are replayed.
 The CPU leg runs the oracle codec; the GPU leg (`-m gpu`) the HIP codec over the same gloo ranks.
 """
@@ -23,7 +25,7 @@ import torch.multiprocessing as mp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLDEN = os.path.join(HERE, "golden")
-CASES = ["p1_fs3_partial", "p2_fs2_single"]
+CASES = ["p1_fs3_partial", "p2_fs2_single", "p3_tp3_partial"]
 PARENT = "mlp.linear_fc1"
 
 
@@ -48,6 +50,7 @@ def _worker(rank, world, port, name, out_dir, deferred, device):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     import megatron_dion_amd as mda
     from megatron_dion_amd.optimizer import attach_dp_routing
+    from oracle import dion_oracle as O
     from oracle.cpu_codec import OracleCodec
 
     dev = torch.device(device)
@@ -67,14 +70,22 @@ def _worker(rank, world, port, name, out_dir, deferred, device):
     fc1 = params[PARENT]
     fc1.is_linear_fc1, fc1.linear_split_rows = True, tuple(entry["split"])
     pi, bi = info[PARENT], info[bname]
-    shards = {PARENT: ((pi["m"], pi["n"]), 0, pi["rows"][0], pi["rows"][1]),
-              bname: ((bi["m"], bi["n"]), 1, bi["cols"][0], bi["cols"][1])}
+    tp = entry.get("axis") == "tp"
+    if tp:  # TP on the rows of both (the plain matrix's Q holds this rank's columns of r)
+        shards = {PARENT: ((pi["m"], pi["n"]), 0, pi["rows"][0], pi["rows"][1]),
+                  bname: ((bi["m"], bi["n"]), 0, bi["rows"][0], bi["rows"][1])}
+    else:
+        shards = {PARENT: ((pi["m"], pi["n"]), 0, pi["rows"][0], pi["rows"][1]),
+                  bname: ((bi["m"], bi["n"]), 1, bi["cols"][0], bi["cols"][1])}
     kw = {"codec": OracleCodec(deferred=deferred)} if dev.type == "cpu" else {}
     opt = mda.MegatronDion([params[n] for n in names], lr=h["lr"], mu=h["mu"], weight_decay=h["weight_decay"],
                            rank_fraction=float(entry["rf"]), epsilon=h["epsilon"],
                            rcqr_oversample=h["rcqr_oversample"], defer_error_feedback=deferred, split_linear=True,
                            **kw)
-    attach_dp_routing(opt, [(n, params[n]) for n in names], fs_group=dist.group.WORLD, fs_shards=shards)
+    if tp:
+        attach_dp_routing(opt, [(n, params[n]) for n in names], tp_group=dist.group.WORLD, tp_shards=shards)
+    else:
+        attach_dp_routing(opt, [(n, params[n]) for n in names], fs_group=dist.group.WORLD, fs_shards=shards)
     st_b = opt.state[params[bname]]
     assert st_b["r"] == bi["r"]
     st_b["Q"].copy_(t(0, f"{bname}_Q0"))
@@ -97,6 +108,19 @@ def _worker(rank, world, port, name, out_dir, deferred, device):
         # owned entry is real); the reference's async runtime ran the ortho calls in another
         # order than the batches, the P heights (the sketch widths) tell them apart here
         grp = batch.batch_group
+        if grp.kernel_kind == "fsdp_tp":
+            # the reference's seeded TP sketch: this rank's rows of every real entry's sketch
+            # (ortho.py:577-640, 682-779; tests/test_dist_gloo_fstp.py)
+            out = {}
+            for i, meta in enumerate(list(batch.dist_metas)[:int(batch.real_batch_size)]):
+                r = int(batch.entries[i].optimizer_state["r"])
+                gm, gn = (int(x) for x in meta.global_shape)
+                ks = O.sketch_rows(r, h["rcqr_oversample"])
+                seed = O.distributed_sketch_seed(cur["step"] + 1, meta.param_uid, meta.param_name)
+                start, end = int(meta.extra["tp_start_idx"]), int(meta.extra["tp_end_idx"])
+                rows = gn if meta.param_config.is_transposed else gm
+                out[i] = O.reference_sharded_sketch(seed, ks, rows, start, end - start).to(dev)
+            return out
         own = int(dist.get_rank(grp.q_norm_group)) if grp.kernel_kind == "fsdp" else 0
         if own >= int(batch.real_batch_size):
             return None
