@@ -290,8 +290,10 @@ def kernel_names(r):
     if r > 64 and ("project_r", False) in out:
         out[("project_r", False)] = (f"colproj_h3_kernel<{rb}, 4, 2>", 1)
     if r > 64 and ("project_p_ef", False) in out:
-        # r = 128: the h3 row kernel runs with pipeline depth 1 (register budget)
-        out[("project_p_ef", False)] = (f"rowproj_efh3_kernel<{rb}, 2, 1, 2, 4>", 1)
+        # r = 128: the LDS-DMA row kernel (bf16 G, rows a multiple of 256: every bench set)
+        out[("project_p_ef", False)] = ("rowproj_efgl_kernel<2>", 1)
+    if r > 64 and ("project_p_ef", True) in out:
+        out[("project_p_ef", True)] = ("colproj_efgl_kernel<2>", 1)
     if r > 64:
         # r = 128: the weight update keeps one X tile in flight (kRankD8)
         out = {k: (name.replace(f"rank_stream_kernel<{rb}, false, 8, 2", f"rank_stream_kernel<{rb}, false, 8, 1"), n)

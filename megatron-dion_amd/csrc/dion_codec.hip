@@ -2710,6 +2710,11 @@ __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a)
 constexpr int kKR8 = 2;
 constexpr int kNW8 = 4;
 constexpr int kPD8 = 1;
+// r = 128 fused pass A row kernel: 1 = rowproj_efgl_kernel (M/G and the splits by LDS-DMA;
+// bf16 or no G, an even number of 128-row blocks), 0 = rowproj_efh3_kernel everywhere
+constexpr int kPaGl8 = 1;
+// rowproj_efgl_kernel's EF product: 1 = the three h3 terms in separate accumulators
+constexpr int kGlEf3 = 0;
 // blocks per CU the r = 128 transposed fused pass A is compiled for
 // transposed pass-A kernel (colproj_efh3_kernel) at r <= 64: 1 = the two-step SA/SB register
 // ring (234 VGPRs, 2 waves per SIMD; it spills at 3), 0 = no ring, the step's M/G loads
@@ -3103,6 +3108,287 @@ __global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : (RB >= 8 ? 8 / NW : kPa
   }
 }
 
+// ---- LDS-DMA staging (global_load_lds_dwordx4).  Lane l's 16 source bytes land at LDS
+// byte lds_base + 16 l (lds_base wave-uniform, in M0).  Written as inline asm so that hipcc
+// neither counts these loads in its own s_waitcnt bookkeeping nor drains them at a barrier
+// or before an LDS read (with the builtin it waits vmcnt(0) before every ds_read of an LDS
+// array it cannot tell apart from the DMA's target); completion is counted by hand
+// (gl_wait_barrier).  Vector-memory operations retire in issue order on gfx9 (loads and
+// stores share vmcnt), which the counts below rely on.
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)p));
+}
+template <bool NT>
+__device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_t lds_base) {
+  // saddr form: wave-uniform 64-bit base in SGPRs, the lane's 32-bit byte offset in a VGPR
+  unsigned keep;
+  if constexpr (NT)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_base) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_base) : "memory");
+}
+// wait until at most N of this wave's vector-memory operations are outstanding and its LDS
+// operations are done, then the block barrier (the "memory" clobber keeps hipcc's LDS
+// accesses on their side of it)
+template <int N>
+__device__ __forceinline__ void gl_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+// ---- pass A, not transposed, r = 128, with LDS-DMA staging: rowproj_efh3_kernel's
+// arithmetic on 32-row waves and 32-column steps, in 8-wave blocks (256 rows, two waves per
+// SIMD, one block per CU).  Nothing in flight sits in registers: each wave's M and G tiles
+// arrive by LDS-DMA two steps ahead into its two slots, the block's Q / R' splits one step
+// ahead into a double buffer.  A slot is refilled as soon as the step has read it (the new
+// M goes back to HBM straight from the MFMA layout, two 64-B pieces per 128-B line).
+//   M slot (per wave, per step): 32 rows x 8 16-B chunks, chunk k of row r at r * 8 + (k ^ (r & 7))
+//   G slot (bf16): 32 rows x 4 chunks, chunk k of row r at r * 4 + (k ^ ((r >> 2) & 3))
+// The DMA's LDS side is lane-linear, so the swizzles are on the source addresses.  LDS:
+// 2 x (16 + 16) KB of splits + 8 waves x 2 slots x 6 KB = 160 KB.  Per wave and step: 4
+// LDS-DMA loads of the splits, 4 of M, 2 of G (bf16), 4 stores; the wait before each
+// step's barrier leaves the newest M/G step and the stores in flight.
+template <int GDT>
+__global__ void __launch_bounds__(512, 1) rowproj_efgl_kernel(const EfProjArgs e) {
+  constexpr int RB = 8, R = 128, KK = 4, KR = 2, NW = 8;
+  constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;  // f16x8 units of one step's splits
+  constexpr int GCH = GDT == DION_DTYPE_BF16 ? 4 : 0;    // 16-B chunks per G row
+  constexpr int NGI = 32 * GCH / 64;
+  constexpr int NMG = 4 + NGI;  // M/G LDS-DMA loads per wave and step
+  static_assert(GDT != DION_DTYPE_F32, "f32 G slots do not fit next to the splits (rowproj_efh3_kernel runs)");
+  __shared__ f16x8 tq[2][NQ];
+  __shared__ f16x8 rs[2][NR];
+  __shared__ f32x4 ms[2][NW][32 * 8];
+  __shared__ u32x4 gs[2][NW][GCH > 0 ? 32 * GCH : 1];
+  const ProjArgs& a = e.p;
+  const BlockXYZ blk = xcd_block();
+  const int b = blk.z;
+  const int nb = gridDim.z;
+  const int kc = blk.y;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar addressing)
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int row_base = blk.x * (16 * KR * NW) + wave * (16 * KR);  // the grid's x is rows / 256
+  const int j_begin = kc * a.kchunk;
+  const int j_end = min(a.cols, j_begin + a.kchunk);
+  const int nsteps = (j_end - j_begin + 31) / 32;
+  // M: the DMA lane (row 8 q + lane / 8, slot chunk lane % 8) reads source chunk (lane % 8) ^ (lane / 8)
+  const char* Mb = reinterpret_cast<const char*>(a.m[b] + static_cast<long>(row_base) * a.ld_m);
+  const uint32_t m_off = static_cast<uint32_t>(((lane >> 3) * a.ld_m + 4 * ((lane & 7) ^ (lane >> 3))) * 4);
+  // the write-back lane (t, g): rows 16 rb + t, columns 16 c + 4 g .. + 3
+  float* __restrict__ Mw = a.m[b] + static_cast<long>(row_base + t) * a.ld_m + 4 * g;
+  const char* Gb = nullptr;
+  uint32_t g_off = 0;
+  if constexpr (GDT == DION_DTYPE_BF16) {  // DMA lane: row 16 i + lane / 4, slot chunk lane % 4
+    Gb = reinterpret_cast<const char*>(static_cast<const uint16_t*>(a.g[b]) + static_cast<long>(row_base) * a.ld_g);
+    g_off = static_cast<uint32_t>(((lane >> 2) * a.ld_g + 8 * ((lane & 3) ^ ((lane >> 4) & 3))) * 2);
+  }
+  const bool has_ef = e.efr[b] != nullptr;
+  const float invQ = e.inv[b];
+  const float invR = e.inv[nb + b];
+  float invF;
+  const float sF = h3_scale(__uint_as_float(e.amax[2 * nb + b]), invF);  // power of two: P' s is exact
+  const float efinv = e.alpha * invF * invR;
+
+  // the EF's fixed operand (P' rows of this wave), loaded before any LDS-DMA is issued
+  Split2h F[KR][KK];
+  if (has_ef) {
+#pragma unroll
+    for (int rb = 0; rb < KR; ++rb)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const float* src = e.efp[b] + static_cast<long>(row_base + 16 * rb + t) * R + 32 * kk + 8 * g;
+        split2h(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), sF, F[rb][kk]);
+      }
+  } else {
+#pragma unroll
+    for (int rb = 0; rb < KR; ++rb)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) F[rb][kk] = Split2h{};
+  }
+
+  f32x4 acc[KR][RB];
+#pragma unroll
+  for (int rb = 0; rb < KR; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t nzb = 0;
+  float mx = 0.f;
+
+  const u32x4* qs = e.qsplit + b * e.split_stride;
+  const u32x4* rsp = e.rsplit + b * e.split_stride;
+  // the step's Q and R' splits: unit it * 512 + tid of each (R' is staged whether or not
+  // the matrix has a pending EF, so the counts stay fixed; the workspace is always there)
+  const uint32_t u_off = static_cast<uint32_t>(tid) * 16;
+  auto issue_splits = [&](int s, int buf) {
+    const long u0 = static_cast<long>((j_begin + 32 * s) / 32);
+#pragma unroll
+    for (int it = 0; it < NQ / (64 * NW); ++it)
+      glds16<false>(qs + u0 * NQ + it * 64 * NW, u_off, lds_off(&tq[buf][it * 64 * NW + wave * 64]));
+#pragma unroll
+    for (int it = 0; it < NR / (64 * NW); ++it)
+      glds16<false>(rsp + u0 * NR + it * 64 * NW, u_off, lds_off(&rs[buf][it * 64 * NW + wave * 64]));
+  };
+  auto issue_mg = [&](int s, int slot) {
+    const int j = j_begin + 32 * s;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      glds16<kNt != 0>(Mb + (static_cast<long>(8 * q) * a.ld_m + j) * 4, m_off, lds_off(&ms[slot][wave][q * 64]));
+    if constexpr (GDT == DION_DTYPE_BF16) {
+#pragma unroll
+      for (int i = 0; i < NGI; ++i)
+        glds16<false>(Gb + (static_cast<long>(16 * i) * a.ld_g + j) * 2, g_off, lds_off(&gs[slot][wave][i * 64]));
+    }
+  };
+
+  issue_splits(0, 0);
+  issue_mg(0, 0);
+  if (nsteps > 1) {
+    issue_mg(1, 1);
+    gl_wait_barrier<NMG>();
+  } else {
+    gl_wait_barrier<0>();
+  }
+
+  for (int s = 0; s < nsteps; ++s) {
+    const int j = j_begin + 32 * s;
+    const int cur = s & 1;
+    const bool more = s + 1 < nsteps;
+    const bool ahead = s + 2 < nsteps;
+    if (more) issue_splits(s + 1, cur ^ 1);
+
+    // the step's M (+ G) in the MFMA layout: lane (t, g) rows 16 rb + t, columns 16 c + 4 g .. + 3
+    const f32x4* xw = ms[cur][wave];
+    f32x4 X[KR][2];
+    uint2 gv[KR][2];
+#pragma unroll
+    for (int rb = 0; rb < KR; ++rb)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int r = 16 * rb + t, k = 4 * c + g;
+        X[rb][c] = xw[r * 8 + (k ^ xt_swz(r))];
+        if constexpr (GDT == DION_DTYPE_BF16) {
+          const int p = (2 * c + (g >> 1)) ^ ((t >> 2) & 3);
+          gv[rb][c] = reinterpret_cast<const uint2*>(gs[cur][wave])[(r * GCH + p) * 2 + (g & 1)];
+        }
+      }
+    if (ahead) {
+      // the slot is read: refill it (the reads retire first; the DMA writes the same bytes)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue_mg(s + 2, cur);
+    }
+    const f16x8* tqc = tq[cur];
+    const f16x8* rsc = rs[cur];
+    if (has_ef) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        f32x4 ev[KR];
+        if constexpr (kGlEf3) {
+          // the three products in separate accumulators: 6 independent MFMA chains of depth
+          // KK instead of 2 of depth 3 KK, summed once (hi*hi last, as in mfma3h)
+          f32x4 e3[3][KR];
+#pragma unroll
+          for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int rb = 0; rb < KR; ++rb) e3[u][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk) {
+            Split2h A;
+            A.hi = rsc[((c * KK + kk) * 2 + 0) * 64 + lane];
+            A.lo = rsc[((c * KK + kk) * 2 + 1) * 64 + lane];
+#pragma unroll
+            for (int rb = 0; rb < KR; ++rb) {
+              e3[0][rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A.lo, F[rb][kk].hi, e3[0][rb], 0, 0, 0);
+              e3[1][rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A.hi, F[rb][kk].lo, e3[1][rb], 0, 0, 0);
+              e3[2][rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A.hi, F[rb][kk].hi, e3[2][rb], 0, 0, 0);
+            }
+          }
+#pragma unroll
+          for (int rb = 0; rb < KR; ++rb) ev[rb] = (e3[0][rb] + e3[1][rb]) + e3[2][rb];
+        } else {
+#pragma unroll
+          for (int rb = 0; rb < KR; ++rb) ev[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk) {
+            Split2h A;
+            A.hi = rsc[((c * KK + kk) * 2 + 0) * 64 + lane];
+            A.lo = rsc[((c * KK + kk) * 2 + 1) * 64 + lane];
+#pragma unroll
+            for (int rb = 0; rb < KR; ++rb) ev[rb] = mfma3h(A, F[rb][kk], ev[rb]);
+          }
+        }
+#pragma unroll
+        for (int rb = 0; rb < KR; ++rb)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) X[rb][c][q] = fmaf(ev[rb][q], efinv, X[rb][c][q]);
+      }
+    }
+#pragma unroll
+    for (int rb = 0; rb < KR; ++rb)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        if constexpr (GDT == DION_DTYPE_BF16) {
+          X[rb][c][0] += __uint_as_float(gv[rb][c].x << 16);
+          X[rb][c][1] += __uint_as_float(gv[rb][c].x & 0xFFFF0000u);
+          X[rb][c][2] += __uint_as_float(gv[rb][c].y << 16);
+          X[rb][c][3] += __uint_as_float(gv[rb][c].y & 0xFFFF0000u);
+        }
+        nzb |= __float_as_uint(X[rb][c][0]) | __float_as_uint(X[rb][c][1]) | __float_as_uint(X[rb][c][2]) |
+               __float_as_uint(X[rb][c][3]);
+        st_part(reinterpret_cast<f32x4*>(Mw + static_cast<long>(16 * rb) * a.ld_m + j + 16 * c), X[rb][c]);
+      }
+    Split2h Bx[KR];
+    float invx[KR];
+#pragma unroll
+    for (int rb = 0; rb < KR; ++rb) {
+      float m8 = max8abs(X[rb][0], X[rb][1]);
+      m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
+      m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
+      mx = fmaxf(mx, m8);
+      const float sx = h3_scale(m8, invx[rb]);
+      split2h(X[rb][0], X[rb][1], sx, Bx[rb]);
+    }
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      Split2h A;
+      A.hi = tqc[(cb * 2 + 0) * 64 + lane];
+      A.lo = tqc[(cb * 2 + 1) * 64 + lane];
+#pragma unroll
+      for (int rb = 0; rb < KR; ++rb) {
+        const f32x4 d = mfma3h(A, Bx[rb], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[rb][cb][q] = fmaf(d[q], invx[rb], acc[rb][cb][q]);
+      }
+    }
+    if (more) {
+      // retire the next step's splits (and, in order, every older M/G load: the next step's
+      // slot); the newest M/G step and this step's 4 stores may stay in flight
+      if (ahead)
+        gl_wait_barrier<NMG + 2 * KR>();
+      else
+        gl_wait_barrier<2 * KR>();
+    }
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int rb = 0; rb < KR; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(row_base + 16 * rb + t) * R + 16 * cb + 4 * g) =
+          acc[rb][cb] * invQ;
+  if (a.nonzero != nullptr) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    const bool nz = __any((nzb & 0x7FFFFFFFu) != 0u);
+    const uint32_t mb = __float_as_uint(mx);
+    if (nz && lane == 0) atomicMax(&a.nonzero[b], mb > 1u ? mb : 1u);
+  }
+}
+
 // ---- pass A, transposed, h3 products: colproj_ef_kernel's geometry (block = 4 waves x
 // 32 columns, step = 32 rows; lane (t, g) holds columns 2t, 2t + 1 of rows 16 h + 4 g + q)
 // with rowproj_efh3_kernel's arithmetic.  The error feedback's fixed operand is P' of
@@ -3301,6 +3587,221 @@ __global__ void __launch_bounds__(256, (RB >= 8 || kCpeRing) ? 2 : 3) colproj_ef
     __syncthreads();
     cur ^= 1;
   }
+  }
+
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(col_base + 2 * t + c) * R + 16 * cb + 4 * g) =
+          acc[c][cb] * invQ;
+  if (a.nonzero != nullptr) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    const bool nz = __any((nzb & 0x7FFFFFFFu) != 0u);
+    const uint32_t mb = __float_as_uint(mx);
+    if (nz && lane == 0) atomicMax(&a.nonzero[b], mb > 1u ? mb : 1u);
+  }
+}
+
+// ---- pass A, transposed, r = 128, with LDS-DMA staging: colproj_efh3_kernel's arithmetic
+// (lane (t, g): columns 2t, 2t + 1 of rows 16 h + 4 g + q) in 8-wave blocks of 256 columns,
+// the slots and splits staged as in rowproj_efgl_kernel (M/G two steps ahead, splits one).
+//   M slot: 32 rows x 128 B (row-major, as in HBM), G slot (bf16): 32 rows x 64 B.
+// Per wave and step: 4 LDS-DMA loads of the splits, 4 of M, 2 of G (bf16), 8 stores.
+template <int GDT>
+__global__ void __launch_bounds__(512, 1) colproj_efgl_kernel(const EfProjArgs e) {
+  constexpr int RB = 8, R = 128, KK = 4, NW = 8;
+  constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;
+  constexpr int NGI = GDT == DION_DTYPE_BF16 ? 2 : 0;
+  constexpr int NMG = 4 + NGI;
+  static_assert(GDT != DION_DTYPE_F32, "f32 G slots do not fit next to the splits (colproj_efh3_kernel runs)");
+  __shared__ f16x8 tq[2][NQ];
+  __shared__ f16x8 rs[2][NR];
+  __shared__ f32x4 ms[2][NW][32 * 8];
+  __shared__ u32x4 gs[2][NW][NGI > 0 ? 32 * 4 : 1];
+  const ProjArgs& a = e.p;
+  const BlockXYZ blk = xcd_block_col();
+  const int b = blk.z;
+  const int nb = gridDim.z;
+  const int kc = blk.y;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int col_base = blk.x * (32 * NW) + wave * 32;  // the grid's x is columns / 256
+  const int i_begin = kc * a.kchunk;
+  const int i_end = min(a.rows, i_begin + a.kchunk);
+  const int nsteps = (i_end - i_begin + 31) / 32;
+  const char* Mb = reinterpret_cast<const char*>(a.m[b] + col_base);
+  const uint32_t m_off = static_cast<uint32_t>(((lane >> 3) * a.ld_m + 4 * (lane & 7)) * 4);  // row lane / 8, chunk lane % 8
+  float* __restrict__ Mw = a.m[b] + static_cast<long>(4 * g) * a.ld_m + col_base + 2 * t;
+  const char* Gb = nullptr;
+  uint32_t g_off = 0;
+  if constexpr (GDT == DION_DTYPE_BF16) {  // row lane / 4, chunk lane % 4
+    Gb = reinterpret_cast<const char*>(static_cast<const uint16_t*>(a.g[b]) + col_base);
+    g_off = static_cast<uint32_t>(((lane >> 2) * a.ld_g + 8 * (lane & 3)) * 2);
+  }
+  const bool has_ef = e.efr[b] != nullptr;
+  const float invQ = e.inv[b];
+  const float invR = e.inv[nb + b];
+  float invF;
+  const float sF = h3_scale(__uint_as_float(e.amax[2 * nb + b]), invF);  // power of two: P' s is exact
+  const float efinv = e.alpha * invF * invR;
+
+  Split2h F[2][KK];
+  if (has_ef) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const float* src = e.efp[b] + static_cast<long>(col_base + 2 * t + c) * R + 32 * kk + 8 * g;
+        split2h(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), sF, F[c][kk]);
+      }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) F[c][kk] = Split2h{};
+  }
+
+  f32x4 acc[2][RB];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t nzb = 0;
+  float mx = 0.f;
+
+  const u32x4* qs = e.qsplit + b * e.split_stride;
+  const u32x4* rsp = e.rsplit + b * e.split_stride;
+  const uint32_t u_off = static_cast<uint32_t>(tid) * 16;
+  auto issue_splits = [&](int s, int buf) {
+    const long u0 = static_cast<long>((i_begin + 32 * s) / 32);
+#pragma unroll
+    for (int it = 0; it < NQ / (64 * NW); ++it)
+      glds16<false>(qs + u0 * NQ + it * 64 * NW, u_off, lds_off(&tq[buf][it * 64 * NW + wave * 64]));
+#pragma unroll
+    for (int it = 0; it < NR / (64 * NW); ++it)
+      glds16<false>(rsp + u0 * NR + it * 64 * NW, u_off, lds_off(&rs[buf][it * 64 * NW + wave * 64]));
+  };
+  auto issue_mg = [&](int s, int slot) {
+    const long i0 = i_begin + 32 * s;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      glds16<kNt != 0>(Mb + (i0 + 8 * q) * a.ld_m * 4, m_off, lds_off(&ms[slot][wave][q * 64]));
+    if constexpr (GDT == DION_DTYPE_BF16) {
+#pragma unroll
+      for (int i = 0; i < NGI; ++i)
+        glds16<kCpeGnt != 0>(Gb + (i0 + 16 * i) * a.ld_g * 2, g_off, lds_off(&gs[slot][wave][i * 64]));
+    }
+  };
+
+  issue_splits(0, 0);
+  issue_mg(0, 0);
+  if (nsteps > 1) {
+    issue_mg(1, 1);
+    gl_wait_barrier<NMG>();
+  } else {
+    gl_wait_barrier<0>();
+  }
+
+  for (int s = 0; s < nsteps; ++s) {
+    const int i0 = i_begin + 32 * s;
+    const int cur = s & 1;
+    const bool more = s + 1 < nsteps;
+    const bool ahead = s + 2 < nsteps;
+    if (more) issue_splits(s + 1, cur ^ 1);
+
+    f32x2 X[2][4];
+    uint32_t gv[2][4];
+    const f32x2* xw = reinterpret_cast<const f32x2*>(ms[cur][wave]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * h + 4 * g + q;
+        X[h][q] = xw[r * 16 + t];
+        if constexpr (GDT == DION_DTYPE_BF16) gv[h][q] = reinterpret_cast<const uint32_t*>(gs[cur][wave])[r * 16 + t];
+      }
+    if (ahead) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue_mg(s + 2, cur);
+    }
+    const f16x8* tqc = tq[cur];
+    const f16x8* rsc = rs[cur];
+    if (has_ef) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 ev[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          Split2h A;
+          A.hi = rsc[((h * KK + kk) * 2 + 0) * 64 + lane];
+          A.lo = rsc[((h * KK + kk) * 2 + 1) * 64 + lane];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) ev[c] = mfma3h(A, F[c][kk], ev[c]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          X[h][q][0] = fmaf(ev[0][q], efinv, X[h][q][0]);
+          X[h][q][1] = fmaf(ev[1][q], efinv, X[h][q][1]);
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (GDT == DION_DTYPE_BF16) {
+          X[h][q][0] += __uint_as_float(gv[h][q] << 16);
+          X[h][q][1] += __uint_as_float(gv[h][q] & 0xFFFF0000u);
+        }
+        if (GDT != DION_DTYPE_NONE || has_ef)
+          st_stream(reinterpret_cast<f32x2*>(Mw + static_cast<long>(i0 + 16 * h + q) * a.ld_m), X[h][q]);
+        nzb |= __float_as_uint(X[h][q][0]) | __float_as_uint(X[h][q][1]);
+      }
+    Split2h Bx[2];
+    float invx[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const f32x4 lo4{X[0][0][c], X[0][1][c], X[0][2][c], X[0][3][c]};
+      const f32x4 hi4{X[1][0][c], X[1][1][c], X[1][2][c], X[1][3][c]};
+      float m8 = max8abs(lo4, hi4);
+      m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
+      m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
+      mx = fmaxf(mx, m8);
+      const float sx = h3_scale(m8, invx[c]);
+      split2h(lo4, hi4, sx, Bx[c]);
+    }
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+      Split2h A;
+      A.hi = tqc[(cb * 2 + 0) * 64 + lane];
+      A.lo = tqc[(cb * 2 + 1) * 64 + lane];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const f32x4 d = mfma3h(A, Bx[c], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[c][cb][q] = fmaf(d[q], invx[c], acc[c][cb][q]);
+      }
+    }
+    if (more) {
+      // the stores of this step: 8 when M is written, else none
+      if (GDT != DION_DTYPE_NONE || has_ef) {
+        if (ahead)
+          gl_wait_barrier<NMG + 8>();
+        else
+          gl_wait_barrier<8>();
+      } else {
+        if (ahead)
+          gl_wait_barrier<NMG>();
+        else
+          gl_wait_barrier<0>();
+      }
+    }
   }
 
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
@@ -4452,9 +4953,16 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
       constexpr int RB = decltype(RBc)::value;
       return dispatch_gdt(d->g_dtype, [&](auto Gc) {
         constexpr int GD = decltype(Gc)::value;
-        if (tr)
-          hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
-        else  // r = 128: one-step pipeline (register budget)
+        if (tr) {
+          if (RB >= 8 && GD != DION_DTYPE_F32 && kPaGl8 && geo.gx % 2 == 0)  // r = 128: LDS-DMA staging
+            hipLaunchKernelGGL((colproj_efgl_kernel<GD == DION_DTYPE_F32 ? DION_DTYPE_NONE : GD>),
+                               dim3(geo.gx / 2, geo.nchunk, nb), dim3(512), 0, st, e);
+          else
+            hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
+        } else if (RB >= 8 && GD != DION_DTYPE_F32 && kPaGl8 && geo.gx % 2 == 0)  // r = 128: LDS-DMA staging
+          hipLaunchKernelGGL((rowproj_efgl_kernel<GD == DION_DTYPE_F32 ? DION_DTYPE_NONE : GD>),
+                             dim3(geo.gx / 2, geo.nchunk, nb), dim3(512), 0, st, e);
+        else  // r = 128 without it: one-step pipeline (register budget)
           hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, RB >= 8 ? kPD8 : kPaPD, RB >= 8 ? kKR8 : kRBE, RB >= 8 ? kNW8 : kPaNW>),
                              grid, dim3(64 * (RB >= 8 ? kNW8 : kPaNW)), 0, st, e);
         return check_launch(tr ? "colproj_ef" : "rowproj_ef");

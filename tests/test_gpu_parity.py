@@ -408,7 +408,13 @@ def test_llama_shape_properties(m, n):
                                        (256, 1024, 128, torch.bfloat16), (512, 256, 128, torch.float32),
                                        # odd row-block counts with K split over fixed-order slabs
                                        (1152, 640, 64, torch.bfloat16), (1536, 1024, 64, torch.float32),
-                                       (896, 1792, 32, torch.bfloat16)])
+                                       (896, 1792, 32, torch.bfloat16),
+                                       # r = 128 row kernel (LDS-DMA staging): 1-, 2- and many-step
+                                       # column runs, both G dtypes, K split
+                                       (384, 128, 128, torch.bfloat16), (256, 160, 128, torch.float32),
+                                       (1152, 640, 128, torch.bfloat16), (1280, 1024, 128, torch.float32),
+                                       (384, 1280, 128, torch.bfloat16), (128, 768, 128, torch.bfloat16),
+                                       (128, 640, 128, torch.bfloat16), (2048, 384, 128, torch.bfloat16)])
 def test_deferred_ef_pass_a_matches_eager_and_fp64(m, n, r, gdt):
     """dion_project_p_ef == (dion_ef_apply on M, then dion_project_p), and both == fp64 math."""
     from megatron_dion_amd.codec import HipDionCodec
