@@ -2713,8 +2713,6 @@ constexpr int kPD8 = 1;
 // r = 128 fused pass A row kernel: 1 = rowproj_efgl_kernel (M/G and the splits by LDS-DMA;
 // bf16 or no G, an even number of 128-row blocks), 0 = rowproj_efh3_kernel everywhere
 constexpr int kPaGl8 = 1;
-// rowproj_efgl_kernel's EF product: 1 = the three h3 terms in separate accumulators
-constexpr int kGlEf3 = 0;
 // blocks per CU the r = 128 transposed fused pass A is compiled for
 // transposed pass-A kernel (colproj_efh3_kernel) at r <= 64: 1 = the two-step SA/SB register
 // ring (234 VGPRs, 2 waves per SIMD; it spills at 3), 0 = no ring, the step's M/G loads
@@ -3286,39 +3284,15 @@ __global__ void __launch_bounds__(512, 1) rowproj_efgl_kernel(const EfProjArgs e
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         f32x4 ev[KR];
-        if constexpr (kGlEf3) {
-          // the three products in separate accumulators: 6 independent MFMA chains of depth
-          // KK instead of 2 of depth 3 KK, summed once (hi*hi last, as in mfma3h)
-          f32x4 e3[3][KR];
 #pragma unroll
-          for (int u = 0; u < 3; ++u)
+        for (int rb = 0; rb < KR; ++rb) ev[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int rb = 0; rb < KR; ++rb) e3[u][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kk = 0; kk < KK; ++kk) {
+          Split2h A;
+          A.hi = rsc[((c * KK + kk) * 2 + 0) * 64 + lane];
+          A.lo = rsc[((c * KK + kk) * 2 + 1) * 64 + lane];
 #pragma unroll
-          for (int kk = 0; kk < KK; ++kk) {
-            Split2h A;
-            A.hi = rsc[((c * KK + kk) * 2 + 0) * 64 + lane];
-            A.lo = rsc[((c * KK + kk) * 2 + 1) * 64 + lane];
-#pragma unroll
-            for (int rb = 0; rb < KR; ++rb) {
-              e3[0][rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A.lo, F[rb][kk].hi, e3[0][rb], 0, 0, 0);
-              e3[1][rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A.hi, F[rb][kk].lo, e3[1][rb], 0, 0, 0);
-              e3[2][rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A.hi, F[rb][kk].hi, e3[2][rb], 0, 0, 0);
-            }
-          }
-#pragma unroll
-          for (int rb = 0; rb < KR; ++rb) ev[rb] = (e3[0][rb] + e3[1][rb]) + e3[2][rb];
-        } else {
-#pragma unroll
-          for (int rb = 0; rb < KR; ++rb) ev[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int kk = 0; kk < KK; ++kk) {
-            Split2h A;
-            A.hi = rsc[((c * KK + kk) * 2 + 0) * 64 + lane];
-            A.lo = rsc[((c * KK + kk) * 2 + 1) * 64 + lane];
-#pragma unroll
-            for (int rb = 0; rb < KR; ++rb) ev[rb] = mfma3h(A, F[rb][kk], ev[rb]);
-          }
+          for (int rb = 0; rb < KR; ++rb) ev[rb] = mfma3h(A, F[rb][kk], ev[rb]);
         }
 #pragma unroll
         for (int rb = 0; rb < KR; ++rb)
