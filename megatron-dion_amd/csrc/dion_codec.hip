@@ -90,6 +90,35 @@ __device__ __forceinline__ void st_stream(T* p, const T& v) {
   else *p = v;
 }
 
+// ---- LDS-DMA staging (global_load_lds_dwordx4).  Lane l's 16 source bytes land at LDS
+// byte lds_base + 16 l (lds_base wave-uniform, in M0).  Written as inline asm so that hipcc
+// neither counts these loads in its own s_waitcnt bookkeeping nor drains them at a barrier
+// or before an LDS read (with the builtin it waits vmcnt(0) before every ds_read of an LDS
+// array it cannot tell apart from the DMA's target); completion is counted by hand
+// (gl_wait_barrier).  Vector-memory operations retire in issue order on gfx9 (loads and
+// stores share vmcnt), which the counts below rely on.
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)p));
+}
+template <bool NT>
+__device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_t lds_base) {
+  // saddr form: wave-uniform 64-bit base in SGPRs, the lane's 32-bit byte offset in a VGPR
+  unsigned keep;
+  if constexpr (NT)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_base) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_base) : "memory");
+}
+// wait until at most N of this wave's vector-memory operations are outstanding and its LDS
+// operations are done, then the block barrier (the "memory" clobber keeps hipcc's LDS
+// accesses on their side of it)
+template <int N>
+__device__ __forceinline__ void gl_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
 // ----------------------------------------------------------------------------- errors
 static thread_local char g_err[512];
 
@@ -3104,35 +3133,6 @@ __global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : (RB >= 8 ? 8 / NW : kPa
     const uint32_t mb = __float_as_uint(mx);
     if (nz && lane == 0) atomicMax(&a.nonzero[b], mb > 1u ? mb : 1u);
   }
-}
-
-// ---- LDS-DMA staging (global_load_lds_dwordx4).  Lane l's 16 source bytes land at LDS
-// byte lds_base + 16 l (lds_base wave-uniform, in M0).  Written as inline asm so that hipcc
-// neither counts these loads in its own s_waitcnt bookkeeping nor drains them at a barrier
-// or before an LDS read (with the builtin it waits vmcnt(0) before every ds_read of an LDS
-// array it cannot tell apart from the DMA's target); completion is counted by hand
-// (gl_wait_barrier).  Vector-memory operations retire in issue order on gfx9 (loads and
-// stores share vmcnt), which the counts below rely on.
-__device__ __forceinline__ uint32_t lds_off(const void* p) {
-  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)p));
-}
-template <bool NT>
-__device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_t lds_base) {
-  // saddr form: wave-uniform 64-bit base in SGPRs, the lane's 32-bit byte offset in a VGPR
-  unsigned keep;
-  if constexpr (NT)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_base) : "memory");
-  else
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_base) : "memory");
-}
-// wait until at most N of this wave's vector-memory operations are outstanding and its LDS
-// operations are done, then the block barrier (the "memory" clobber keeps hipcc's LDS
-// accesses on their side of it)
-template <int N>
-__device__ __forceinline__ void gl_wait_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
 }
 
 // ---- pass A, not transposed, r = 128, with LDS-DMA staging: rowproj_efh3_kernel's

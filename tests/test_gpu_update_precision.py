@@ -67,6 +67,11 @@ CASES = [
     (4096, 4096, 64, False, 0.128, 0.02),
     (4096, 14336, 64, True, 0.24, 0.0),
     (14336, 4096, 128, False, 0.24, 0.02),
+    # r = 128 LDS-DMA update (columns a multiple of 256): a 5-step and a 1-strip-block run; and
+    # the register-staged kernel it falls back to (416 columns)
+    (160, 768, 128, False, 0.5, 0.02),
+    (2048, 256, 128, False, 0.3, 0.02),
+    (512, 416, 128, False, 0.5, 0.02),
 ]
 
 
