@@ -2742,6 +2742,7 @@ constexpr int kPD8 = 1;
 // r = 128 fused pass A row kernel: 1 = rowproj_efgl_kernel (M/G and the splits by LDS-DMA;
 // bf16 or no G, an even number of 128-row blocks), 0 = rowproj_efh3_kernel everywhere
 constexpr int kPaGl8 = 1;
+constexpr int kPaGlMinRB = 8;  // the smallest rank block (r = 16 RB) that takes it (r = 64 measured slower)
 // blocks per CU the r = 128 transposed fused pass A is compiled for
 // transposed pass-A kernel (colproj_efh3_kernel) at r <= 64: 1 = the two-step SA/SB register
 // ring (234 VGPRs, 2 waves per SIMD; it spills at 3), 0 = no ring, the step's M/G loads
@@ -3147,9 +3148,9 @@ __global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : (RB >= 8 ? 8 / NW : kPa
 // 2 x (16 + 16) KB of splits + 8 waves x 2 slots x 6 KB = 160 KB.  Per wave and step: 4
 // LDS-DMA loads of the splits, 4 of M, 2 of G (bf16), 4 stores; the wait before each
 // step's barrier leaves the newest M/G step and the stores in flight.
-template <int GDT>
+template <int RB, int GDT>
 __global__ void __launch_bounds__(512, 1) rowproj_efgl_kernel(const EfProjArgs e) {
-  constexpr int RB = 8, R = 128, KK = 4, KR = 2, NW = 8;
+  constexpr int R = 16 * RB, KK = RB / 2, KR = 2, NW = 8;
   constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;  // f16x8 units of one step's splits
   constexpr int GCH = GDT == DION_DTYPE_BF16 ? 4 : 0;    // 16-B chunks per G row
   constexpr int NGI = 32 * GCH / 64;
@@ -3584,9 +3585,9 @@ __global__ void __launch_bounds__(256, (RB >= 8 || kCpeRing) ? 2 : 3) colproj_ef
 // the slots and splits staged as in rowproj_efgl_kernel (M/G two steps ahead, splits one).
 //   M slot: 32 rows x 128 B (row-major, as in HBM), G slot (bf16): 32 rows x 64 B.
 // Per wave and step: 4 LDS-DMA loads of the splits, 4 of M, 2 of G (bf16), 8 stores.
-template <int GDT>
+template <int RB, int GDT>
 __global__ void __launch_bounds__(512, 1) colproj_efgl_kernel(const EfProjArgs e) {
-  constexpr int RB = 8, R = 128, KK = 4, NW = 8;
+  constexpr int R = 16 * RB, KK = RB / 2, NW = 8;
   constexpr int NQ = RB * 2 * 64, NR = 2 * KK * 2 * 64;
   constexpr int NGI = GDT == DION_DTYPE_BF16 ? 2 : 0;
   constexpr int NMG = 4 + NGI;
@@ -4928,13 +4929,13 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
       return dispatch_gdt(d->g_dtype, [&](auto Gc) {
         constexpr int GD = decltype(Gc)::value;
         if (tr) {
-          if (RB >= 8 && GD != DION_DTYPE_F32 && kPaGl8 && geo.gx % 2 == 0)  // r = 128: LDS-DMA staging
-            hipLaunchKernelGGL((colproj_efgl_kernel<GD == DION_DTYPE_F32 ? DION_DTYPE_NONE : GD>),
+          if (RB >= kPaGlMinRB && GD != DION_DTYPE_F32 && kPaGl8 && geo.gx % 2 == 0)  // LDS-DMA staging
+            hipLaunchKernelGGL((colproj_efgl_kernel<(RB >= kPaGlMinRB ? RB : kPaGlMinRB), GD == DION_DTYPE_F32 ? DION_DTYPE_NONE : GD>),
                                dim3(geo.gx / 2, geo.nchunk, nb), dim3(512), 0, st, e);
           else
             hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
-        } else if (RB >= 8 && GD != DION_DTYPE_F32 && kPaGl8 && geo.gx % 2 == 0)  // r = 128: LDS-DMA staging
-          hipLaunchKernelGGL((rowproj_efgl_kernel<GD == DION_DTYPE_F32 ? DION_DTYPE_NONE : GD>),
+        } else if (RB >= kPaGlMinRB && GD != DION_DTYPE_F32 && kPaGl8 && geo.gx % 2 == 0)  // LDS-DMA staging
+          hipLaunchKernelGGL((rowproj_efgl_kernel<(RB >= kPaGlMinRB ? RB : kPaGlMinRB), GD == DION_DTYPE_F32 ? DION_DTYPE_NONE : GD>),
                              dim3(geo.gx / 2, geo.nchunk, nb), dim3(512), 0, st, e);
         else  // r = 128 without it: one-step pipeline (register budget)
           hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, RB >= 8 ? kPD8 : kPaPD, RB >= 8 ? kKR8 : kRBE, RB >= 8 ? kNW8 : kPaNW>),
