@@ -291,9 +291,9 @@ def kernel_names(r):
         out[("project_r", False)] = (f"colproj_h3_kernel<{rb}, 4, 2>", 1)
     if r > 64 and ("project_p_ef", False) in out:
         # r = 128: the LDS-DMA row kernel (bf16 G, rows a multiple of 256: every bench set)
-        out[("project_p_ef", False)] = ("rowproj_efgl_kernel<2>", 1)
+        out[("project_p_ef", False)] = ("rowproj_efgl_kernel<8, 2>", 1)
     if r > 64 and ("project_p_ef", True) in out:
-        out[("project_p_ef", True)] = ("colproj_efgl_kernel<2>", 1)
+        out[("project_p_ef", True)] = ("colproj_efgl_kernel<8, 2>", 1)
     if r > 64:
         # r = 128: the weight update keeps one X tile in flight (kRankD8)
         out = {k: (name.replace(f"rank_stream_kernel<{rb}, false, 8, 2", f"rank_stream_kernel<{rb}, false, 8, 1"), n)
