@@ -2729,8 +2729,9 @@ __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a)
 // pre-split P is the A operand (A[row j = 16 cb + t'][k]), one scale per matrix.  Each
 // step's product lands in a fresh accumulator D[j][col] (lane (t, g): R rows CT t + c,
 // r columns 16 cb + 4 g + q) and is added as acc += D / s_col.
-// the r = 128 fused pass A row kernel: 32-row waves in 4-wave blocks, one-step pipeline (324
-// VGPRs with the EF operand: one wave per SIMD).  Measured slower: 16-row waves in 4-wave
+// the r = 128 fused pass A row kernel without LDS-DMA (fp32 G, odd 128-row block counts; bf16
+// G takes rowproj_efgl_kernel): 32-row waves in 4-wave blocks, one-step pipeline (242-256
+// VGPRs, two waves per SIMD, no tile in flight).  Measured slower: 16-row waves in 4-wave
 // blocks with a prefetch stage (5.33 vs 4.60 ms, round 2: twice the staging traffic), and
 // 16-row waves in 8-wave blocks (184 VGPRs, two waves per SIMD, the same 128 rows per staged
 // step: 5.84 vs 4.79 ms, round 3) -- each wave reads the whole staged Q and R' splits (32 KB
