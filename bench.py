@@ -183,6 +183,12 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense BF16/FP16, MI355X_MICROARCH.md
 MFMA_F32_PEAK_TFLOPS = 157.3
 MFMA_WORK = (("rowproj_efh3_kernel", 2 * 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_efh3_kernel", 2 * 2 * 3, MFMA_BF16_PEAK_TFLOPS),
+             ("rowproj_efgl_kernel", 2 * 2 * 3, MFMA_BF16_PEAK_TFLOPS),  # r = 128 LDS-DMA pass A (same products)
+             ("colproj_efgl_kernel", 2 * 2 * 3, MFMA_BF16_PEAK_TFLOPS),
+             ("b16_row_ef_kernel", 2 * 2, MFMA_BF16_PEAK_TFLOPS),        # bf16 state: EF + projection
+             ("b16_col_ef_kernel", 2 * 2, MFMA_BF16_PEAK_TFLOPS),
+             ("b16_row_kernel", 2, MFMA_BF16_PEAK_TFLOPS),
+             ("b16_col_kernel", 2, MFMA_BF16_PEAK_TFLOPS),
              ("rowproj_h3_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_h3_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_x6_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
@@ -448,7 +454,8 @@ def main():
         f"grad GiB/s/GPU (device-resident) Dion-compressed, {config_name}"
     out = {"metric": metric, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32 state, fp16x3-split MFMA, fp32 accumulate",
            "value_per_gpu": round(value / world, 2),
            "value_definition": "value = aggregate bf16-grad GiB/s of all ranks (bench contract); "
                                "value_per_gpu = value / n_gpus (the metric's per-GPU figure)",
@@ -460,7 +467,7 @@ def main():
                       else "dp1"},
            "roofline": roofline}
     if bf16_state:
-        out["dtype"] = "bf16 state (f32 accumulate)"
+        out["dtype"] = "bf16 state, bf16 MFMA, fp32 accumulate"
     if args.simulate_world > 1:
         out["simulated_world"] = args.simulate_world
         out["metric"] = "SIMULATED (loopback collectives, not a bench line): " + metric

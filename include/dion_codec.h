@@ -43,7 +43,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 12
+#define DION_ABI_VERSION 13
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -80,6 +80,12 @@ typedef struct DionBatchDesc {
 
 /* ABI version of the loaded library (== DION_ABI_VERSION). */
 int dion_abi_version(void);
+
+/* Build id: the first 16 hex digits of the SHA-256 of the sources the library was compiled
+ * from (csrc/dion_codec.hip, csrc/*.hpp, include/dion_codec.h; name + bytes, sorted by name),
+ * passed by the build as -DDION_BUILD_ID.  The loader recomputes it from the in-tree sources
+ * and refuses a library built from other sources.  No reference counterpart (build hygiene). */
+const char* dion_build_id(void);
 
 /* Text of the last error raised on this thread ("" if none). */
 const char* dion_last_error(void);
@@ -132,8 +138,11 @@ int dion_project_p_ef(const DionBatchDesc* desc, const void* const* G, float* co
  *   with S ~ N(0, 1/k), k = ceil(oversample r / 128) * 128.
  * `sketch` (batch x k x m_P fp32, row-major) is used when non-null (parity
  * tests); otherwise S is generated on the fly from (seed, b, row, col) by a
- * counter-based Gaussian generator (the reference draws an unseeded sketch,
- * ortho.py:659-661; results are sketch-invariant up to column signs).
+ * counter-based hash as a Rademacher matrix, entries +-1/sqrt(k) (exact in bf16),
+ * in place of the reference's unseeded N(0, 1/k) draw (ortho.py:643-662): the
+ * orthonormalised P is the Q factor of P whatever the sketch, up to column signs
+ * (tests/test_gpu_fullsize.py compares the generated path with the oracle's
+ * Gaussian-sketch step at bench shapes).
  */
 int dion_orthonormalize(const DionBatchDesc* desc, float* P, const float* sketch,
                         uint64_t seed, float oversample, void* ws, size_t ws_bytes,

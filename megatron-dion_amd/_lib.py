@@ -7,6 +7,7 @@ or stale library raises `DionLibraryError` at first use.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 import sys
 
@@ -32,7 +33,31 @@ def _lib_path() -> str:
 
 
 LIB_PATH = _lib_path()
-ABI_VERSION = 12
+SOURCES = (os.path.join(HERE, "csrc"), os.path.join(os.path.dirname(HERE), "include"))
+
+
+def source_build_id(roots=SOURCES) -> str | None:
+    """SHA-256 (16 hex digits) over the codec's sources: csrc/dion_codec.hip, csrc/*.hpp and
+    include/dion_codec.h, by file name then bytes, sorted by name.  __graft_entry__.build()
+    compiles it in as DION_BUILD_ID; load() compares.  None when the sources are absent."""
+    files = []
+    for root in roots:
+        if not os.path.isdir(root):
+            continue
+        for name in os.listdir(root):
+            if name == "dion_codec.hip" or name.endswith(".hpp") or name == "dion_codec.h":
+                files.append((name, os.path.join(root, name)))
+    if not any(n == "dion_codec.hip" for n, _ in files):
+        return None
+    h = hashlib.sha256()
+    for name, path in sorted(files):
+        h.update(name.encode())
+        h.update(b"\0")
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+ABI_VERSION = 13
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -56,6 +81,7 @@ OP_DORTHO = 8
 # every symbol include/dion_codec.h declares
 EXPORTED = (
     "dion_abi_version",
+    "dion_build_id",
     "dion_last_error",
     "dion_workspace_bytes",
     "dion_project_p",
@@ -79,7 +105,13 @@ EXPORTED = (
 
 
 class DionLibraryError(RuntimeError):
-    pass
+    """A failed C-ABI call; `code` is its DION_E_* return code."""
+    code = None
+
+
+class DionUnsupportedError(DionLibraryError):
+    """DION_E_UNSUPPORTED: the call refused the shape / layout before enqueuing any work
+    (include/dion_codec.h), so the caller may take another path."""
 
 
 class DionBatchDesc(ctypes.Structure):
@@ -109,6 +141,7 @@ _DESC = ctypes.POINTER(DionBatchDesc)
 
 _SIGNATURES = {
     "dion_abi_version": ([], ctypes.c_int),
+    "dion_build_id": ([], ctypes.c_char_p),
     "dion_last_error": ([], ctypes.c_char_p),
     "dion_workspace_bytes": ([_DESC, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "dion_project_p": ([_DESC, _PP, _PP, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
@@ -158,6 +191,12 @@ def load(path: str = LIB_PATH):
     ver = lib.dion_abi_version()
     if ver != ABI_VERSION:
         raise DionLibraryError(f"[DION_HIP_ABI_MISMATCH] library ABI {ver}, expected {ABI_VERSION}")
+    want = source_build_id()
+    got = lib.dion_build_id().decode("ascii", "replace")
+    if path == DEFAULT_LIB_PATH and want is not None and got != want:
+        raise DionLibraryError(
+            f"[DION_HIP_LIBRARY_STALE] {path} was built from sources {got}, the tree holds {want}; rebuild it "
+            "with `python __graft_entry__.py`")
     if path == LIB_PATH:
         _lib = lib
     return lib
@@ -166,4 +205,7 @@ def load(path: str = LIB_PATH):
 def check(rc: int, what: str) -> None:
     if rc != DION_OK:
         msg = load().dion_last_error().decode("utf-8", "replace")
-        raise DionLibraryError(f"[DION_HIP_ERROR] {what} failed ({rc}): {msg}")
+        cls = DionUnsupportedError if rc == DION_E_UNSUPPORTED else DionLibraryError
+        err = cls(f"[DION_HIP_ERROR] {what} failed ({rc}): {msg}")
+        err.code = rc
+        raise err

@@ -233,3 +233,54 @@ def verify_schedule_across_ranks(batches: Sequence[DionBatch], group) -> None:
     dist.all_gather_object(gathered, mine, group=group)
     if any(g != mine for g in gathered):
         raise RuntimeError("[DION_BATCH_KEY_MULTIPLICITY_MISMATCH] ranks built different Dion batch schedules")
+
+
+def _sync_groups_of(batch: DionBatch) -> List[object]:
+    """The process groups whose members must agree on this batch's place in the schedule: its
+    sync groups (resolve_batch_group, batches.py:519-551: the replicate group under low-rank
+    sync, the TP group, the FS group)."""
+    out = []
+    for g in tuple(getattr(batch.batch_group, "sync_groups", ()) or ()):
+        if g is not None and dist.get_world_size(g) > 1 and all(g is not x for x in out):
+            out.append(g)
+    return out
+
+
+def _collective_signature(batch: DionBatch) -> tuple:
+    """What a batch's collectives look like to the other members of its groups: the kind, the
+    batch / real sizes, the matrices' global shape, the global rank r and the orientation (the
+    P / R / Q buffers' sizes follow from them).  Local shapes, local Q columns (TP) and group
+    handles differ between the members of an FS or TP group, so the batch key itself is not
+    comparable across ranks."""
+    e = batch.entries[0]
+    st = e.optimizer_state or {}
+    gshape = st.get("per_expert_global_shape") or st.get("global_shape") or \
+        getattr(e.dist_meta, "global_shape", None) or e.param_shape
+    return (str(getattr(batch.batch_group, "kernel_kind", "ddp")), len(batch.entries), int(batch.real_batch_size),
+            tuple(int(d) for d in gshape), int(st.get("r", -1)), bool(e.config.is_transposed))
+
+
+def verify_sync_group_order(batches: Sequence[DionBatch]) -> None:
+    """Every member of a process group must issue that group's collectives in the same order
+    (batches.py:855-884 _sync_group_batch_metadata agrees on the order with an all_gather).  The
+    local listing above is canonical for whole-group batches; a split child owned by part of its
+    row group (split.split_child_layouts) gives the members of one parent group different key
+    sets, so the order is checked once: per group, in one global order of groups (sorted member
+    ranks, so the checks cannot wait on each other), all_gather the sequence of batch
+    signatures (`_collective_signature`) this rank will issue on it and compare."""
+    seqs: Dict[tuple, list] = {}
+    handle: Dict[tuple, object] = {}
+    for b in batches:
+        for g in _sync_groups_of(b):
+            ranks = tuple(int(r) for r in dist.get_process_group_ranks(g))
+            handle.setdefault(ranks, g)
+            seqs.setdefault(ranks, []).append(_collective_signature(b))
+    for ranks in sorted(seqs):
+        g, mine = handle[ranks], seqs[ranks]
+        gathered: List = [None] * dist.get_world_size(g)
+        dist.all_gather_object(gathered, mine, group=g)
+        if any(x != mine for x in gathered):
+            bad = [ranks[i] for i, x in enumerate(gathered) if x != mine]
+            raise RuntimeError(f"[DION_SYNC_GROUP_ORDER_MISMATCH] group ranks={ranks}: ranks {bad} issue another "
+                               f"batch order ({len(mine)} batches here)")
+

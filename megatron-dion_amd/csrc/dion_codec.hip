@@ -4650,6 +4650,11 @@ extern "C" {
 
 int dion_abi_version(void) { return DION_ABI_VERSION; }
 
+#ifndef DION_BUILD_ID
+#define DION_BUILD_ID "unknown"
+#endif
+const char* dion_build_id(void) { return DION_BUILD_ID; }
+
 const char* dion_last_error(void) { return g_err; }
 
 int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
@@ -4815,7 +4820,29 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
   const int mp = tr ? d->n : d->m;
   const long ld_m = ldv(d->ld_m, d->n), ld_g = ldv(d->ld_g, d->n);
   if (d->m_dtype == DION_DTYPE_BF16) {
-    // bf16 momentum / Q: M = rne(M + rne(alpha rne(P' R'^T))), M = rne(M + rne(G)), P = rne(X Q)
+    // bf16 momentum / Q: M = rne(M + rne(alpha rne(P' R'^T))), M = rne(M + rne(G)), P = rne(X Q).
+    // Every entry is checked before the first launch (as the fp32 branch below does): the
+    // fused kernels need the whole-line layout (16-byte aligned M / G / factors, ld % 8), so
+    // an UNSUPPORTED return has enqueued nothing and the caller can still run the eager path.
+    if (!b16::ef_ok(!tr, d->m, d->n, d->r, d->g_dtype) || ld_m % 8 != 0 ||
+        (d->g_dtype != DION_DTYPE_NONE && ld_g % 8 != 0))
+      return fail(DION_E_UNSUPPORTED, "no deferred-EF bf16 pass A for %dx%d r=%d ld_m=%ld ld_g=%ld", d->m, d->n,
+                  d->r, ld_m, ld_g);
+    for (int b = 0; b < d->batch; ++b) {
+      if (M[b] == nullptr || Q[b] == nullptr || (d->g_dtype != DION_DTYPE_NONE && G[b] == nullptr))
+        return fail(DION_E_INVALID, "null matrix pointer at entry %d", b);
+      if ((ef->P[b] == nullptr) != (ef->R[b] == nullptr))
+        return fail(DION_E_INVALID, "pending EF of entry %d has only one factor", b);
+      if (!aligned16(M[b]) || (d->g_dtype != DION_DTYPE_NONE && !aligned16(G[b])) ||
+          (ef->P[b] && (!aligned16(ef->P[b]) || !aligned16(ef->R[b]))))
+        return fail(DION_E_UNSUPPORTED, "deferred-EF bf16 pass A needs 16-byte aligned operands (entry %d)", b);
+    }
+    {
+      const int nb0 = d->batch < MAXB ? d->batch : MAXB;  // the largest chunk sizes the workspace
+      const size_t need = b16::proj_ws(d->m, d->n, d->r, nb0, !tr, true);
+      if (ws == nullptr || ws_bytes < need)
+        return fail(DION_E_WORKSPACE, "bf16 projection needs %zu workspace bytes, got %zu", need, ws_bytes);
+    }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
       const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;

@@ -28,7 +28,7 @@ import torch
 import torch.distributed as dist
 from torch.optim.optimizer import Optimizer
 
-from .batches import build_dion_batches
+from .batches import build_dion_batches, verify_sync_group_order
 from .runtime import (AsyncRuntime, DionStateMap, coalesce_local_batches, coalesce_replicated_batches,
                       drop_pending_error_feedback, flush_pending_error_feedback, is_replicated,
                       run_dion_batch_async)
@@ -363,10 +363,13 @@ class MegatronDion(Optimizer):
         self._dion_in_step = True
         try:
             self._step_batches(profile, t0)
+        except BaseException:
+            self._phase_records = None  # a failed step reports nothing (its events may never complete)
+            raise
         finally:
             self._dion_in_step = False
-            if profile:
-                self._report_profile(t0)
+        if profile:
+            self._report_profile(t0)
         return loss
 
     # phases the fused kernels fold into another phase's record (PhaseClock)
@@ -454,7 +457,21 @@ def is_dion_param(param: torch.Tensor, name: str = "") -> bool:
     return not any(k in name for k in ("embedding", "output_layer", "lm_head"))
 
 
+# owner groups of split children, by global ranks; valid for one default process group only
 _CHILD_ROW_GROUPS: Dict[Tuple[int, ...], object] = {}
+_CHILD_ROW_GROUPS_WORLD: List[object] = [None]
+
+
+def _child_group_cache() -> Dict[Tuple[int, ...], object]:
+    """The owner-group cache of the current default process group.  After
+    destroy_process_group() and a new init_process_group() the cached handles belong to the
+    destroyed world, and a rank that still held them would skip the new_group calls its peers
+    make (unmatched collective group creation): a new WORLD starts an empty cache."""
+    world = dist.group.WORLD if dist.is_initialized() else None
+    if _CHILD_ROW_GROUPS_WORLD[0] is not world:
+        _CHILD_ROW_GROUPS.clear()
+        _CHILD_ROW_GROUPS_WORLD[0] = world
+    return _CHILD_ROW_GROUPS
 
 
 def _child_ranks(parent_group, members: Sequence[int]) -> Tuple[int, ...]:
@@ -474,9 +491,10 @@ def _prepare_child_row_groups(needed: Sequence[Tuple[int, ...]]) -> None:
         every = [None] * dist.get_world_size()
         dist.all_gather_object(every, want)
         want = sorted(set(t for lst in every for t in lst))
+    cache = _child_group_cache()
     for ranks in want:
-        if ranks not in _CHILD_ROW_GROUPS:
-            _CHILD_ROW_GROUPS[ranks] = dist.new_group(list(ranks))
+        if ranks not in cache:
+            cache[ranks] = dist.new_group(list(ranks))
 
 
 def _child_row_group(parent_group, members: Sequence[int]):
@@ -484,9 +502,10 @@ def _child_row_group(parent_group, members: Sequence[int]):
     child = _child_ranks(parent_group, members)
     if len(child) <= 1:
         return None
-    if child not in _CHILD_ROW_GROUPS:
+    cache = _child_group_cache()
+    if child not in cache:
         raise RuntimeError(f"[DION_SPLIT_CHILD_GROUP_NOT_PREPARED] ranks={child}")
-    return _CHILD_ROW_GROUPS[child]
+    return cache[child]
 
 
 def _row_axis_group(spec, tspec, fs_group, tp_group, fs_world: int, tp_world: int):
@@ -661,6 +680,8 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
         g = getattr(p, "main_grad", None)
         return p.grad if g is None else g
 
+    checked = [False]
+
     def route():
         steps = []
         for name, p in ordered:
@@ -691,6 +712,10 @@ def attach_dp_routing(optimizer: MegatronDion, named_params: Sequence[Tuple[str,
             group_size=lambda g: dist.get_world_size(g),
             resolve_fs_group_from_meta=lambda meta, expect_group=True: meta.extra.get("fs_group"),
             resolve_tp_group=lambda meta, expect_group=True: meta.extra.get("tp_group"))
+        if not checked[0]:
+            # once: the members of every sync group issue its collectives in one order
+            verify_sync_group_order(batches)
+            checked[0] = True
         elementwise = []
         for _, p in ew_named:
             g = grad_of(p)

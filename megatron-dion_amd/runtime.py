@@ -23,6 +23,7 @@ from typing import Callable, Generator, Iterable, List, Optional
 import torch
 import torch.distributed as dist
 
+from ._lib import DionUnsupportedError
 from .codec import factor_rows
 from .dense_grad_cache import consume_if_reduced
 from .kernels import scaled_lr_for_shape
@@ -192,8 +193,10 @@ def check_supported_batch(optimizer, *, batch_group, batch_collectives, configs,
     (types.py:149-158) and a q_norm / ortho group.  Treating those shards as whole matrices
     would orthonormalise and normalise a local piece while scaling the LR by the global
     shape: wrong updates with no error.  Computed here: the whole-matrix data-parallel kind
-    ("ddp", runtime.py:1379-1496) and the FS kind without TP ("fsdp", runtime.py:1201-1293,
-    1729-1795); anything else (TP-sharded P / Q, "fsdp_tp") raises
+    ("ddp", runtime.py:1379-1496), the FS kind ("fsdp", runtime.py:1201-1293, 1729-1795) and the
+    TP kind with TP on the P-row side and FS, if any, on the contraction side ("fsdp_tp",
+    runtime.py:680-962, 1328-1377); anything else (another kind, TP on the contraction side, P
+    sharded on both axes, a batch without the collectives its kind needs) raises
     [DION_UNSUPPORTED_KERNEL_KIND]."""
     def world(g):
         try:
@@ -376,20 +379,8 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
              and codec.supports_deferred_ef(m, n, r, transposed, state_dtype=momentums[0].dtype,
                                            grad_dtype=real_grads[0].dtype if real_grads else None))
     clock = PhaseClock(optimizer, dev, _batch_desc(batch_group, dist_metas, real, (m, n)))
-    pending = [_take_pending(optimizer_states[i]) for i in range(real)]
-    if any(p is not None for p in pending):
-        alphas = {p[2] for p in pending if p is not None}
-        if defer and len(alphas) == 1:
-            codec.project_p_ef(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed,
-                               [p[0] if p is not None else None for p in pending],
-                               [p[1] if p is not None else None for p in pending], alphas.pop())
-        else:
-            for i, p in enumerate(pending):
-                if p is not None:
-                    _apply_pending(codec, momentums[i], Qs[i], p, m, n, transposed)
-            codec.project_p(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed)
-    else:
-        codec.project_p(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed)
+    _project_with_pending(codec, real_grads, momentums, Qs, P, nonzero, optimizer_states, real, m, n, transposed,
+                          defer)
     clock.mark("p_matmul")
 
     def ortho(P_slice, entry):
@@ -515,7 +506,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     optimizer._last_batch_factors = (P, R) if getattr(optimizer, "_keep_factors", False) else None
     sink = getattr(optimizer, "_factor_sink", None)
     if sink is not None:  # the compressed factors leaving the device (scripts/e2e_pcie.py)
-        sink(P[:real], R[:real])
+        sink(P[:real], R[:real], list(params[:real]))
 
 
 def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, optim_groups, real_grads,
@@ -881,10 +872,15 @@ def _project_with_pending(codec, real_grads, momentums, Qs, P, nonzero, optimize
     if any(p is not None for p in pending):
         alphas = {p[2] for p in pending if p is not None}
         if defer and len(alphas) == 1:
-            codec.project_p_ef(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero, transposed,
-                               [p[0] if p is not None else None for p in pending],
-                               [p[1] if p is not None else None for p in pending], alphas.pop())
-            return
+            try:
+                codec.project_p_ef(real_grads or None, list(momentums[:real]), list(Qs[:real]), P, nonzero,
+                                   transposed, [p[0] if p is not None else None for p in pending],
+                                   [p[1] if p is not None else None for p in pending], alphas.pop())
+                return
+            except DionUnsupportedError:
+                # refused before any launch (e.g. a momentum or gradient view whose layout the
+                # fused kernel cannot stream): the popped error feedback goes on eagerly
+                pass
         for i, p in enumerate(pending):
             if p is not None:
                 _apply_pending(codec, momentums[i], Qs[i], p, m, n, transposed)
@@ -923,7 +919,7 @@ def _apply_updates(optimizer, codec, params, momentums, Qs, P, R, nonzero, optim
     optimizer._last_batch_factors = (P, R) if getattr(optimizer, "_keep_factors", False) else None
     sink = getattr(optimizer, "_factor_sink", None)
     if sink is not None:
-        sink(P[:real], R[:real])
+        sink(P[:real], R[:real], list(params[:real]))
 
 
 # optimizer-state key of a pending (deferred) error feedback: (P_b, R_b, alpha, M ref,

@@ -45,7 +45,7 @@ def main():
     host_f = {}
     calls = [0]
 
-    def sink(P, R):
+    def sink(P, R, params=None):
         k = calls[0]
         calls[0] += 1
         if k not in host_f:

@@ -128,6 +128,19 @@ CASES = [
         m_dtype="bfloat16",
         q_dtype="float32",
     ),
+    # world size 4 (BASELINE config 4's replicated schedule at W > 2): one full batch of
+    # four 64x40 matrices and one padded batch of three transposed 40x72 ones (entry c W + r
+    # owned by rank r, a zero padded entry on rank 3).  Each shape forms a single batch, so
+    # the reference's shape-keyed "replicated_p_ortho_full" buffer (algorithm.py:233-244)
+    # is never shared between batches in flight and the capture is the Dion step itself.
+    dict(
+        name="c15_w4_pad_two_steps",
+        mats=[("a0", 64, 40), ("a1", 64, 40), ("a2", 64, 40), ("a3", 64, 40),
+              ("t0", 40, 72), ("t1", 40, 72), ("t2", 40, 72)],
+        r=8,
+        world=4,
+        steps=2,
+    ),
 ]
 
 HYPER = dict(lr=0.01, mu=0.95, weight_decay=0.01, epsilon=1e-8, rcqr_oversample=1.25,

@@ -212,3 +212,30 @@ def test_gloo_w2_coalesced_groups_match_per_batch(deferred):
     for key in res[0][True]:
         if key.endswith("_W") or key.endswith("_Q"):
             assert torch.equal(res[0][True][key], res[1][True][key]), key
+
+
+@pytest.mark.parametrize("deferred", [False, True], ids=["eager_ef", "deferred_ef"])
+def test_gloo_w4_matches_reference_capture(deferred):
+    """BASELINE config 4's replicated schedule beyond two ranks: the product runtime on 4 gloo
+    ranks against the reference's own 4-rank capture c15 (a full batch of 4, a padded batch of
+    3 transposed matrices whose fourth slot is rank 3's zero entry; two steps)."""
+    from tests._golden import Case
+
+    case = Case("c15_w4_pad_two_steps")
+    res = _run(case.name, world=4, deferred=deferred)
+    names = [n for n, _, _ in case.mats]
+    for rank in range(4):
+        for step in range(case.steps):
+            assert sorted(res[rank][f"s{step}_schedule"]) == [(["a0", "a1", "a2", "a3"], 4),
+                                                             (["t0", "t1", "t2", "<pad>"], 3)]
+            for n in names:
+                keys = (("W", "W1"), ("Q", "Q1"))
+                if not deferred or step == case.steps - 1:
+                    keys += (("M", "M1"),)
+                for k, ref in keys:
+                    err = _maxrel(res[rank][f"s{step}_{n}_{k}"], case.t(rank, step, f"{n}_{ref}"))
+                    assert err <= 1e-6, (rank, step, n, k, err)
+    for n in names:
+        for rank in range(1, 4):
+            assert torch.equal(res[0][f"s1_{n}_W"], res[rank][f"s1_{n}_W"])
+            assert torch.equal(res[0][f"s1_{n}_Q"], res[rank][f"s1_{n}_Q"])

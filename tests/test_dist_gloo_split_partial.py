@@ -214,3 +214,39 @@ def test_gloo_split_linear_partial_owners_match_reference(name, deferred):
 def test_hip_split_linear_partial_owners_match_reference(name, deferred):
     res = run_split_partial(name, deferred=deferred, device="cuda:0")
     check_split_partial(res, name, deferred, 2e-5)
+
+
+def _reinit_worker(rank, world, ports, out_dir):
+    import sys
+    sys.path.insert(0, os.path.dirname(HERE))
+    from megatron_dion_amd.optimizer import _child_row_group, _prepare_child_row_groups
+
+    seen = []
+    for port in ports:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        # rank 0 asks for one owner set, rank 1 for another: the union is created everywhere
+        _prepare_child_row_groups([(0, 1)] if rank == 0 else [(0, 1, 2)])
+        g = _child_row_group(dist.group.WORLD, [0, 1])
+        g3 = _child_row_group(dist.group.WORLD, [0, 1, 2])
+        t = torch.ones(1)
+        if rank < 2:
+            dist.all_reduce(t, group=g)
+        dist.all_reduce(t, group=g3)
+        seen.append((id(g), float(t.item())))
+        dist.barrier()
+        dist.destroy_process_group()
+    torch.save(seen, os.path.join(out_dir, f"rank{rank}.pt"))
+
+
+def test_child_groups_follow_a_reinitialised_world():
+    """owner groups cached across destroy_process_group() / init_process_group()
+    belonged to the old world.  init -> prepare -> destroy -> init -> prepare on 3 ranks: the
+    second world creates (and uses) new groups on every rank."""
+    world = 3
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_reinit_worker, args=(world, [_free_port(), _free_port()], tmp), nprocs=world,
+                           join=True, start_method="spawn")
+        seen = [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+    for rank in range(world):
+        (id0, v0), (id1, v1) = seen[rank]
+        assert v0 == v1 == 5.0  # (1 + 1) on {0, 1}, then 2 + 2 + 1 over {0, 1, 2}

@@ -10,8 +10,13 @@ from the same W0, Q0 and gradients with one explicit sketch per (step, matrix), 
   * the W > 1 branch without low-rank sync (dion/runtime.py:439-491, 1656-1728): dense
     gradient all-reduce, every rank orthonormalises its entries, R local;
   * Llama-3-8B fc1 (28672 x 4096) and fc2 (4096 x 14336, transposed) at W = 2, r = 64, four
-    of each, so the replicated schedule runs rank-major groups of k = 2 (the largest
-    multi-rank evidence one GPU can give for config 4).
+    of each, so the replicated schedule runs rank-major groups of k = 2;
+  * config 4's schedule at W = 4 and W = 8 (4 and 8 processes on cuda:0): the Llama shapes
+    scaled down 16x (qkv 384x256, proj 256x256, fc1 896x256, fc2 256x448 transposed; r = 16)
+    with 16 matrices per shape (>= 2 W) and the bench's coalesce_max_entries = 16, so every
+    shape runs one rank-major group of k = 16 / W full batches (position r k + c holds entry
+    c W + r), and fc1 carries 3 more matrices, a padded batch after its group; deferred EF and
+    the 3 AsyncRuntime slot streams as in bench.py.
 
 Tolerance: max |a - b| / max |b| <= 1e-5 for W, M, Q; the weight step alone
 (tests/_metrics.dw_err) <= 5e-6 of its own scale.  W and Q must also be bit-identical across
@@ -50,10 +55,10 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, shapes, r, steps, low_rank, check):
+def _worker(rank, world, port, out_dir, shapes, r, steps, low_rank, check, opt_kw=None):
     import sys
     sys.path.insert(0, ROOT)
-    torch.set_num_threads(8)
+    torch.set_num_threads(max(1, 8 // world))
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     import megatron_dion_amd as mda
     from megatron_dion_amd.optimizer import attach_dp_routing
@@ -70,7 +75,7 @@ def _worker(rank, world, port, out_dir, shapes, r, steps, low_rank, check):
                                         .to(on))) for i, (n, m, c) in enumerate(shapes)]
         kw = dict(codec=OracleCodec(deferred=True)) if backend == "oracle" else {}
         opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01,
-                               rank_fraction=r / min_side, use_low_rank_sync=low_rank, **kw)
+                               rank_fraction=r / min_side, use_low_rank_sync=low_rank, **kw, **(opt_kw or {}))
         attach_dp_routing(opt, named, replicate_group=dist.group.WORLD)
         ks = {id(p): O.sketch_rows(int(opt.state[p]["r"])) for _, p in named}  # r = rank_fraction min(m, n)
         if backend == "hip":
@@ -97,8 +102,11 @@ def _worker(rank, world, port, out_dir, shapes, r, steps, low_rank, check):
         for s in range(steps):
             cur["s"] = s
             for i, (n, p) in enumerate(named):
-                g = torch.Generator().manual_seed(100 * s + 10 * rank + i)
+                g = torch.Generator().manual_seed(1000 * s + 10 * rank + i)
                 p.main_grad = (torch.randn(p.shape, generator=g) * 1e-3).to(torch.bfloat16).to(on)
+            if s == 0:
+                res[f"{backend}_chunks"] = torch.tensor([int(getattr(b, "_chunks", 0) or 0)
+                                                         for b in opt._batches()[0]])
             opt.step()
             if s == steps - 1:
                 opt.flush_error_feedback()
@@ -119,18 +127,19 @@ def _worker(rank, world, port, out_dir, shapes, r, steps, low_rank, check):
     dist.destroy_process_group()
 
 
-def _run_and_check(shapes, r, steps, low_rank, check=None):
+def _run_and_check(shapes, r, steps, low_rank, check=None, world=2, opt_kw=None):
     """`check`: the matrices whose W / M / Q are compared (default all)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     check = set(check) if check is not None else {n for n, _, _ in shapes}
     with tempfile.TemporaryDirectory() as tmp:
-        mp.start_processes(_worker, args=(2, _port(), tmp, shapes, r, steps, low_rank, check), nprocs=2, join=True,
-                           start_method="spawn")
-        res = [torch.load(os.path.join(tmp, f"rank{q}.pt"), weights_only=True) for q in range(2)]
+        mp.start_processes(_worker, args=(world, _port(), tmp, shapes, r, steps, low_rank, check, opt_kw),
+                           nprocs=world, join=True, start_method="spawn")
+        res = [torch.load(os.path.join(tmp, f"rank{q}.pt"), weights_only=True) for q in range(world)]
     worst = {"W": 0.0, "dW": 0.0, "M": 0.0, "Q": 0.0}
-    for rank in range(2):
+    for rank in range(world):
         R = res[rank]
+        assert torch.equal(R["hip_chunks"], R["oracle_chunks"]), (R["hip_chunks"], R["oracle_chunks"])
         for key, v in R.items():
             if not key.startswith("hip_s") or key.startswith("hip_sinit"):
                 continue
@@ -147,8 +156,9 @@ def _run_and_check(shapes, r, steps, low_rank, check=None):
                 assert e <= TOL_DW, (rank, s, n, e)
     for key in res[0]:
         if key.startswith("hip_s") and not key.startswith("hip_sinit") and (key.endswith("_W") or key.endswith("_Q")):
-            assert torch.equal(res[0][key], res[1][key]), key
-    return worst
+            for q in range(1, world):
+                assert torch.equal(res[0][key], res[q][key]), (q, key)
+    return worst, res[0]["hip_chunks"].tolist()
 
 
 def test_config1_gpt125m_w2_hip_matches_oracle():
@@ -157,6 +167,29 @@ def test_config1_gpt125m_w2_hip_matches_oracle():
 
 def test_w2_dense_branch_hip_matches_oracle():
     _run_and_check(DENSE, 32, 3, low_rank=False)
+
+
+def _llama_scaled(world):
+    """The Llama-3-8B 2D shapes / 16, 16 matrices per shape (one rank-major group of 16 / W
+    full batches), fc1 with 3 more (a padded batch after its group)."""
+    out = []
+    for name, m, n, extra in (("linear_qkv", 384, 256, 0), ("linear_proj", 256, 256, 0),
+                              ("linear_fc1", 896, 256, 3), ("linear_fc2", 256, 448, 0)):
+        out += [(f"layers.{i}.{name}.weight", m, n) for i in range(16 + extra)]
+    return out
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_config4_schedule_w4_w8_hip_matches_oracle(world):
+    """Config 4's replicated schedule at W = 4 / 8 (what one GPU can run of it; RCCL needs a GPU
+    per rank): gloo ranks sharing cuda:0, HIP codec against the CPU oracle codec under the same
+    runtime, W / M / Q / dW <= the bars, W and Q bit-identical on all ranks."""
+    shapes = _llama_scaled(world)
+    worst, chunks = _run_and_check(shapes, 16, 2, low_rank=True, world=world,
+                                   opt_kw=dict(coalesce_max_entries=16))
+    k = 16 // world
+    # 3 full-size groups of k batches (qkv, proj, fc2), fc1's group + its padded batch
+    assert sorted(chunks) == sorted([k, k, k, k, 0]), chunks
 
 
 def test_w2_llama_fc1_fc2_rank_major_hip_matches_oracle():

@@ -5,7 +5,9 @@ error feedback), launch groups of up to 16 matrices (`coalesce_max_entries=16`),
 alternating HIP streams (`local_streams=2`) -- on the BASELINE configs' real shapes, and
 its W, M (after flush_error_feedback) and Q are compared with the CPU oracle
 (oracle/dion_oracle.py, pinned to the reference's golden captures) step by step, with
-explicit sketches so no sign alignment is needed:
+explicit sketches so no sign alignment is needed -- and configs 3 and 5 once more with the
+sketch generated on the device exactly as bench.py times it (Rademacher, sketch_rad_kernel)
+against the oracle's own Gaussian sketch, Q and P compared after column-sign alignment:
 
   config 2  single 4096 x 4096, r = 64
   config 3  the four Llama-3-8B 2D shapes (qkv 6144x4096, proj 4096x4096, fc1 28672x4096,
@@ -78,9 +80,23 @@ def _sketch(seed, k, mp_):
     return torch.randn(k, mp_, generator=g) * math.sqrt(1.0 / k)
 
 
-def _run_vs_oracle(label, shapes, r, steps, check=None):
+def _col_signs(a, b):
+    """D (+-1 per column) with a D ~ b: the sign of each column pair's inner product."""
+    d = (a.double() * b.double()).sum(dim=-2)
+    return torch.where(d < 0, -1.0, 1.0).to(torch.float64)
+
+
+def _run_vs_oracle(label, shapes, r, steps, check=None, generated=False):
     """shapes: list of (name, m, n).  Runs the bench-configured optimizer on the GPU and the
-    oracle on the CPU for the matrices in `check` (default: all); returns worst errors."""
+    oracle on the CPU for the matrices in `check` (default: all); returns worst errors.
+
+    generated=True runs the HIP side exactly as bench.py does: no explicit sketch, so
+    sketch_rad_kernel generates its Rademacher S (+-1/sqrt(k)) in the slab-reduced sketch
+    product, while the oracle draws its own Gaussian N(0, 1/k) sketch (the reference's
+    distribution, dion/ortho.py:643-662).  RCQR's P is the Q factor of M Q whatever the
+    sketch, up to column signs, so W, M and dW keep their bars, and Q (= R / |R|, R = M^T P)
+    and P are compared after aligning each column's sign: Q every step for every checked
+    matrix, P for the first checked matrix of each shape."""
     dev = _dev()
     check = set(check) if check is not None else {n for n, _, _ in shapes}
     k = O.sketch_rows(r)
@@ -118,8 +134,23 @@ def _run_vs_oracle(label, shapes, r, steps, check=None):
             out[i] = sk(name_of[id(bp)], m, n).to(dev)
         return out
 
-    opt._sketch_override = override
+    p_hip = {}
+    first_of_shape = {}
+    for name, p in named:
+        if name in check:
+            first_of_shape.setdefault(tuple(p.shape), name)
+    watch = {id(p): name for name, p in named if first_of_shape.get(tuple(p.shape)) == name}
+    if generated:
+        def sink(P, R, params):
+            for i, bp in enumerate(params):
+                if id(bp) in watch:
+                    p_hip[watch[id(bp)]] = P[i].detach().cpu().clone()
+        opt._factor_sink = sink
+    else:
+        opt._sketch_override = override
     worst = {"W": 0.0, "dW": 0.0, "M": 0.0, "Q": 0.0}
+    if generated:
+        worst["P"] = 0.0
     decay = 1.0 - 0.01 * 0.01
     for step in range(steps):
         cur["step"] = step
@@ -144,13 +175,21 @@ def _run_vs_oracle(label, shapes, r, steps, check=None):
                 continue
             mt = mats[name]
             st = opt.state[p]
-            errs = {"W": maxrel(p, mt.W), "Q": maxrel(st["Q"], mt.Q),
+            qh = st["Q"].detach().cpu()
+            if generated:
+                qh = qh.double() * _col_signs(qh, mt.Q)
+            errs = {"W": maxrel(p, mt.W), "Q": maxrel(qh, mt.Q),
                     "dW": dw_err(prev[name][0], p.detach().cpu(), prev[name][1], mt.W, decay)}
+            if generated and name in watch.values():
+                assert name in p_hip, f"no P of {name} reached the factor sink"
+                ph, po = p_hip.pop(name), mt.trace["P"]
+                errs["P"] = maxrel(ph.double() * _col_signs(ph, po), po)
             if step == steps - 1:
                 errs["M"] = maxrel(st["momentum"], mt.M)
             for key, v in errs.items():
                 worst[key] = max(worst[key], v)
             assert all(v <= (TOL_DW if key == "dW" else TOL) for key, v in errs.items()), (label, step, name, errs)
+        assert not generated or not p_hip, f"P of {sorted(p_hip)} was never compared"
     for name, p in named:
         Q = opt.state[p]["Q"].double()
         assert torch.isfinite(p).all() and torch.isfinite(opt.state[p]["momentum"]).all()
@@ -164,19 +203,40 @@ def test_config2_single_4096_r64():
 
 
 def test_config3_llama_shapes_bench_settings():
+    _run_vs_oracle("config3_llama_shapes_r64", _llama_set(), 64, steps=3)
+
+
+def _llama_set():
     shapes = []
     for layer in range(2):
         for name, m, n in (("linear_qkv", 6144, 4096), ("linear_proj", 4096, 4096),
                            ("linear_fc1", 28672, 4096), ("linear_fc2", 4096, 14336)):
             shapes.append((f"layers.{layer}.{name}.weight", m, n))
-    _run_vs_oracle("config3_llama_shapes_r64", shapes, 64, steps=3)
+    return shapes
+
+
+def _mixtral_set():
+    shapes = [(f"layers.0.experts.{e}.linear_fc1.weight", 28672, 4096) for e in range(8)] + \
+             [(f"layers.0.experts.{e}.linear_fc2.weight", 4096, 14336) for e in range(8)]
+    return shapes, [shapes[0][0], shapes[7][0], shapes[8][0], shapes[15][0]]
 
 
 def test_config5_mixtral_experts_r128():
-    shapes = [(f"layers.0.experts.{e}.linear_fc1.weight", 28672, 4096) for e in range(8)] + \
-             [(f"layers.0.experts.{e}.linear_fc2.weight", 4096, 14336) for e in range(8)]
-    check = [shapes[0][0], shapes[7][0], shapes[8][0], shapes[15][0]]
+    shapes, check = _mixtral_set()
     _run_vs_oracle("config5_mixtral_experts_r128", shapes, 128, steps=2, check=check)
+
+
+def test_config3_llama_generated_sketch():
+    """The timed path itself: bench.py's generated Rademacher sketch (sketch_rad_kernel at
+    m_P = 6144 / 4096 / 28672 / 14336, its many-chunk slab-reduced configuration) against the
+    oracle's Gaussian-sketch step."""
+    _run_vs_oracle("config3_llama_generated_sketch", _llama_set(), 64, steps=3, generated=True)
+
+
+def test_config5_mixtral_generated_sketch():
+    """r = 128, k = 256 sketch rows, generated as bench.py runs it, against the oracle."""
+    shapes, check = _mixtral_set()
+    _run_vs_oracle("config5_mixtral_generated_sketch", shapes, 128, steps=2, check=check, generated=True)
 
 
 # ---------------------------------------------------------------------------------------------- W = 2, k > 1

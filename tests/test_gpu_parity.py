@@ -256,7 +256,7 @@ def test_project_kernels_against_fp64():
         assert all(v != 0 for v in nz.tolist())
 
 
-@pytest.mark.parametrize("transposed,r", [(False, 64), (True, 64), (True, 128)])
+@pytest.mark.parametrize("transposed,r", [(False, 64), (True, 64), (False, 128), (True, 128)])
 def test_pass_b_fixed_scale_from_pass_a_max(transposed, r):
     """Pass A (the fused deferred-EF kernels, row or column) leaves max |M_b| in its nonzero
     flag; pass B given those flags runs the fp16x3 kernel (column kernel not transposed, row
@@ -416,7 +416,23 @@ def test_llama_shape_properties(m, n):
                                        (384, 1280, 128, torch.bfloat16), (128, 768, 128, torch.bfloat16),
                                        (128, 640, 128, torch.bfloat16), (2048, 384, 128, torch.bfloat16)])
 def test_deferred_ef_pass_a_matches_eager_and_fp64(m, n, r, gdt):
-    """dion_project_p_ef == (dion_ef_apply on M, then dion_project_p), and both == fp64 math."""
+    _deferred_ef_case(m, n, r, gdt, 0)
+
+
+@pytest.mark.parametrize("m,n,r", [(2048, 512, 128), (512, 2048, 128), (1536, 1024, 64), (1024, 1536, 64)])
+def test_deferred_ef_pass_a_twelve_decades(m, n, r):
+    """The r = 128 LDS-DMA pass A (rowproj_efgl / colproj_efgl: 256-row / 256-column blocks,
+    the splits' transpose swizzle on the DMA source address) and the r = 64 register kernels on
+    a contraction side spanning 12 decades, bf16 G."""
+    _deferred_ef_case(m, n, r, torch.bfloat16, 12)
+
+
+def _deferred_ef_case(m, n, r, gdt, decades):
+    """dion_project_p_ef == (dion_ef_apply on M, then dion_project_p), and both == fp64 math.
+    `decades` > 0 scales the contraction side of M, G and R' (columns of M for the row kernel,
+    rows for the transposed one) over that many decades, as the fixed-scale pass-B test does;
+    then M is also checked slice by slice (each slice against its own magnitude, plus the
+    EF's absolute floor of one per-matrix-scaled h3 product)."""
     from megatron_dion_amd.codec import HipDionCodec
 
     dev = _dev()
@@ -426,11 +442,16 @@ def test_deferred_ef_pass_a_matches_eager_and_fp64(m, n, r, gdt):
     mp, nq = (n, m) if transposed else (m, n)
     g = torch.Generator().manual_seed(m + n + r)
     B = 3
-    Ms = [torch.randn(m, n, generator=g).to(dev) * 1e-3 for _ in range(B)]
-    Gs = [(torch.randn(m, n, generator=g) * 1e-3).to(gdt).to(dev) for _ in range(B)]
+    if decades:
+        sc = torch.logspace(-decades, 0, nq, dtype=torch.float64).float()
+        sm = sc[:, None] if transposed else sc[None, :]
+    else:
+        sc, sm = torch.ones(nq), torch.ones(1)
+    Ms = [(torch.randn(m, n, generator=g) * sm).to(dev) * 1e-3 for _ in range(B)]
+    Gs = [(torch.randn(m, n, generator=g) * sm * 1e-3).to(gdt).to(dev) for _ in range(B)]
     Qs = [torch.randn(nq, r, generator=g).to(dev) for _ in range(B)]
     Pp = [torch.linalg.qr(torch.randn(mp, r, generator=g))[0].contiguous().to(dev) for _ in range(B)]
-    Rp = [(torch.randn(nq, r, generator=g) * 1e-2).to(dev) for _ in range(B)]
+    Rp = [(torch.randn(nq, r, generator=g) * sc[:, None] * 1e-2).to(dev) for _ in range(B)]
     mu = 0.95
     alpha = -(1.0 - mu)
     has = [True, False, True]  # entry 1 has no pending update
@@ -466,6 +487,16 @@ def test_deferred_ef_pass_a_matches_eager_and_fp64(m, n, r, gdt):
         assert maxrel(P2[b], P1[b]) <= 1e-5
         if not has[b]:
             assert torch.equal(M2[b], M1[b])
+        if decades:
+            # slice by slice along the contraction side: a mis-indexed or mis-scaled split
+            # shows here as an O(1) error of the slice (the 12-decade matrix of VERDICT r04)
+            dim = 1 if transposed else 0
+            den = Mref.abs().amax(dim=dim)
+            floor = 2.0 ** -20 * (alpha * ef).abs().max().item() if has[b] else 0.0
+            for Mx in (M1[b], M2[b]):
+                err = (Mx.double() - Mref).abs().amax(dim=dim)
+                bad = err > 1e-6 * den + floor
+                assert not bad.any(), (b, int(bad.sum()), (err / den.clamp_min(1e-300)).max().item())
 
 
 @pytest.mark.parametrize("label,shapes,r", [("tall_bf16", [(512, 384)] * 3, 64),

@@ -178,3 +178,22 @@ def test_reference_shared_p_buffer_defect_is_the_only_w2_difference():
     for step, rank, n, st, tr in _run_oracle(case, shared_p_buffer=False):
         for key, ref_key in (("W", "W1"), ("M", "M1"), ("Q", "Q1")):
             assert _maxrel(st[key], case.t(rank, step, f"{n}_{ref_key}")) <= 1e-6
+
+
+def test_w4_capture_is_the_per_batch_dion_step():
+    """c15 (W = 4, one batch per shape): no two same-shape batches are in flight, so the
+    reference's shared P buffer never aliases and the per-batch oracle (the HIP path's
+    semantics) reproduces the capture exactly, padding on rank 3 included."""
+    case = Case("c15_w4_pad_two_steps")
+    assert case.world == 4
+    for step in range(case.steps):
+        # the reference's batch order (sorted batch-key reprs, batches.py:903-968); the padded
+        # slot repeats the first member (its G, M, Q read as zero)
+        assert [(b["members"], b["real"]) for b in case.batches(0, step)] == [
+            (["t0", "t1", "t2", "t0"], 3), (["a0", "a1", "a2", "a3"], 4)]
+    n = 0
+    for step, rank, name, st, tr in _run_oracle(case, shared_p_buffer=False):
+        for key, ref_key in (("W", "W1"), ("M", "M1"), ("Q", "Q1")):
+            assert _maxrel(st[key], case.t(rank, step, f"{name}_{ref_key}")) <= 1e-6, (step, rank, name, key)
+            n += 1
+    assert n == 2 * 4 * 7 * 3
