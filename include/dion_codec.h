@@ -43,7 +43,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 13
+#define DION_ABI_VERSION 14
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -64,6 +64,9 @@ typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 #define DION_OP_EF_APPLY 6     /* optional: pre-split P for the rank-update kernels   */
 #define DION_OP_GRAD_SUM_SQ 7  /* dion_grad_sum_sq (only batch, m, n, g_dtype, ld_g used) */
 #define DION_OP_DORTHO 8       /* dion_dortho_sketch / dion_dortho_gram (row-sharded P)   */
+#define DION_OP_PSPLIT 9       /* not scratch: bytes of the p_split buffer of
+                                  dion_orthonormalize_fused / dion_project_r_split;
+                                  DION_E_UNSUPPORTED: no fused split for this shape        */
 
 typedef struct DionBatchDesc {
   int32_t batch;      /* matrices in this call (all the same shape)            */
@@ -191,10 +194,35 @@ int dion_project_r(const DionBatchDesc* desc, const float* const* M, const float
                    dion_stream_t stream);
 
 /*
+ * The W = 1 path with fewer passes over P (same results as dion_orthonormalize,
+ * dion_project_r and dion_fixup_colnorm in that order, for every input those reach:
+ * an orthonormalised P is NaN only in whole columns, and a whole NaN column gives
+ * R = 0 in that column either way).
+ * dion_orthonormalize_fused: dion_orthonormalize, then
+ *   `nonzero` (optional): the fix-up of P, P_b <- z ? 0 : nan_to_num(P_b) (in the last
+ *     solve's epilogue where it can; dion_fixup_colnorm is then called with P = NULL);
+ *   `p_split` (optional, DION_OP_PSPLIT bytes, 16-byte aligned): the fp16x3 limbs of the
+ *     final P in pass B's operand layout on the fixed scale 2^14 (|P| <= 1: orthonormal
+ *     columns), written by the last solve; DION_E_UNSUPPORTED (nothing enqueued) when
+ *     DION_OP_PSPLIT is unsupported for this desc.
+ * dion_project_r_split: dion_project_r reading P's limbs from `p_split` (NULL: as
+ *   dion_project_r); a pass B whose h3 kernel does not run for these pointers ignores it.
+ * No reference counterpart beyond the functions they fuse (ortho.py:71-123,
+ * runtime.py:1476-1477, kernels.py:185-188).
+ */
+int dion_orthonormalize_fused(const DionBatchDesc* desc, float* P, const float* sketch, uint64_t seed,
+                              float oversample, const uint32_t* nonzero, void* p_split, void* ws,
+                              size_t ws_bytes, dion_stream_t stream);
+int dion_project_r_split(const DionBatchDesc* desc, const float* const* M, const float* P,
+                         const void* p_split, float* R, const uint32_t* m_absmax, void* ws,
+                         size_t ws_bytes, dion_stream_t stream);
+
+/*
  * fix_all_zero_or_nan (kernels.py:157-204) + column normalisation
  * (kernels.py:207-210, 279-290) + Q commit (runtime.py:1132), for the
  * `desc->batch` real entries:
- *   z = !nonzero[b];  P_b <- z ? 0 : nan_to_num(P_b);
+ *   z = !nonzero[b];  P_b <- z ? 0 : nan_to_num(P_b)   (skipped when P is NULL: fixed by
+ *                                                     dion_orthonormalize_fused);
  *   R_b <- z ? nan_to_num(Q_b) : nan_to_num(R_b);
  *   Q_b <- R_b / (sqrt(sum_rows R_b^2) + eps)          (Q_b is overwritten)
  */

@@ -57,7 +57,7 @@ def source_build_id(roots=SOURCES) -> str | None:
             h.update(fh.read())
         h.update(b"\0")
     return h.hexdigest()[:16]
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -77,6 +77,7 @@ OP_PROJECT_P_EF = 5
 OP_EF_APPLY = 6
 OP_GRAD_SUM_SQ = 7
 OP_DORTHO = 8
+OP_PSPLIT = 9
 
 # every symbol include/dion_codec.h declares
 EXPORTED = (
@@ -87,12 +88,14 @@ EXPORTED = (
     "dion_project_p",
     "dion_project_p_ef",
     "dion_orthonormalize",
+    "dion_orthonormalize_fused",
     "dion_dortho_sketch",
     "dion_dortho_qr_inv",
     "dion_dortho_apply",
     "dion_dortho_gram",
     "dion_dortho_chol_inv",
     "dion_project_r",
+    "dion_project_r_split",
     "dion_fixup_colnorm",
     "dion_fixup_colsum",
     "dion_colnorm_apply",
@@ -150,6 +153,9 @@ _SIGNATURES = {
     "dion_orthonormalize": ([_DESC, _P, _P, ctypes.c_uint64, ctypes.c_float, _P, ctypes.c_size_t, _P],
                             ctypes.c_int),
     "dion_project_r": ([_DESC, _PP, _P, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "dion_orthonormalize_fused": ([_DESC, _P, _P, ctypes.c_uint64, ctypes.c_float, _P, _P, _P, ctypes.c_size_t, _P],
+                                  ctypes.c_int),
+    "dion_project_r_split": ([_DESC, _PP, _P, _P, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_fixup_colnorm": ([_DESC, _P, _P, _PP, _P, ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_fixup_colsum": ([_DESC, _P, _P, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_colnorm_apply": ([_DESC, _P, _PP, _P, ctypes.c_float, _P], ctypes.c_int),

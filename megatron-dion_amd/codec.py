@@ -67,6 +67,7 @@ class HipDionCodec:
     """Enqueue the Dion codec kernels for batches of same-shape matrices."""
 
     name = "hip"
+    fuses_p_fixup = True  # orthonormalize(fix_nonzero=...) + fixup_colnorm(P=None)
 
     def __init__(self, device: Optional[torch.device] = None):
         self.lib = _lib.load()
@@ -177,20 +178,47 @@ class HipDionCodec:
 
     def orthonormalize(self, P: torch.Tensor, m: int, n: int, transposed: bool, seed: int,
                        oversample: float = 1.25, sketch: Optional[torch.Tensor] = None,
-                       state_dtype=torch.float32) -> None:
+                       state_dtype=torch.float32, fix_nonzero: Optional[torch.Tensor] = None,
+                       p_split: Optional[torch.Tensor] = None) -> None:
         """Randomised Cholesky QR of every P_b in place.  ortho.py:71-123.
 
-        With a bf16 state the fp32 result is rounded back to bf16 values (ortho.py:123)."""
+        With a bf16 state the fp32 result is rounded back to bf16 values (ortho.py:123).
+        `fix_nonzero` (B,): also the fix-up of P (kernels.py:185-188; fixup_colnorm then gets
+        P=None); `p_split` (psplit_buffer): also pass B's split of P (project_r(p_split=...))."""
         B, _, r = P.shape
         if B == 0:
             return
         d = self._desc(B, m, n, r, transposed, state_dtype=state_dtype)
         ws = self.workspace(d, _lib.OP_ORTHONORMALIZE)
-        rc = self.lib.dion_orthonormalize(ctypes.byref(d), P.data_ptr(),
-                                          None if sketch is None else sketch.data_ptr(),
-                                          int(seed) & ((1 << 64) - 1), float(oversample),
-                                          ws.data_ptr(), ws.numel(), self._stream())
+        if fix_nonzero is None and p_split is None:
+            rc = self.lib.dion_orthonormalize(ctypes.byref(d), P.data_ptr(),
+                                              None if sketch is None else sketch.data_ptr(),
+                                              int(seed) & ((1 << 64) - 1), float(oversample),
+                                              ws.data_ptr(), ws.numel(), self._stream())
+        else:
+            rc = self.lib.dion_orthonormalize_fused(ctypes.byref(d), P.data_ptr(),
+                                                    None if sketch is None else sketch.data_ptr(),
+                                                    int(seed) & ((1 << 64) - 1), float(oversample),
+                                                    None if fix_nonzero is None else fix_nonzero.data_ptr(),
+                                                    None if p_split is None else p_split.data_ptr(),
+                                                    ws.data_ptr(), ws.numel(), self._stream())
         _lib.check(rc, "dion_orthonormalize")
+
+    def psplit_buffer(self, B: int, m: int, n: int, r: int, transposed: bool,
+                      state_dtype=torch.float32) -> Optional[torch.Tensor]:
+        """The (B, per-entry bytes) buffer for pass B's split of P written by the last solve of the
+        orthonormalisation (DION_OP_PSPLIT), or None when this shape has no fused split."""
+        key = ("psplit", int(m), int(n), int(r), bool(transposed), state_dtype)
+        ok = self._ef_ok.get(key)
+        if ok is None:
+            d = self._desc(1, m, n, r, transposed, state_dtype=state_dtype)
+            nbytes = ctypes.c_size_t(0)
+            ok = self.lib.dion_workspace_bytes(ctypes.byref(d), _lib.OP_PSPLIT, ctypes.byref(nbytes)) == 0
+            self._ef_ok[key] = (int(nbytes.value) if ok else 0)
+            ok = self._ef_ok[key]
+        if not ok:
+            return None
+        return torch.empty((int(B), int(ok)), dtype=torch.uint8, device=self.device)
 
     # ------------------------------------------------------------ distributed RCQR
     # the per-rank pieces of dion/ortho.py:682-834 (P row-sharded over the TP group); the
@@ -246,9 +274,11 @@ class HipDionCodec:
                    "dion_dortho_chol_inv")
 
     def project_r(self, momentums: List[torch.Tensor], P: torch.Tensor, R: torch.Tensor,
-                  transposed: bool, nonzero: Optional[torch.Tensor] = None) -> None:
+                  transposed: bool, nonzero: Optional[torch.Tensor] = None,
+                  p_split: Optional[torch.Tensor] = None) -> None:
         """R = M^T P (or M P).  runtime.py:1476-1477.  `nonzero`: the flags project_p /
-        project_p_ef left for these momentums (their max |M|: fixed-scale pass B)."""
+        project_p_ef left for these momentums (their max |M|: fixed-scale pass B).  `p_split`:
+        P's limbs from orthonormalize(p_split=...) (no absmax / presplit of P here)."""
         B = len(momentums)
         if B == 0:
             return
@@ -256,21 +286,23 @@ class HipDionCodec:
         r = int(P.shape[2])
         d = self._desc(B, m, n, r, transposed, M=momentums[0])
         ws = self.workspace(d, _lib.OP_PROJECT_R)
-        rc = self.lib.dion_project_r(ctypes.byref(d), _ptrs(momentums), P.data_ptr(), R.data_ptr(),
-                                     None if nonzero is None else nonzero.data_ptr(),
-                                     ws.data_ptr(), ws.numel(), self._stream())
+        rc = self.lib.dion_project_r_split(ctypes.byref(d), _ptrs(momentums), P.data_ptr(),
+                                           None if p_split is None else p_split.data_ptr(), R.data_ptr(),
+                                           None if nonzero is None else nonzero.data_ptr(),
+                                           ws.data_ptr(), ws.numel(), self._stream())
         _lib.check(rc, "dion_project_r")
 
-    def fixup_colnorm(self, P: torch.Tensor, R: torch.Tensor, qs: List[torch.Tensor],
+    def fixup_colnorm(self, P: Optional[torch.Tensor], R: torch.Tensor, qs: List[torch.Tensor],
                       nonzero: torch.Tensor, eps: float, m: int, n: int, transposed: bool) -> None:
-        """fix_all_zero_or_nan + column normalisation; Q states receive Q_new."""
+        """fix_all_zero_or_nan + column normalisation; Q states receive Q_new.  P=None: P was
+        already fixed (orthonormalize(fix_nonzero=...))."""
         B = len(qs)
         if B == 0:
             return
-        r = int(P.shape[2])
+        r = int(R.shape[2])
         d = self._desc(B, m, n, r, transposed, state_dtype=_state_dtype(None, qs))
         ws = self.workspace(d, _lib.OP_FIXUP_COLNORM)
-        rc = self.lib.dion_fixup_colnorm(ctypes.byref(d), P.data_ptr(), R.data_ptr(), _ptrs(qs),
+        rc = self.lib.dion_fixup_colnorm(ctypes.byref(d), None if P is None else P.data_ptr(), R.data_ptr(), _ptrs(qs),
                                          nonzero.data_ptr(), float(eps), ws.data_ptr(), ws.numel(),
                                          self._stream())
         _lib.check(rc, "dion_fixup_colnorm")

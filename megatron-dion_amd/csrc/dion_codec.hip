@@ -2168,6 +2168,120 @@ __global__ void __launch_bounds__(256) trsm_right_kernel(const float* __restrict
   }
 }
 
+// The same solve for r = RT = 32 or 64 with the rows staged through LDS.  trsm_right_kernel
+// reads a row per lane straight from HBM (each load instruction touches 64 rows); here each
+// wave owns 64 consecutive rows (one contiguous 64 x RT fp32 block), stages them by LDS-DMA
+// (global_load_lds_dwordx4: every instruction reads 1 KB of consecutive lines), solves its
+// row from LDS, writes the row back into the same LDS image and stores the block as
+// consecutive lines.  No block barrier: a wave reads only what it loaded.  The LDS image is
+// XOR-swizzled by 16-B chunk (chunk c of row i at slot i CH + (c ^ swz(i))) so the per-row
+// ds_read_b128 / ds_write_b128 are conflict-free; the DMA's LDS side is lane-linear, so the
+// swizzle is applied on the source offsets.  Same arithmetic, in the same order, as
+// trsm_right_kernel (bitwise identical).
+//
+// FINAL (the last solve of the RCQR, P = P1 R2^-1) can fold in what follows it on the W = 1
+// path, from the LDS image of the finished rows:
+//   * `nonzero`: the fix-up of P (kernels.py:185-188, pfix_kernel): z ? 0 : nan_to_num(x);
+//   * `psplit`: the fp16x3 limbs of P in pass B's operand layout (presplit16_kernel layout 0,
+//     `kmap`), on the fixed scale 2^14: the columns of P are orthonormal, so |x| <= 1 and
+//     x 2^14 stays far inside fp16 (the measured-maximum scale of presplit16 would be 2^14 or
+//     larger); a NaN column stays NaN in both limbs.  Pass B then needs no absmax / presplit.
+template <int RT>
+__device__ __forceinline__ int trsm_swz(int row) {
+  return RT == 64 ? (row & 15) : ((row >> 1) & 7);
+}
+constexpr float kPSplitScale = 16384.f;  // 2^14: the fixed h3 scale of an orthonormal P
+constexpr float kPSplitInv = 1.f / 16384.f;
+
+struct TrsmArgs {
+  const float* src;
+  float* dst;
+  const float* fac;           // (batch, RT RT + RT): factor + reciprocal diagonal
+  const uint32_t* nonzero;    // FINAL: fix P with these flags (null: no fix)
+  f16x8* psplit;              // FINAL: pass-B split of P (null: none)
+  long pstride;               // f16x8 units per matrix of psplit
+  int mp, kmap;
+};
+
+template <int RT, bool FINAL>
+__global__ void __launch_bounds__(256, 2) trsm_lds_kernel(const TrsmArgs a) {
+  static_assert(RT == 32 || RT == 64, "trsm_lds_kernel: r = 32 or 64");
+  constexpr int CH = RT / 4;  // 16-B chunks per row
+  constexpr int RB = RT / 16;
+  __shared__ f32x4 img[4][64 * CH];
+  const int b = blockIdx.y;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  const long row0 = static_cast<long>(blockIdx.x) * 256 + wave * 64;
+  const int mp = a.mp;
+  const int nrows = static_cast<int>(min(static_cast<long>(64), static_cast<long>(mp) - row0));
+  if (nrows <= 0) return;
+  const float* R = a.fac + static_cast<long>(b) * (RT * RT + RT);
+  f32x4* w = img[wave];
+  const char* s = reinterpret_cast<const char*>(a.src + (static_cast<long>(b) * mp + row0) * RT);
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int slot = 64 * i + lane, row = slot / CH, cp = slot % CH;
+    if (row < nrows) glds16<false>(s, static_cast<uint32_t>((row * CH + (cp ^ trsm_swz<RT>(row))) * 16), lds_off(&w[64 * i]));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float x[RT];
+  if (lane < nrows) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const f32x4 v = w[lane * CH + (c ^ trsm_swz<RT>(lane))];
+      x[4 * c] = v[0], x[4 * c + 1] = v[1], x[4 * c + 2] = v[2], x[4 * c + 3] = v[3];
+    }
+#pragma unroll
+    for (int k = 0; k < RT; ++k) {
+      x[k] *= R[RT * RT + k];
+#pragma unroll
+      for (int j = k + 1; j < RT; ++j) x[j] = fmaf(-x[k], R[k * RT + j], x[j]);
+    }
+    if constexpr (FINAL) {
+      if (a.nonzero != nullptr) {
+        const bool zero = a.nonzero[b] == 0u;
+#pragma unroll
+        for (int j = 0; j < RT; ++j) x[j] = zero ? 0.f : nan_to_num(x[j]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      w[lane * CH + (c ^ trsm_swz<RT>(lane))] = f32x4{x[4 * c], x[4 * c + 1], x[4 * c + 2], x[4 * c + 3]};
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  f32x4* d = reinterpret_cast<f32x4*>(a.dst + (static_cast<long>(b) * mp + row0) * RT);
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int slot = 64 * i + lane, row = slot / CH, cp = slot % CH;
+    if (row < nrows) d[row * CH + (cp ^ trsm_swz<RT>(row))] = w[slot];
+  }
+  if constexpr (FINAL) {
+    if (a.psplit != nullptr) {
+      // unit (32-row block q, column block cb), lane (t, g): rows 32 q + kmap(g, e), column 16 cb + t
+      const float* wf = reinterpret_cast<const float*>(w);
+      const int t = lane & 15, g = lane >> 4;
+      f16x8* out = a.psplit + b * a.pstride;
+#pragma unroll
+      for (int u = 0; u < 2 * RB; ++u) {
+        const int q = u / RB, cb = u % RB;
+        if (32 * q >= nrows) break;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int row = 32 * q + (a.kmap == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3));
+          const int col = 16 * cb + t;
+          v[e] = wf[(row * CH + ((col >> 2) ^ trsm_swz<RT>(row))) * 4 + (col & 3)];
+        }
+        Split2h sp;
+        split2h(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, kPSplitScale, sp);
+        const long grp = (row0 / 32 + q) * RB + cb;
+        out[grp * 128 + lane] = sp.hi;
+        out[grp * 128 + 64 + lane] = sp.lo;
+      }
+    }
+  }
+}
+
 // ============================================================================
 // S P for a generated sketch (ortho.py:90-104: SP = sketch @ P, k = ceil(1.25 r / 128) 128
 // rows).  The reference draws S ~ N(0, 1/k) from the unseeded global RNG (ortho.py:659-661),
@@ -2907,8 +3021,10 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colpr
   else
     run(std::false_type{});
 
-  // P's per-matrix scale (and M's, fixed mode), then lane (t, g): R row CT t + c, columns 16 cb + 4 g .. + 3
-  const float ps = a.tinv[b] * (fixed ? finv : 1.f);
+  // P's per-matrix scale (a.tinv: presplit16's; null: the fixed scale of an orthonormal P split
+  // by the final solve, trsm_lds_kernel<..., true>) and M's (fixed mode), then lane (t, g): R row
+  // CT t + c, columns 16 cb + 4 g .. + 3
+  const float ps = (a.tinv != nullptr ? a.tinv[b] : kPSplitInv) * (fixed ? finv : 1.f);
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
 #pragma unroll
   for (int c = 0; c < CT; ++c)
@@ -3991,8 +4107,8 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ?
   else
     run(std::false_type{});
 
-  // lane (t, g): R row 16 rb + t, columns 16 cb + 4 g .. + 3
-  const float ps = a.tinv[b] * (fixed ? finv : 1.f);
+  // lane (t, g): R row 16 rb + t, columns 16 cb + 4 g .. + 3 (a.tinv null: fixed P split scale)
+  const float ps = (a.tinv != nullptr ? a.tinv[b] : kPSplitInv) * (fixed ? finv : 1.f);
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
 #pragma unroll
   for (int rb = 0; rb < kRBE; ++rb)
@@ -4256,6 +4372,29 @@ OrthoPlan ortho_plan(int mp, int r, int batch, float oversample) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// P <- z ? 0 : nan_to_num(P) over batch entries of per_entry values (kernels.py:185-188)
+int launch_pfix(float* P, const uint32_t* nonzero, long per_entry, int batch, hipStream_t st) {
+  long blocks = ceil_div(per_entry * batch, 256);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) return DION_OK;
+  hipLaunchKernelGGL(pfix_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, P, nonzero, per_entry, batch);
+  return check_launch("pfix");
+}
+
+// The final solve of the orthonormalisation writes pass B's fp16x3 split of P (fixed scale,
+// trsm_lds_kernel<..., true>) when pass B runs its h3 kernels on this shape: fp32 state, r = 32
+// or 64, m_P > r (the Cholesky QR path), m_P a multiple of 32, and run_projection's h3 shape
+// conditions for the orientation (the layout / ld / alignment conditions are checked per call:
+// a pass B that cannot use the split ignores it).
+bool psplit_ok(const DionBatchDesc* d) {
+  if (d->m_dtype != DION_DTYPE_F32 || !(d->r == 32 || d->r == 64)) return false;
+  const bool tr = d->transposed != 0;
+  const int mp = tr ? d->n : d->m;
+  if (mp <= d->r || mp % 32 != 0) return false;
+  if (tr) return kPbH3r && rowproj_fast_ok(d->m, d->n, d->r) && d->m % (16 * kRBE * kPbRNW) == 0;
+  return colproj_fast_ok(d->m, d->n, d->r) && colh3_ok(d->m, d->n, d->r);
+}
+
 // one absmax_kernel launch over `groups` groups of nb matrices (AbsMaxArgs order)
 void launch_absmax(AbsMaxArgs& ma, int groups, hipStream_t st) {
   long most = 0;
@@ -4307,7 +4446,8 @@ int launch_reduce(float* out, const float* slab, int nchunk, long per_entry, int
 // One projection over up to MAXB matrices.  `row_mode`: reduce over columns.
 int run_projection(bool row_mode, int rows, int cols, int r, int batch, const void* const* G, float* const* M,
                    const float* const* thin, long ld_m, long ld_g, int gdt, float* out, uint32_t* nonzero,
-                   void* ws, size_t ws_bytes, hipStream_t st, const uint32_t* mabs = nullptr) {
+                   void* ws, size_t ws_bytes, hipStream_t st, const uint32_t* mabs = nullptr,
+                   const f16x8* thin_split = nullptr) {
   bool fast = row_mode ? rowproj_fast_ok(rows, cols, r) : colproj_fast_ok(rows, cols, r);
   fast = fast && (ld_m % 8) == 0 && (gdt == DION_DTYPE_NONE || (ld_g % 8) == 0);
   for (int b = 0; b < batch && fast; ++b)
@@ -4331,7 +4471,12 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     return fail(DION_E_WORKSPACE, "projection needs %zu workspace bytes, got %zu", need, ws_bytes);
   ProjArgs a;
   memset(&a, 0, sizeof(a));
-  if (h3) {
+  if (h3 && thin_split != nullptr) {
+    // the final solve of the orthonormalisation already wrote P's limbs (fixed scale)
+    a.tsplit = thin_split;
+    a.ts_stride = static_cast<long>(thin_rows) * r / 8 * 2;
+    a.tinv = nullptr;
+  } else if (h3) {
     // fp16x3: the thin operand's per-matrix |max|, then its two fp16 limbs
     char* base = static_cast<char*>(ws) + slab;
     const long per = static_cast<long>(thin_rows) * r;
@@ -4547,6 +4692,14 @@ int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t s
 // factor kernels)
 int launch_trsm(const float* src, float* dst, const float* fac, int mp, int r, int batch, hipStream_t st) {
   const dim3 grid(static_cast<unsigned>(ceil_div(mp, 256)), batch);
+  if ((r == 32 || r == 64) && aligned16(src) && aligned16(dst)) {  // rows staged through LDS
+    TrsmArgs a{src, dst, fac, nullptr, nullptr, 0, mp, 0};
+    if (r == 64)
+      hipLaunchKernelGGL((trsm_lds_kernel<64, false>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((trsm_lds_kernel<32, false>), grid, dim3(256), 0, st, a);
+    return check_launch("trsm_lds");
+  }
   switch (trsm_rt(r)) {
     case 32: hipLaunchKernelGGL((trsm_right_kernel<32>), grid, dim3(256), 0, st, src, dst, fac, mp, r); break;
     case 64: hipLaunchKernelGGL((trsm_right_kernel<64>), grid, dim3(256), 0, st, src, dst, fac, mp, r); break;
@@ -4687,6 +4840,12 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
   if (bytes == nullptr) return fail(DION_E_INVALID, "bytes is null");
   const int mp = d->transposed ? d->n : d->m;
   const int nq = d->transposed ? d->m : d->n;
+  if (op == DION_OP_PSPLIT) {
+    // not scratch: the caller's buffer for dion_orthonormalize_fused -> dion_project_r_split
+    if (!psplit_ok(d)) return fail(DION_E_UNSUPPORTED, "no fused pass-B split for %dx%d r=%d", d->m, d->n, d->r);
+    *bytes = sizeof(uint16_t) * 2 * static_cast<size_t>(d->batch) * mp * d->r;
+    return DION_OK;
+  }
   size_t need = 0;
   const int chunks[2] = {d->batch < MAXB ? d->batch : MAXB, d->batch % MAXB};
   if (d->m_dtype == DION_DTYPE_BF16) {
@@ -4985,6 +5144,11 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
 
 int dion_project_r(const DionBatchDesc* d, const float* const* M, const float* P, float* R,
                    const uint32_t* m_absmax, void* ws, size_t ws_bytes, dion_stream_t stream) {
+  return dion_project_r_split(d, M, P, nullptr, R, m_absmax, ws, ws_bytes, stream);
+}
+
+int dion_project_r_split(const DionBatchDesc* d, const float* const* M, const float* P, const void* p_split,
+                         float* R, const uint32_t* m_absmax, void* ws, size_t ws_bytes, dion_stream_t stream) {
   int rc = validate(d);
   if (rc != DION_OK) return rc;
   if (M == nullptr || P == nullptr || R == nullptr) return fail(DION_E_INVALID, "null argument");
@@ -5011,7 +5175,9 @@ int dion_project_r(const DionBatchDesc* d, const float* const* M, const float* P
     for (int b = 0; b < nb; ++b) thin[b] = P + static_cast<long>(b0 + b) * mp * d->r;
     rc = run_projection(d->transposed != 0, d->m, d->n, d->r, nb, nullptr, const_cast<float* const*>(M + b0), thin,
                         ld_m, 0, DION_DTYPE_NONE, R + static_cast<long>(b0) * nq * d->r, nullptr, ws, ws_bytes, st,
-                        m_absmax != nullptr ? m_absmax + b0 : nullptr);
+                        m_absmax != nullptr ? m_absmax + b0 : nullptr,
+                        p_split != nullptr ? static_cast<const f16x8*>(p_split) + static_cast<long>(b0) * mp * d->r / 4
+                                           : nullptr);
     if (rc != DION_OK) return rc;
   }
   return DION_OK;
@@ -5019,15 +5185,27 @@ int dion_project_r(const DionBatchDesc* d, const float* const* M, const float* P
 
 int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, uint64_t seed, float oversample,
                         void* ws, size_t ws_bytes, dion_stream_t stream) {
+  return dion_orthonormalize_fused(d, P, sketch, seed, oversample, nullptr, nullptr, ws, ws_bytes, stream);
+}
+
+int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* sketch, uint64_t seed, float oversample,
+                              const uint32_t* nonzero, void* p_split, void* ws, size_t ws_bytes,
+                              dion_stream_t stream) {
   int rc = validate(d);
   if (rc != DION_OK) return rc;
   if (d->r > d->m || d->r > d->n)
     return fail(DION_E_INVALID, "rank r=%d exceeds min(m=%d, n=%d) of a whole matrix", d->r, d->m, d->n);
   if (P == nullptr) return fail(DION_E_INVALID, "P is null");
   if (!(oversample > 0.f)) return fail(DION_E_INVALID, "oversample=%f", oversample);
+  if (p_split != nullptr && (!psplit_ok(d) || !aligned16(P) || !aligned16(p_split)))
+    return fail(DION_E_UNSUPPORTED, "no fused pass-B split for %dx%d r=%d", d->m, d->n, d->r);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int mp = d->transposed ? d->n : d->m;
   const int r = d->r;
+  // the fix-up of P rides on the last solve when it is the LDS solve of an fp32 P; elsewhere
+  // (plain QR, other r, bf16 rounding) pfix_kernel runs after the orthonormalisation
+  const bool fuse_fix = nonzero != nullptr && d->m_dtype == DION_DTYPE_F32 && (r == 32 || r == 64) && mp > r &&
+                        aligned16(P);
   for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
     const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
     float* Pb = P + static_cast<long>(b0) * mp * r;
@@ -5082,12 +5260,28 @@ int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, u
     rc = launch_chol_inv(gm, fac, r, nb, st, false);
     if (rc != DION_OK) return rc;
     (void)r2;
-    // (6) P = P1 R2^-1 (back into the caller's buffer)
-    rc = launch_trsm(p1, Pb, fac, mp, r, nb, st);
+    // (6) P = P1 R2^-1 (back into the caller's buffer), with the fix-up and pass B's split
+    if (fuse_fix || p_split != nullptr) {
+      TrsmArgs ta{p1, Pb, fac, fuse_fix ? nonzero + b0 : nullptr,
+                  p_split != nullptr ? static_cast<f16x8*>(p_split) + static_cast<long>(b0) * mp * r / 4 : nullptr,
+                  static_cast<long>(mp) * r / 4, mp, d->transposed ? 1 : 0};
+      const dim3 grid(static_cast<unsigned>(ceil_div(mp, 256)), nb);
+      if (r == 64)
+        hipLaunchKernelGGL((trsm_lds_kernel<64, true>), grid, dim3(256), 0, st, ta);
+      else
+        hipLaunchKernelGGL((trsm_lds_kernel<32, true>), grid, dim3(256), 0, st, ta);
+      rc = check_launch("trsm_lds(final)");
+    } else {
+      rc = launch_trsm(p1, Pb, fac, mp, r, nb, st);
+    }
     if (rc != DION_OK) return rc;
   }
   // ortho.py:123: the fp32 result is cast back to P's dtype
-  if (d->m_dtype == DION_DTYPE_BF16) return b16::round_buffer(P, static_cast<long>(d->batch) * mp * r, st);
+  if (d->m_dtype == DION_DTYPE_BF16) {
+    rc = b16::round_buffer(P, static_cast<long>(d->batch) * mp * r, st);
+    if (rc != DION_OK) return rc;
+  }
+  if (nonzero != nullptr && !fuse_fix) return launch_pfix(P, nonzero, static_cast<long>(mp) * r, d->batch, st);
   return DION_OK;
 }
 
@@ -5189,19 +5383,14 @@ int dion_fixup_colnorm(const DionBatchDesc* d, float* P, float* R, float* const*
                        float eps, void* ws, size_t ws_bytes, dion_stream_t stream) {
   int rc = validate(d);
   if (rc != DION_OK) return rc;
-  if (P == nullptr || R == nullptr || Q == nullptr || nonzero == nullptr)
-    return fail(DION_E_INVALID, "null argument");
+  if (R == nullptr || Q == nullptr || nonzero == nullptr) return fail(DION_E_INVALID, "null argument");
   if (d->batch == 0) return DION_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int mp = d->transposed ? d->n : d->m;
   const int nq = d->transposed ? d->m : d->n;
   const int r = d->r;
-  {
-    const long per = static_cast<long>(mp) * r;
-    long blocks = ceil_div(per * d->batch, 256);
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(pfix_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, P, nonzero, per, d->batch);
-    rc = check_launch("pfix");
+  if (P != nullptr) {  // null: P was fixed by dion_orthonormalize_fused
+    rc = launch_pfix(P, nonzero, static_cast<long>(mp) * r, d->batch, st);
     if (rc != DION_OK) return rc;
   }
   for (int b0 = 0; b0 < d->batch; b0 += MAXB) {

@@ -389,6 +389,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
                              oversample, sketch=None if S is None else S.reshape(1, *S.shape[-2:]).contiguous(),
                              state_dtype=sdt)
 
+    p_fixed = False
     if W > 1 and kch:
         rank = dist.get_rank(group)
         mine = P[rank * kch:(rank + 1) * kch]
@@ -459,22 +460,36 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
             if bf16_state:
                 codec.round_bf16(R)
     else:
+        # W = 1, fp32 state: the last solve of the orthonormalisation also fixes P (the fix-up's
+        # P half, kernels.py:185-188: an orthonormalised P is NaN only in whole columns, whose R
+        # column is zero either way) and writes pass B's split of P, so pass B needs no absmax /
+        # presplit of P and the fix-up no pass over P.  The split is allocated here, on the
+        # stream of the batch's streaming passes (as P is), before a pipelined schedule moves
+        # the orthonormalisation to its latency stream.
+        fused = real == B and not bf16_state and getattr(codec, "fuses_p_fixup", False)
+        split = codec.psplit_buffer(B, m, n, r, transposed) if fused and hasattr(codec, "psplit_buffer") else None
+        fix = nonzero if fused else None
+        p_fixed = fused
         if phase_marks:
             yield "ortho"
         if sketches is None:
             codec.orthonormalize(P[:real], m, n, transposed, _sketch_seed(optimizer, batch_cache_key, 0),
-                                 oversample, state_dtype=sdt)
+                                 oversample, state_dtype=sdt, **_fused_kw(fix, split, 0, real))
         else:
             for i in range(real):
-                ortho(P[i:i + 1], i)
+                S = sketches.get(i)
+                codec.orthonormalize(P[i:i + 1], m, n, transposed, _sketch_seed(optimizer, batch_cache_key, i),
+                                     oversample, sketch=None if S is None else S.reshape(1, *S.shape[-2:]).contiguous(),
+                                     state_dtype=sdt, **_fused_kw(fix, split, i, i + 1))
         if phase_marks:
             yield "stream"
         R = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
-        codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero)
+        codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero,
+                        **({} if split is None else {"p_split": split}))
 
     clock.mark("ortho_r")
     eps = float(optimizer.defaults["epsilon"])
-    codec.fixup_colnorm(P, R, list(Qs[:real]), nonzero, eps, m, n, transposed)
+    codec.fixup_colnorm(None if (W == 1 and p_fixed) else P, R, list(Qs[:real]), nonzero, eps, m, n, transposed)
     clock.mark("q_normalize")
 
     grp = optim_groups[0] or {}
@@ -939,6 +954,16 @@ def _record_pending(state, P_b, R_b, alpha, transposed: bool) -> None:
     M = dict.get(state, "momentum")
     dict.__setitem__(state, _PENDING_EF, (P_b, R_b, alpha, weakref.ref(M) if M is not None else None,
                                           bool(transposed)))
+
+
+def _fused_kw(fix, split, i0, i1) -> dict:
+    """orthonormalize's fused fix-up / pass-B split arguments for entries [i0, i1)."""
+    kw = {}
+    if fix is not None:
+        kw["fix_nonzero"] = fix[i0:i1]
+    if split is not None:
+        kw["p_split"] = split[i0:i1]
+    return kw
 
 
 def _take_pending(state):

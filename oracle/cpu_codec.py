@@ -13,6 +13,7 @@ from . import dion_oracle as O
 
 class OracleCodec:
     name = "oracle-cpu"
+    fuses_p_fixup = True  # orthonormalize(fix_nonzero=...) + fixup_colnorm(P=None)
 
     def __init__(self, sketch_lookup=None, hyper_eps=1e-8, deferred=False):
         self.sketch_lookup = sketch_lookup  # fn(P (1, m_P, r)) -> sketch (1, k, m_P) or None
@@ -38,7 +39,8 @@ class OracleCodec:
             P[b] = X @ qs[b].to(X.dtype)          # bf16 state: a bf16 matmul (runtime.py:1607-1616)
             nonzero[b] = int(bool((M != 0).any()))
 
-    def orthonormalize(self, P, m, n, transposed, seed, oversample=1.25, sketch=None, state_dtype=torch.float32):
+    def orthonormalize(self, P, m, n, transposed, seed, oversample=1.25, sketch=None, state_dtype=torch.float32,
+                       fix_nonzero=None, p_split=None):
         for b in range(P.shape[0]):
             S = sketch
             if S is None and self.sketch_lookup is not None:
@@ -46,6 +48,8 @@ class OracleCodec:
             gen = torch.Generator().manual_seed(int(seed) & ((1 << 63) - 1))
             out = O.orthogonalize(P[b:b + 1], oversample, sketch=S, generator=gen)
             P[b:b + 1] = out.to(state_dtype)      # ortho.py:123 casts back to P's dtype
+            if fix_nonzero is not None:           # the fused fix-up (kernels.py:185-188)
+                P[b] = torch.zeros_like(P[b]) if int(fix_nonzero[b]) == 0 else P[b].nan_to_num()
 
     # distributed RCQR pieces (dion/ortho.py:682-834): the reference's arithmetic, with the
     # triangular solves as products with the explicit inverses the codec interface passes on
@@ -73,7 +77,7 @@ class OracleCodec:
     def round_bf16(self, X):
         X.copy_(X.to(torch.bfloat16).float())
 
-    def project_r(self, momentums, P, R, transposed, nonzero=None):
+    def project_r(self, momentums, P, R, transposed, nonzero=None, p_split=None):
         for b, M in enumerate(momentums):
             X = M.mT if transposed else M
             R[b] = X.mT @ P[b].to(X.dtype)
@@ -82,7 +86,8 @@ class OracleCodec:
         B = len(qs)
         Q = torch.stack(qs, 0)
         zero = (nonzero[:B] == 0).view(B, 1, 1)
-        P[:B] = torch.where(zero, torch.zeros_like(P[:B]), P[:B].nan_to_num())
+        if P is not None:  # None: fixed by orthonormalize(fix_nonzero=...)
+            P[:B] = torch.where(zero, torch.zeros_like(P[:B]), P[:B].nan_to_num())
         R[:B] = torch.where(zero, Q.nan_to_num(), R[:B].nan_to_num())
         Qn = O.column_normalize(R[:B], eps)
         for b in range(B):
