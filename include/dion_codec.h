@@ -112,7 +112,9 @@ int dion_project_p(const DionBatchDesc* desc, const void* const* G, float* const
 
 /* The previous step's error feedback, not yet applied to M (see dion_project_p_ef). */
 typedef struct DionPendingEF {
-  const float* const* P; /* per matrix: its m_P x r factor P_b of the previous step, or NULL */
+  const float* const* P; /* per matrix: its m_P x r factor P_b of the previous step (after the
+                            fix-up: orthonormal or zero columns, every |x| < 2; the fp32 kernels
+                            split it on the fixed scale 2^14), or NULL */
   const float* const* R; /* per matrix: its n_Q x r factor R_b of the previous step, or NULL */
   float alpha;           /* -(1 - mu) of that step */
 } DionPendingEF;

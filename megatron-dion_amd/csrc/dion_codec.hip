@@ -2282,6 +2282,115 @@ __global__ void __launch_bounds__(256, 2) trsm_lds_kernel(const TrsmArgs a) {
   }
 }
 
+// The first solve of the RCQR (P1 = P R1^-1) with the Gram product of the next step
+// (ortho.py:106-110: Gram = P1^T P1) folded in: trsm_lds_kernel's solve and stores, then each
+// wave adds its 64 finished rows (still in its LDS image) to the Gram on
+// v_mfma_f32_16x16x4f32 (exact fp32 products, as colproj_kernel's panel Gram), so P1 is not read
+// again for it.  A block takes L consecutive 256-row chunks; its 4 waves' Grams are summed in
+// wave order through LDS and the block writes one r x r partial, summed in block order by
+// reduce_slabs_kernel (deterministic).
+template <int RT, int L>
+__global__ void __launch_bounds__(256, 2) trsm_gram_kernel(const TrsmArgs a, float* __restrict__ gslab) {
+  static_assert(RT == 32 || RT == 64, "trsm_gram_kernel: r = 32 or 64");
+  constexpr int CH = RT / 4, RB = RT / 16;
+  __shared__ f32x4 img[4][64 * CH];
+  const int b = blockIdx.y;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  const int t = lane & 15, g = lane >> 4;
+  const int mp = a.mp;
+  const float* R = a.fac + static_cast<long>(b) * (RT * RT + RT);
+  f32x4* w = img[wave];
+  const float* wf = reinterpret_cast<const float*>(w);
+  f32x4 acc[RB][RB];
+#pragma unroll
+  for (int i = 0; i < RB; ++i)
+#pragma unroll
+    for (int j = 0; j < RB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int it = 0; it < L; ++it) {
+    const long row0 = (static_cast<long>(blockIdx.x) * L + it) * 256 + wave * 64;
+    const int nrows = static_cast<int>(min(static_cast<long>(64), static_cast<long>(mp) - row0));
+    if (nrows <= 0) break;
+    const char* s = reinterpret_cast<const char*>(a.src + (static_cast<long>(b) * mp + row0) * RT);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous chunk's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int slot = 64 * i + lane, row = slot / CH, cp = slot % CH;
+      if (row < nrows)
+        glds16<false>(s, static_cast<uint32_t>((row * CH + (cp ^ trsm_swz<RT>(row))) * 16), lds_off(&w[64 * i]));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane < nrows) {
+      float x[RT];
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const f32x4 v = w[lane * CH + (c ^ trsm_swz<RT>(lane))];
+        x[4 * c] = v[0], x[4 * c + 1] = v[1], x[4 * c + 2] = v[2], x[4 * c + 3] = v[3];
+      }
+#pragma unroll
+      for (int k = 0; k < RT; ++k) {
+        x[k] *= R[RT * RT + k];
+#pragma unroll
+        for (int j = k + 1; j < RT; ++j) x[j] = fmaf(-x[k], R[k * RT + j], x[j]);
+      }
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+        w[lane * CH + (c ^ trsm_swz<RT>(lane))] = f32x4{x[4 * c], x[4 * c + 1], x[4 * c + 2], x[4 * c + 3]};
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    f32x4* d = reinterpret_cast<f32x4*>(a.dst + (static_cast<long>(b) * mp + row0) * RT);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int slot = 64 * i + lane, row = slot / CH, cp = slot % CH;
+      if (row < nrows) d[row * CH + (cp ^ trsm_swz<RT>(row))] = w[slot];
+    }
+    // Gram += X^T X over this chunk: tile (i, j), 4 rows per MFMA; lane (t, g) holds row k0 + g
+#pragma unroll 4
+    for (int k0 = 0; k0 < 64; k0 += 4) {
+      const int row = k0 + g;
+      float v[RB];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int col = 16 * i + t;
+        v[i] = row < nrows ? wf[(row * CH + ((col >> 2) ^ trsm_swz<RT>(row))) * 4 + (col & 3)] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < RB; ++i)
+#pragma unroll
+        for (int j = 0; j < RB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], v[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // the block's Gram: waves 1..3 add theirs to wave 0's in wave order (LDS), one partial per block
+  float* red = reinterpret_cast<float*>(img[0]);  // RB RB 4 floats per lane, lane-major
+  for (int src = 1; src < 4; ++src) {
+    __syncthreads();
+    if (wave == src) {
+#pragma unroll
+      for (int i = 0; i < RB; ++i)
+#pragma unroll
+        for (int j = 0; j < RB; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) red[((i * RB + j) * 4 + q) * 64 + lane] = acc[i][j][q];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int i = 0; i < RB; ++i)
+#pragma unroll
+        for (int j = 0; j < RB; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[i][j][q] += red[((i * RB + j) * 4 + q) * 64 + lane];
+    }
+  }
+  if (wave != 0) return;
+  float* out = gslab + (static_cast<long>(b) * gridDim.x + blockIdx.x) * RT * RT;
+#pragma unroll
+  for (int i = 0; i < RB; ++i)
+#pragma unroll
+    for (int j = 0; j < RB; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) out[(16 * i + 4 * g + q) * RT + 16 * j + t] = acc[i][j][q];
+}
+
 // ============================================================================
 // S P for a generated sketch (ortho.py:90-104: SP = sketch @ P, k = ceil(1.25 r / 128) 128
 // rows).  The reference draws S ~ N(0, 1/k) from the unseeded global RNG (ortho.py:659-661),
@@ -2409,7 +2518,7 @@ struct EfProjArgs {
   const u32x4* rsplit;     // R'_b pre-split, A-operand layout
   long split_stride;
   float alpha;
-  const uint32_t* amax;    // h3 kernels: (3, batch) max |x| bits of Q, R', P'
+  const uint32_t* amax;    // h3 kernels: (2, batch) max |x| bits of Q, R' (P' is split on the fixed scale 2^14)
   const float* inv;        // h3 kernels: (2, batch) 1 / scale of the Q and R' splits
 };
 
@@ -3071,7 +3180,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : (RB >= 8 ? 8 / NW : kPa
   const float invQ = e.inv[b];
   const float invR = e.inv[nb + b];
   float invF;
-  const float sF = h3_scale(__uint_as_float(e.amax[2 * nb + b]), invF);  // power of two: P' s is exact
+  const float sF = h3_scale(1.f, invF);  // P' (fixed-up P: orthonormal columns, |x| <= 1) on 2^14: exact
   const float efinv = e.alpha * invF * invR;
 
   Split2h F[KR][KK];
@@ -3306,7 +3415,7 @@ __global__ void __launch_bounds__(512, 1) rowproj_efgl_kernel(const EfProjArgs e
   const float invQ = e.inv[b];
   const float invR = e.inv[nb + b];
   float invF;
-  const float sF = h3_scale(__uint_as_float(e.amax[2 * nb + b]), invF);  // power of two: P' s is exact
+  const float sF = h3_scale(1.f, invF);  // P' (fixed-up P: orthonormal columns, |x| <= 1) on 2^14: exact
   const float efinv = e.alpha * invF * invR;
 
   // the EF's fixed operand (P' rows of this wave), loaded before any LDS-DMA is issued
@@ -3519,7 +3628,7 @@ __global__ void __launch_bounds__(256, (RB >= 8 || kCpeRing) ? 2 : 3) colproj_ef
   const float invQ = e.inv[b];
   const float invR = e.inv[nb + b];
   float invF;
-  const float sF = h3_scale(__uint_as_float(e.amax[2 * nb + b]), invF);  // power of two: P' s is exact
+  const float sF = h3_scale(1.f, invF);  // P' (fixed-up P: orthonormal columns, |x| <= 1) on 2^14: exact
   const float efinv = e.alpha * invF * invR;
 
   // fixed EF factor: P'[col_base + 2t + c][32 kk + 8 g ...] (B operand of tile c)
@@ -3740,7 +3849,7 @@ __global__ void __launch_bounds__(512, 1) colproj_efgl_kernel(const EfProjArgs e
   const float invQ = e.inv[b];
   const float invR = e.inv[nb + b];
   float invF;
-  const float sF = h3_scale(__uint_as_float(e.amax[2 * nb + b]), invF);  // power of two: P' s is exact
+  const float sF = h3_scale(1.f, invF);  // P' (fixed-up P: orthonormal columns, |x| <= 1) on 2^14: exact
   const float efinv = e.alpha * invF * invR;
 
   Split2h F[2][KK];
@@ -4336,6 +4445,15 @@ Geo sketch_rad_geo(int mp, int K, int batch) {
 int trsm_rt(int r) { return r <= 32 ? 32 : (r <= 64 ? 64 : 128); }
 size_t factor_floats(int r) { return static_cast<size_t>(trsm_rt(r)) * (trsm_rt(r) + 1); }
 
+// trsm_gram_kernel: 256-row chunks per block (L) so that ~512 blocks cover the batch, and the
+// blocks per matrix (one r x r Gram partial each)
+int trsm_gram_l(int mp, int batch) {
+  const long chunks = ceil_div(mp, 256) * (batch > 0 ? batch : 1);
+  const long l = ceil_div(chunks, 512);
+  return l <= 1 ? 1 : (l <= 2 ? 2 : (l <= 4 ? 4 : 8));
+}
+long trsm_gram_blocks(int mp, int batch) { return ceil_div(ceil_div(mp, 256), trsm_gram_l(mp, batch)); }
+
 struct OrthoPlan {
   bool plain_qr;
   int k;
@@ -4361,7 +4479,8 @@ OrthoPlan ortho_plan(int mp, int r, int batch, float oversample) {
   p.off_sk_slab = take(std::max(slab_bytes(p.sk, batch, r), rad_slab));
   p.off_sp = take(sizeof(float) * static_cast<size_t>(batch) * p.k * r);
   p.off_r1 = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
-  p.off_gslab = take(slab_bytes(p.gr, batch, r));
+  p.off_gslab = take(std::max(slab_bytes(p.gr, batch, r),
+                              sizeof(float) * static_cast<size_t>(batch) * trsm_gram_blocks(mp, batch) * r * r));
   p.off_g = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
   p.off_r2 = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
   p.off_inv = take(sizeof(float) * static_cast<size_t>(batch) * std::max(static_cast<size_t>(r) * r, factor_floats(r)));
@@ -5041,24 +5160,24 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
     uint32_t* amax = nullptr;
     float* inv = nullptr;
     {
-      // fp16x3: per-matrix |max| of Q, R' and P', then the two fp16 limbs of Q and R'
+      // fp16x3: per-matrix |max| of Q and R', then the two fp16 limbs of Q and R'.  P' is the
+      // previous step's fixed-up P, orthonormal columns with |x| <= 1: the kernels split it on
+      // the fixed scale 2^14 (no pass over P' for its maximum)
       char* tail = reinterpret_cast<char*>(rsplit + sstride * nb);
       amax = reinterpret_cast<uint32_t*>(tail);
       inv = reinterpret_cast<float*>(tail + 1024);
-      hipError_t me = hipMemsetAsync(amax, 0, sizeof(uint32_t) * 3 * nb, st);
+      hipError_t me = hipMemsetAsync(amax, 0, sizeof(uint32_t) * 2 * nb, st);
       if (me != hipSuccess) return fail(DION_E_LAUNCH, "memset: %s", hipGetErrorString(me));
       AbsMaxArgs ma;
       memset(&ma, 0, sizeof(ma));
       for (int b = 0; b < nb; ++b) {
         ma.src[b] = Q[b0 + b];
         ma.src[nb + b] = ef->R[b0 + b];
-        ma.src[2 * nb + b] = ef->P[b0 + b];
       }
       ma.out = amax;
       ma.count[0] = ma.count[1] = static_cast<long>(nq) * d->r;
-      ma.count[2] = static_cast<long>(mp) * d->r;
       ma.nb = nb;
-      launch_absmax(ma, 3, st);
+      launch_absmax(ma, 2, st);
       Presplit16Args pa;
       memset(&pa, 0, sizeof(pa));
       pa.rows = nq;
@@ -5252,11 +5371,35 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     rc = launch_sketch_qr_inv(sp, fac, K, r, nb, st, false);
     if (rc != DION_OK) return rc;
     (void)r1;
-    rc = launch_trsm(Pb, p1, fac, mp, r, nb, st);
-    if (rc != DION_OK) return rc;
-    // (4) Gram = P1^T P1, (5) R2 = chol_upper(Gram)
-    rc = run_panel(0, mp, r, r, nb, p1, nullptr, 0, 0.f, gm, gslab, plan.gr, st);
-    if (rc != DION_OK) return rc;
+    if ((r == 32 || r == 64) && d->m_dtype == DION_DTYPE_F32 && aligned16(Pb) && aligned16(p1)) {
+      // (3) + (4): the solve with Gram = P1^T P1 of its rows folded in, block partials reduced
+      // (fp32 state; the bf16 state keeps the panel Gram's summation order)
+      TrsmArgs ta{Pb, p1, fac, nullptr, nullptr, 0, mp, 0};
+      const int L = trsm_gram_l(mp, nb);
+      const dim3 grid(static_cast<unsigned>(trsm_gram_blocks(mp, nb)), nb);
+      auto go = [&](auto Lc) {
+        constexpr int LL = decltype(Lc)::value;
+        if (r == 64)
+          hipLaunchKernelGGL((trsm_gram_kernel<64, LL>), grid, dim3(256), 0, st, ta, gslab);
+        else
+          hipLaunchKernelGGL((trsm_gram_kernel<32, LL>), grid, dim3(256), 0, st, ta, gslab);
+      };
+      if (L == 1) go(std::integral_constant<int, 1>{});
+      else if (L == 2) go(std::integral_constant<int, 2>{});
+      else if (L == 4) go(std::integral_constant<int, 4>{});
+      else go(std::integral_constant<int, 8>{});
+      rc = check_launch("trsm_gram");
+      if (rc != DION_OK) return rc;
+      rc = launch_reduce(gm, gslab, static_cast<int>(grid.x), static_cast<long>(r) * r, nb, st);
+      if (rc != DION_OK) return rc;
+    } else {
+      rc = launch_trsm(Pb, p1, fac, mp, r, nb, st);
+      if (rc != DION_OK) return rc;
+      // (4) Gram = P1^T P1
+      rc = run_panel(0, mp, r, r, nb, p1, nullptr, 0, 0.f, gm, gslab, plan.gr, st);
+      if (rc != DION_OK) return rc;
+    }
+    // (5) R2 = chol_upper(Gram)
     rc = launch_chol_inv(gm, fac, r, nb, st, false);
     if (rc != DION_OK) return rc;
     (void)r2;

@@ -18,8 +18,9 @@ from the same W0, Q0 and gradients with one explicit sketch per (step, matrix), 
     c W + r), and fc1 carries 3 more matrices, a padded batch after its group; deferred EF and
     the 3 AsyncRuntime slot streams as in bench.py.
 
-Tolerance: max |a - b| / max |b| <= 1e-5 for W, M, Q; the weight step alone
-(tests/_metrics.dw_err) <= 5e-6 of its own scale.  W and Q must also be bit-identical across
+Tolerance: max |a - b| / max |b| <= 1e-5 for W, M, Q (Q up to column signs,
+tests/_metrics.q_err: a near-zero Householder pivot of the sketch QR fixes a column's sign by
+rounding); the weight step alone (tests/_metrics.dw_err) <= 5e-6 of its own scale.  W and Q must also be bit-identical across
 the two ranks (replicas).
 """
 import math
@@ -33,7 +34,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from tests._metrics import dw_err
+from tests._metrics import dw_err, q_err
 
 pytestmark = pytest.mark.gpu
 
@@ -144,7 +145,8 @@ def _run_and_check(shapes, r, steps, low_rank, check=None, world=2, opt_kw=None)
             if not key.startswith("hip_s") or key.startswith("hip_sinit"):
                 continue
             ref = R["oracle" + key[3:]]
-            e = (v.double() - ref.double()).abs().max().item() / max(ref.double().abs().max().item(), 1e-30)
+            e = q_err(v, ref) if key.endswith("_Q") else \
+                (v.double() - ref.double()).abs().max().item() / max(ref.double().abs().max().item(), 1e-30)
             worst[key[-1]] = max(worst[key[-1]], e)
             assert e <= TOL, (rank, key, e)
         for s in range(steps):

@@ -643,3 +643,34 @@ def test_split_qkv_and_linear_children_on_device():
         for (n, ph), (_, po) in zip(hn, on_):
             assert maxrel(ph, po) <= 1e-5, (step, n, maxrel(ph, po))
             assert maxrel(hip.state[ph]["momentum"], ora.state[po]["momentum"]) <= 1e-5
+
+
+@pytest.mark.parametrize("m,n,r", [(512, 384, 64), (384, 1024, 64), (2048, 512, 128), (512, 2048, 128)])
+def test_deferred_ef_pending_p_at_the_unit_bound(m, n, r):
+    """The fused pass A splits the pending P' on the fixed scale 2^14 (include/dion_codec.h: P' is
+    the fixed-up P, orthonormal columns, |x| <= 1).  One-hot columns put |x| = 1 exactly, with both
+    signs, and a zero column: M must still match fp64 to the usual bar."""
+    from megatron_dion_amd.codec import HipDionCodec
+
+    dev = _dev()
+    codec = HipDionCodec(dev)
+    transposed = m < n
+    mp, nq = (n, m) if transposed else (m, n)
+    g = torch.Generator().manual_seed(m * 3 + r)
+    Pp = torch.zeros(mp, r)
+    for c in range(r - 1):
+        Pp[(7 * c) % mp, c] = 1.0 if c % 2 == 0 else -1.0
+    M = (torch.randn(m, n, generator=g) * 1e-3).to(dev)
+    G = (torch.randn(m, n, generator=g) * 1e-3).to(torch.bfloat16).to(dev)
+    Q = torch.randn(nq, r, generator=g).to(dev)
+    Rp = (torch.randn(nq, r, generator=g) * 1e-2).to(dev)
+    M0 = M.double().clone()
+    P = torch.zeros(1, mp, r, device=dev)
+    nz = torch.zeros(1, dtype=torch.int32, device=dev)
+    codec.project_p_ef([G], [M], [Q], P, nz, transposed, [Pp.to(dev)], [Rp], -0.05)
+    torch.cuda.synchronize()
+    ef = (Rp.double() @ Pp.double().t().to(dev)) if transposed else (Pp.double().to(dev) @ Rp.double().t())
+    Mref = M0 - 0.05 * ef + G.double()
+    assert maxrel(M, Mref) <= 1e-6, maxrel(M, Mref)
+    Xo = Mref.t() if transposed else Mref
+    assert maxrel(P[0], Xo @ Q.double()) <= 1e-5
