@@ -2114,15 +2114,18 @@ __global__ void __launch_bounds__(NT) chol_reg_kernel(const float* __restrict__ 
 //   x_j = (p_j - sum_{k<j} R_kj x_k) * (1 / R_jj)
 // with the subtractions in k order (right-looking: once x_k is final, every later x_j takes
 // its fused term).  R (the factor kernels' padded RT x RT layout plus reciprocal diagonal)
-// is read with wave-uniform addresses: from global memory for RT <= 64 (the scalar cache
-// holds it), from a per-block LDS copy for RT = 128 (uniform global loads of the 64 KB factor
-// thrash the scalar cache: 361 us per 16-matrix group); the vector traffic is the row in and out.  Columns past r are zero and
-// stay zero.  In place (src == dst) is allowed.
+// is read with wave-uniform addresses from a per-block LDS copy (uniform global loads of the
+// factor thrash the scalar cache: 361 us per 16-matrix group at RT = 128, and at RT = 64 the
+// solve still waited on scalar misses); the vector traffic is the row in and out.  Columns past
+// r are zero and stay zero.  In place (src == dst) is allowed.
 // ============================================================================
 template <int RT>
 __global__ void __launch_bounds__(256) trsm_right_kernel(const float* __restrict__ src, float* __restrict__ dst,
                                                          const float* __restrict__ Rf, int mp, int r) {
-  constexpr bool kLds = RT >= 128;  // RT <= 64: the 16 KB factor stays in the scalar cache
+  // the factor from LDS at every RT: wave-uniform reads are broadcasts there, while the
+  // scalar-cache path (s_load of 2 080 values for RT = 64) left the solve waiting on scalar
+  // misses -- 60 us per Llama launch group against ~12 us of FMA issue (round 5 rocprof)
+  constexpr bool kLds = true;
   __shared__ f32x4 Rs4[kLds ? (RT * RT + RT) / 4 : 1];
   const int b = blockIdx.y;
   const float* R = Rf + static_cast<long>(b) * (RT * RT + RT);
@@ -2203,19 +2206,27 @@ struct TrsmArgs {
   int mp, kmap;
 };
 
+constexpr int kTrsmWaves = 2;  // 128-row blocks: 2 x 16 KB row images + the 16.6 KB factor, 3 blocks per CU
+
 template <int RT, bool FINAL>
-__global__ void __launch_bounds__(256, 2) trsm_lds_kernel(const TrsmArgs a) {
+__global__ void __launch_bounds__(64 * kTrsmWaves, 3) trsm_lds_kernel(const TrsmArgs a) {
   static_assert(RT == 32 || RT == 64, "trsm_lds_kernel: r = 32 or 64");
   constexpr int CH = RT / 4;  // 16-B chunks per row
   constexpr int RB = RT / 16;
-  __shared__ f32x4 img[4][64 * CH];
+  __shared__ f32x4 img[kTrsmWaves][64 * CH];
+  __shared__ f32x4 Rs4[(RT * RT + RT) / 4];  // the factor, read by wave-uniform (broadcast) LDS loads
   const int b = blockIdx.y;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-  const long row0 = static_cast<long>(blockIdx.x) * 256 + wave * 64;
+  const long row0 = static_cast<long>(blockIdx.x) * (64 * kTrsmWaves) + wave * 64;
   const int mp = a.mp;
   const int nrows = static_cast<int>(min(static_cast<long>(64), static_cast<long>(mp) - row0));
+  {
+    const f32x4* Rg = reinterpret_cast<const f32x4*>(a.fac + static_cast<long>(b) * (RT * RT + RT));
+    for (int i = threadIdx.x; i < (RT * RT + RT) / 4; i += 64 * kTrsmWaves) Rs4[i] = Rg[i];
+  }
+  __syncthreads();
   if (nrows <= 0) return;
-  const float* R = a.fac + static_cast<long>(b) * (RT * RT + RT);
+  const float* R = reinterpret_cast<const float*>(Rs4);
   f32x4* w = img[wave];
   const char* s = reinterpret_cast<const char*>(a.src + (static_cast<long>(b) * mp + row0) * RT);
 #pragma unroll
@@ -2280,115 +2291,6 @@ __global__ void __launch_bounds__(256, 2) trsm_lds_kernel(const TrsmArgs a) {
       }
     }
   }
-}
-
-// The first solve of the RCQR (P1 = P R1^-1) with the Gram product of the next step
-// (ortho.py:106-110: Gram = P1^T P1) folded in: trsm_lds_kernel's solve and stores, then each
-// wave adds its 64 finished rows (still in its LDS image) to the Gram on
-// v_mfma_f32_16x16x4f32 (exact fp32 products, as colproj_kernel's panel Gram), so P1 is not read
-// again for it.  A block takes L consecutive 256-row chunks; its 4 waves' Grams are summed in
-// wave order through LDS and the block writes one r x r partial, summed in block order by
-// reduce_slabs_kernel (deterministic).
-template <int RT, int L>
-__global__ void __launch_bounds__(256, 2) trsm_gram_kernel(const TrsmArgs a, float* __restrict__ gslab) {
-  static_assert(RT == 32 || RT == 64, "trsm_gram_kernel: r = 32 or 64");
-  constexpr int CH = RT / 4, RB = RT / 16;
-  __shared__ f32x4 img[4][64 * CH];
-  const int b = blockIdx.y;
-  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-  const int t = lane & 15, g = lane >> 4;
-  const int mp = a.mp;
-  const float* R = a.fac + static_cast<long>(b) * (RT * RT + RT);
-  f32x4* w = img[wave];
-  const float* wf = reinterpret_cast<const float*>(w);
-  f32x4 acc[RB][RB];
-#pragma unroll
-  for (int i = 0; i < RB; ++i)
-#pragma unroll
-    for (int j = 0; j < RB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int it = 0; it < L; ++it) {
-    const long row0 = (static_cast<long>(blockIdx.x) * L + it) * 256 + wave * 64;
-    const int nrows = static_cast<int>(min(static_cast<long>(64), static_cast<long>(mp) - row0));
-    if (nrows <= 0) break;
-    const char* s = reinterpret_cast<const char*>(a.src + (static_cast<long>(b) * mp + row0) * RT);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous chunk's LDS reads are done
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int slot = 64 * i + lane, row = slot / CH, cp = slot % CH;
-      if (row < nrows)
-        glds16<false>(s, static_cast<uint32_t>((row * CH + (cp ^ trsm_swz<RT>(row))) * 16), lds_off(&w[64 * i]));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane < nrows) {
-      float x[RT];
-#pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        const f32x4 v = w[lane * CH + (c ^ trsm_swz<RT>(lane))];
-        x[4 * c] = v[0], x[4 * c + 1] = v[1], x[4 * c + 2] = v[2], x[4 * c + 3] = v[3];
-      }
-#pragma unroll
-      for (int k = 0; k < RT; ++k) {
-        x[k] *= R[RT * RT + k];
-#pragma unroll
-        for (int j = k + 1; j < RT; ++j) x[j] = fmaf(-x[k], R[k * RT + j], x[j]);
-      }
-#pragma unroll
-      for (int c = 0; c < CH; ++c)
-        w[lane * CH + (c ^ trsm_swz<RT>(lane))] = f32x4{x[4 * c], x[4 * c + 1], x[4 * c + 2], x[4 * c + 3]};
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    f32x4* d = reinterpret_cast<f32x4*>(a.dst + (static_cast<long>(b) * mp + row0) * RT);
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int slot = 64 * i + lane, row = slot / CH, cp = slot % CH;
-      if (row < nrows) d[row * CH + (cp ^ trsm_swz<RT>(row))] = w[slot];
-    }
-    // Gram += X^T X over this chunk: tile (i, j), 4 rows per MFMA; lane (t, g) holds row k0 + g
-#pragma unroll 4
-    for (int k0 = 0; k0 < 64; k0 += 4) {
-      const int row = k0 + g;
-      float v[RB];
-#pragma unroll
-      for (int i = 0; i < RB; ++i) {
-        const int col = 16 * i + t;
-        v[i] = row < nrows ? wf[(row * CH + ((col >> 2) ^ trsm_swz<RT>(row))) * 4 + (col & 3)] : 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < RB; ++i)
-#pragma unroll
-        for (int j = 0; j < RB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[i], v[j], acc[i][j], 0, 0, 0);
-    }
-  }
-  // the block's Gram: waves 1..3 add theirs to wave 0's in wave order (LDS), one partial per block
-  float* red = reinterpret_cast<float*>(img[0]);  // RB RB 4 floats per lane, lane-major
-  for (int src = 1; src < 4; ++src) {
-    __syncthreads();
-    if (wave == src) {
-#pragma unroll
-      for (int i = 0; i < RB; ++i)
-#pragma unroll
-        for (int j = 0; j < RB; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) red[((i * RB + j) * 4 + q) * 64 + lane] = acc[i][j][q];
-    }
-    __syncthreads();
-    if (wave == 0) {
-#pragma unroll
-      for (int i = 0; i < RB; ++i)
-#pragma unroll
-        for (int j = 0; j < RB; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc[i][j][q] += red[((i * RB + j) * 4 + q) * 64 + lane];
-    }
-  }
-  if (wave != 0) return;
-  float* out = gslab + (static_cast<long>(b) * gridDim.x + blockIdx.x) * RT * RT;
-#pragma unroll
-  for (int i = 0; i < RB; ++i)
-#pragma unroll
-    for (int j = 0; j < RB; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) out[(16 * i + 4 * g + q) * RT + 16 * j + t] = acc[i][j][q];
 }
 
 // ============================================================================
@@ -4445,15 +4347,6 @@ Geo sketch_rad_geo(int mp, int K, int batch) {
 int trsm_rt(int r) { return r <= 32 ? 32 : (r <= 64 ? 64 : 128); }
 size_t factor_floats(int r) { return static_cast<size_t>(trsm_rt(r)) * (trsm_rt(r) + 1); }
 
-// trsm_gram_kernel: 256-row chunks per block (L) so that ~512 blocks cover the batch, and the
-// blocks per matrix (one r x r Gram partial each)
-int trsm_gram_l(int mp, int batch) {
-  const long chunks = ceil_div(mp, 256) * (batch > 0 ? batch : 1);
-  const long l = ceil_div(chunks, 512);
-  return l <= 1 ? 1 : (l <= 2 ? 2 : (l <= 4 ? 4 : 8));
-}
-long trsm_gram_blocks(int mp, int batch) { return ceil_div(ceil_div(mp, 256), trsm_gram_l(mp, batch)); }
-
 struct OrthoPlan {
   bool plain_qr;
   int k;
@@ -4479,8 +4372,7 @@ OrthoPlan ortho_plan(int mp, int r, int batch, float oversample) {
   p.off_sk_slab = take(std::max(slab_bytes(p.sk, batch, r), rad_slab));
   p.off_sp = take(sizeof(float) * static_cast<size_t>(batch) * p.k * r);
   p.off_r1 = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
-  p.off_gslab = take(std::max(slab_bytes(p.gr, batch, r),
-                              sizeof(float) * static_cast<size_t>(batch) * trsm_gram_blocks(mp, batch) * r * r));
+  p.off_gslab = take(slab_bytes(p.gr, batch, r));
   p.off_g = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
   p.off_r2 = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
   p.off_inv = take(sizeof(float) * static_cast<size_t>(batch) * std::max(static_cast<size_t>(r) * r, factor_floats(r)));
@@ -4811,14 +4703,6 @@ int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t s
 // factor kernels)
 int launch_trsm(const float* src, float* dst, const float* fac, int mp, int r, int batch, hipStream_t st) {
   const dim3 grid(static_cast<unsigned>(ceil_div(mp, 256)), batch);
-  if ((r == 32 || r == 64) && aligned16(src) && aligned16(dst)) {  // rows staged through LDS
-    TrsmArgs a{src, dst, fac, nullptr, nullptr, 0, mp, 0};
-    if (r == 64)
-      hipLaunchKernelGGL((trsm_lds_kernel<64, false>), grid, dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((trsm_lds_kernel<32, false>), grid, dim3(256), 0, st, a);
-    return check_launch("trsm_lds");
-  }
   switch (trsm_rt(r)) {
     case 32: hipLaunchKernelGGL((trsm_right_kernel<32>), grid, dim3(256), 0, st, src, dst, fac, mp, r); break;
     case 64: hipLaunchKernelGGL((trsm_right_kernel<64>), grid, dim3(256), 0, st, src, dst, fac, mp, r); break;
@@ -5371,34 +5255,11 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     rc = launch_sketch_qr_inv(sp, fac, K, r, nb, st, false);
     if (rc != DION_OK) return rc;
     (void)r1;
-    if ((r == 32 || r == 64) && d->m_dtype == DION_DTYPE_F32 && aligned16(Pb) && aligned16(p1)) {
-      // (3) + (4): the solve with Gram = P1^T P1 of its rows folded in, block partials reduced
-      // (fp32 state; the bf16 state keeps the panel Gram's summation order)
-      TrsmArgs ta{Pb, p1, fac, nullptr, nullptr, 0, mp, 0};
-      const int L = trsm_gram_l(mp, nb);
-      const dim3 grid(static_cast<unsigned>(trsm_gram_blocks(mp, nb)), nb);
-      auto go = [&](auto Lc) {
-        constexpr int LL = decltype(Lc)::value;
-        if (r == 64)
-          hipLaunchKernelGGL((trsm_gram_kernel<64, LL>), grid, dim3(256), 0, st, ta, gslab);
-        else
-          hipLaunchKernelGGL((trsm_gram_kernel<32, LL>), grid, dim3(256), 0, st, ta, gslab);
-      };
-      if (L == 1) go(std::integral_constant<int, 1>{});
-      else if (L == 2) go(std::integral_constant<int, 2>{});
-      else if (L == 4) go(std::integral_constant<int, 4>{});
-      else go(std::integral_constant<int, 8>{});
-      rc = check_launch("trsm_gram");
-      if (rc != DION_OK) return rc;
-      rc = launch_reduce(gm, gslab, static_cast<int>(grid.x), static_cast<long>(r) * r, nb, st);
-      if (rc != DION_OK) return rc;
-    } else {
-      rc = launch_trsm(Pb, p1, fac, mp, r, nb, st);
-      if (rc != DION_OK) return rc;
-      // (4) Gram = P1^T P1
-      rc = run_panel(0, mp, r, r, nb, p1, nullptr, 0, 0.f, gm, gslab, plan.gr, st);
-      if (rc != DION_OK) return rc;
-    }
+    rc = launch_trsm(Pb, p1, fac, mp, r, nb, st);
+    if (rc != DION_OK) return rc;
+    // (4) Gram = P1^T P1
+    rc = run_panel(0, mp, r, r, nb, p1, nullptr, 0, 0.f, gm, gslab, plan.gr, st);
+    if (rc != DION_OK) return rc;
     // (5) R2 = chol_upper(Gram)
     rc = launch_chol_inv(gm, fac, r, nb, st, false);
     if (rc != DION_OK) return rc;
@@ -5408,11 +5269,11 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
       TrsmArgs ta{p1, Pb, fac, fuse_fix ? nonzero + b0 : nullptr,
                   p_split != nullptr ? static_cast<f16x8*>(p_split) + static_cast<long>(b0) * mp * r / 4 : nullptr,
                   static_cast<long>(mp) * r / 4, mp, d->transposed ? 1 : 0};
-      const dim3 grid(static_cast<unsigned>(ceil_div(mp, 256)), nb);
+      const dim3 grid(static_cast<unsigned>(ceil_div(mp, 64 * kTrsmWaves)), nb);
       if (r == 64)
-        hipLaunchKernelGGL((trsm_lds_kernel<64, true>), grid, dim3(256), 0, st, ta);
+        hipLaunchKernelGGL((trsm_lds_kernel<64, true>), grid, dim3(64 * kTrsmWaves), 0, st, ta);
       else
-        hipLaunchKernelGGL((trsm_lds_kernel<32, true>), grid, dim3(256), 0, st, ta);
+        hipLaunchKernelGGL((trsm_lds_kernel<32, true>), grid, dim3(64 * kTrsmWaves), 0, st, ta);
       rc = check_launch("trsm_lds(final)");
     } else {
       rc = launch_trsm(p1, Pb, fac, mp, r, nb, st);
