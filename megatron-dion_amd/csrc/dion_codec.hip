@@ -1291,6 +1291,11 @@ struct FixArgs {
   float eps;
 };
 
+// rows of R per fix-up block: 64 (was 256) gives 4x the blocks, so the fix-up and the column
+// norm, latency-bound row loops of 256 / r rows per thread, run wide (they sit on the
+// critical path between pass B and the weight update of every launch group)
+constexpr int kFixRows = 64;
+
 // phase 1: fix R rows of one chunk and write its column partial sums
 __global__ void __launch_bounds__(256) fixup_partial_kernel(const FixArgs a) {
   __shared__ float red[256];
@@ -4925,7 +4930,7 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
       }
       case DION_OP_FIXUP_COLNORM: {
         const int nq = d->transposed ? d->m : d->n;
-        n = sizeof(float) * static_cast<size_t>(chunk) * ceil_div(nq, 256) * d->r;
+        n = sizeof(float) * static_cast<size_t>(chunk) * ceil_div(nq, kFixRows) * d->r;
         break;
       }
       default:
@@ -5411,7 +5416,7 @@ int dion_fixup_colnorm(const DionBatchDesc* d, float* P, float* R, float* const*
     a.nq = nq;
     a.r = r;
     a.tpc = 256 / r;
-    a.rows_per_chunk = 256;
+    a.rows_per_chunk = kFixRows;
     a.nchunk = static_cast<int>(ceil_div(nq, a.rows_per_chunk));
     if (ws_bytes < sizeof(float) * static_cast<size_t>(nb) * a.nchunk * r || ws == nullptr)
       return fail(DION_E_WORKSPACE, "fixup needs %zu workspace bytes", sizeof(float) * static_cast<size_t>(nb) * a.nchunk * r);
@@ -5460,7 +5465,7 @@ int dion_fixup_colsum(const DionBatchDesc* d, float* P, float* R, const void* co
     a.nq = nq;
     a.r = r;
     a.tpc = 256 / r;
-    a.rows_per_chunk = 256;
+    a.rows_per_chunk = kFixRows;
     a.nchunk = static_cast<int>(ceil_div(nq, a.rows_per_chunk));
     if (ws_bytes < sizeof(float) * static_cast<size_t>(nb) * a.nchunk * r || ws == nullptr)
       return fail(DION_E_WORKSPACE, "fixup needs %zu workspace bytes", sizeof(float) * static_cast<size_t>(nb) * a.nchunk * r);
@@ -5497,7 +5502,7 @@ int dion_colnorm_apply(const DionBatchDesc* d, const float* R, void* const* Q, c
     a.nq = nq;
     a.r = r;
     a.tpc = 256 / r;
-    a.rows_per_chunk = 256;
+    a.rows_per_chunk = kFixRows;
     a.nchunk = static_cast<int>(ceil_div(nq, a.rows_per_chunk));
     a.eps = eps;
     hipLaunchKernelGGL(colnorm_given_kernel, dim3(a.nchunk, nb), dim3(256), 0, st, a,
