@@ -2119,18 +2119,17 @@ __global__ void __launch_bounds__(NT) chol_reg_kernel(const float* __restrict__ 
 //   x_j = (p_j - sum_{k<j} R_kj x_k) * (1 / R_jj)
 // with the subtractions in k order (right-looking: once x_k is final, every later x_j takes
 // its fused term).  R (the factor kernels' padded RT x RT layout plus reciprocal diagonal)
-// is read with wave-uniform addresses from a per-block LDS copy (uniform global loads of the
-// factor thrash the scalar cache: 361 us per 16-matrix group at RT = 128, and at RT = 64 the
-// solve still waited on scalar misses); the vector traffic is the row in and out.  Columns past
-// r are zero and stay zero.  In place (src == dst) is allowed.
+// is read with wave-uniform addresses: from global memory for RT <= 64 (scalar loads), from a
+// per-block LDS copy for RT = 128 (uniform global loads of the 64 KB factor thrash the scalar
+// cache: 361 us per 16-matrix group); the vector traffic is the row in and out.  Columns past r
+// are zero and stay zero.  In place (src == dst) is allowed.
 // ============================================================================
 template <int RT>
 __global__ void __launch_bounds__(256) trsm_right_kernel(const float* __restrict__ src, float* __restrict__ dst,
                                                          const float* __restrict__ Rf, int mp, int r) {
-  // the factor from LDS at every RT: wave-uniform reads are broadcasts there, while the
-  // scalar-cache path (s_load of 2 080 values for RT = 64) left the solve waiting on scalar
-  // misses -- 60 us per Llama launch group against ~12 us of FMA issue (round 5 rocprof)
-  constexpr bool kLds = true;
+  // RT <= 64: the factor by wave-uniform global (scalar) loads; from LDS it measured slower
+  // (fc1 group 79.5 vs 129 us, scripts/ubench/trsm_ab.hip, profiles/r05/i_trsm_variants.txt)
+  constexpr bool kLds = RT >= 128;
   __shared__ f32x4 Rs4[kLds ? (RT * RT + RT) / 4 : 1];
   const int b = blockIdx.y;
   const float* R = Rf + static_cast<long>(b) * (RT * RT + RT);
@@ -2211,7 +2210,7 @@ struct TrsmArgs {
   int mp, kmap;
 };
 
-constexpr int kTrsmWaves = 2;  // 128-row blocks: 2 x 16 KB row images + the 16.6 KB factor, 3 blocks per CU
+constexpr int kTrsmWaves = 2;  // 128-row blocks: 2 x 16 KB row images
 
 template <int RT, bool FINAL>
 __global__ void __launch_bounds__(64 * kTrsmWaves, 3) trsm_lds_kernel(const TrsmArgs a) {
@@ -2219,19 +2218,13 @@ __global__ void __launch_bounds__(64 * kTrsmWaves, 3) trsm_lds_kernel(const Trsm
   constexpr int CH = RT / 4;  // 16-B chunks per row
   constexpr int RB = RT / 16;
   __shared__ f32x4 img[kTrsmWaves][64 * CH];
-  __shared__ f32x4 Rs4[(RT * RT + RT) / 4];  // the factor, read by wave-uniform (broadcast) LDS loads
   const int b = blockIdx.y;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const long row0 = static_cast<long>(blockIdx.x) * (64 * kTrsmWaves) + wave * 64;
   const int mp = a.mp;
   const int nrows = static_cast<int>(min(static_cast<long>(64), static_cast<long>(mp) - row0));
-  {
-    const f32x4* Rg = reinterpret_cast<const f32x4*>(a.fac + static_cast<long>(b) * (RT * RT + RT));
-    for (int i = threadIdx.x; i < (RT * RT + RT) / 4; i += 64 * kTrsmWaves) Rs4[i] = Rg[i];
-  }
-  __syncthreads();
   if (nrows <= 0) return;
-  const float* R = reinterpret_cast<const float*>(Rs4);
+  const float* R = a.fac + static_cast<long>(b) * (RT * RT + RT);  // wave-uniform (scalar) loads
   f32x4* w = img[wave];
   const char* s = reinterpret_cast<const char*>(a.src + (static_cast<long>(b) * mp + row0) * RT);
 #pragma unroll
