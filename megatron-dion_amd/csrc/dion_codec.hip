@@ -2124,12 +2124,16 @@ __global__ void __launch_bounds__(NT) chol_reg_kernel(const float* __restrict__ 
 // cache: 361 us per 16-matrix group); the vector traffic is the row in and out.  Columns past r
 // are zero and stay zero.  In place (src == dst) is allowed.
 // ============================================================================
+#ifndef DION_TRSM_LDS_MIN_RT
+#define DION_TRSM_LDS_MIN_RT 128  // the smallest padded order whose solve stages the factor in LDS
+#endif
 template <int RT>
 __global__ void __launch_bounds__(256) trsm_right_kernel(const float* __restrict__ src, float* __restrict__ dst,
-                                                         const float* __restrict__ Rf, int mp, int r) {
+                                                         const float* __restrict__ Rf, int mp, int r,
+                                                         const uint32_t* __restrict__ nonzero) {
   // RT <= 64: the factor by wave-uniform global (scalar) loads; from LDS it measured slower
-  // (fc1 group 79.5 vs 129 us, scripts/ubench/trsm_ab.hip, profiles/r05/i_trsm_variants.txt)
-  constexpr bool kLds = RT >= 128;
+  // alone (fc1 group 79.5 vs 129 us, scripts/ubench/trsm_ab.hip, profiles/r05/i_trsm_variants.txt)
+  constexpr bool kLds = RT >= DION_TRSM_LDS_MIN_RT;
   __shared__ f32x4 Rs4[kLds ? (RT * RT + RT) / 4 : 1];
   const int b = blockIdx.y;
   const float* R = Rf + static_cast<long>(b) * (RT * RT + RT);
@@ -2162,6 +2166,12 @@ __global__ void __launch_bounds__(256) trsm_right_kernel(const float* __restrict
     x[k] *= R[RT * RT + k];
 #pragma unroll
     for (int j = k + 1; j < RT; ++j) x[j] = fmaf(-x[k], R[k * RT + j], x[j]);
+  }
+  if (nonzero != nullptr) {
+    // the last solve of the RCQR with pfix_kernel folded in (kernels.py:185-188)
+    const bool zero = nonzero[b] == 0u;
+#pragma unroll
+    for (int j = 0; j < RT; ++j) x[j] = zero ? 0.f : nan_to_num(x[j]);
   }
   float* q = dst + (static_cast<long>(b) * mp + row) * r;
   if ((r & 3) == 0) {
@@ -2218,13 +2228,22 @@ __global__ void __launch_bounds__(64 * kTrsmWaves, 3) trsm_lds_kernel(const Trsm
   constexpr int CH = RT / 4;  // 16-B chunks per row
   constexpr int RB = RT / 16;
   __shared__ f32x4 img[kTrsmWaves][64 * CH];
+  // the factor as in trsm_right_kernel: scalar loads, or a per-block LDS copy
+  constexpr bool kLds = RT >= DION_TRSM_LDS_MIN_RT;
+  __shared__ f32x4 Rs4[kLds ? (RT * RT + RT) / 4 : 1];
   const int b = blockIdx.y;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const long row0 = static_cast<long>(blockIdx.x) * (64 * kTrsmWaves) + wave * 64;
   const int mp = a.mp;
   const int nrows = static_cast<int>(min(static_cast<long>(64), static_cast<long>(mp) - row0));
-  if (nrows <= 0) return;
   const float* R = a.fac + static_cast<long>(b) * (RT * RT + RT);  // wave-uniform (scalar) loads
+  if constexpr (kLds) {
+    const f32x4* Rg = reinterpret_cast<const f32x4*>(R);
+    for (int i = threadIdx.x; i < (RT * RT + RT) / 4; i += 64 * kTrsmWaves) Rs4[i] = Rg[i];
+    __syncthreads();
+    R = reinterpret_cast<const float*>(Rs4);
+  }
+  if (nrows <= 0) return;
   f32x4* w = img[wave];
   const char* s = reinterpret_cast<const char*>(a.src + (static_cast<long>(b) * mp + row0) * RT);
 #pragma unroll
@@ -2301,10 +2320,11 @@ __global__ void __launch_bounds__(64 * kTrsmWaves, 3) trsm_lds_kernel(const Trsm
 // split, P is split into three bf16 limbs (24 bits), and S P is three bf16 MFMAs per tile
 // instead of the fp32 MFMA (16x slower) with a Box-Muller draw per element.
 //   v_mfma_f32_32x32x16_bf16: A = S tile (32 sketch rows x 16 P rows, from the sign
-//   bits), B = P tile (16 rows x 32 columns, 8 rows of one column per lane, coalesced
-//   across the 32 lanes of a row).  A block takes kchunk rows of one matrix; wave w owns
-//   sketch-row tiles w, w + 4 (KT4 of them) and all NT column tiles, so no cross-wave
-//   reduction; partial sums go to fixed-order slabs (reduce_slabs_kernel).
+//   bits), B = P tile (16 rows x 32 columns, 8 rows of one column per lane).  A block takes
+//   kchunk rows of one matrix in 32-row panels, each loaded once (16-byte loads, one panel
+//   ahead) into LDS for all four waves; wave w owns sketch-row tiles w, w + 4 (KT4 of them)
+//   and all NT column tiles, so no cross-wave reduction; partial sums go to fixed-order
+//   slabs (reduce_slabs_kernel).
 // ============================================================================
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
@@ -2332,13 +2352,16 @@ struct SketchArgs {
   uint64_t seed;
   float scale;      // 1 / sqrt(K)
   int mp, r, K, kchunk, nchunk;
+  int vec;          // P 16-byte aligned and r % 4 == 0
 };
 
 template <int KT4, int NT>
-__global__ void __launch_bounds__(256) sketch_rad_kernel(const SketchArgs a) {
+__global__ void __launch_bounds__(256, 2) sketch_rad_kernel(const SketchArgs a) {
+  constexpr int R = 32 * NT;  // the column tiles (r <= R; the tile's columns past r are zero)
+  __shared__ __attribute__((aligned(16))) float tile[2][32 * R];
   const int b = blockIdx.y, chunk = blockIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63, t = lane & 31, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, t = lane & 31, h = lane >> 5;
   const int i_begin = chunk * a.kchunk;
   const int i_end = min(a.mp, i_begin + a.kchunk);
   const int r = a.r;
@@ -2355,30 +2378,62 @@ __global__ void __launch_bounds__(256) sketch_rad_kernel(const SketchArgs a) {
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[q][nt][e] = 0.f;
-  for (int i0 = i_begin; i0 < i_end; i0 += 16) {
-    Split3 B[NT];
+  // the 32-row panel P[i0 .. i0 + 31][0 .. r) staged through LDS once per block (one 16-byte
+  // slot per thread and column tile), loaded one panel ahead; rows past i_end are zero
+  f32x4 pre[NT];
+  auto load = [&](int i0) {
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int col = 32 * nt + t;
-      float v[8];
+    for (int v = 0; v < NT; ++v) {
+      const int idx = tid + 256 * v, row = i0 + idx / (R / 4), c = 4 * (idx % (R / 4));
+      if (row < i_end && a.vec && c < r) {
+        pre[v] = *reinterpret_cast<const f32x4*>(Pb + static_cast<long>(row) * r + c);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int row = i0 + 8 * h + j;
-        v[j] = (row < i_end && col < r) ? Pb[static_cast<long>(row) * r + col] : 0.f;
+        for (int e = 0; e < 4; ++e) pre[v][e] = (row < i_end && c + e < r) ? Pb[static_cast<long>(row) * r + c + e] : 0.f;
       }
-      split3(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, 1.f, B[nt]);
     }
+  };
+  auto store = [&](int buf) {
 #pragma unroll
-    for (int q = 0; q < KT4; ++q) {
-      const uint32_t bits = hash32(hk[q] ^ (0xC2B2AE35u * static_cast<uint32_t>(i0 >> 5)));
-      const bf16x8 S = signs_bf16x8(bits >> ((i0 & 16) + 8 * h));
+    for (int v = 0; v < NT; ++v) reinterpret_cast<f32x4*>(tile[buf])[tid + 256 * v] = pre[v];
+  };
+  if (i_begin >= i_end) return;
+  load(i_begin);
+  store(0);
+  __syncthreads();
+  int cur = 0;
+  for (int i0 = i_begin; i0 < i_end; i0 += 32) {
+    const bool more = i0 + 32 < i_end;
+    if (more) load(i0 + 32);
+    uint32_t bits[KT4];
+#pragma unroll
+    for (int q = 0; q < KT4; ++q) bits[q] = hash32(hk[q] ^ (0xC2B2AE35u * static_cast<uint32_t>(i0 >> 5)));
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+      bf16x8 S[KT4];
+#pragma unroll
+      for (int q = 0; q < KT4; ++q) S[q] = signs_bf16x8(bits[q] >> (16 * half + 8 * h));
+      // one column tile at a time (all NT split tiles live would cost a wave per SIMD at
+      // r = 128); the KT4 accumulators of a limb are independent MFMAs
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        acc[q][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(S, B[nt].lo, acc[q][nt], 0, 0, 0);
-        acc[q][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(S, B[nt].mid, acc[q][nt], 0, 0, 0);
-        acc[q][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(S, B[nt].hi, acc[q][nt], 0, 0, 0);
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = tile[cur][(16 * half + 8 * h + j) * R + 32 * nt + t];
+        Split3 B;
+        split3(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, 1.f, B);
+#pragma unroll
+        for (int q = 0; q < KT4; ++q) acc[q][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(S[q], B.lo, acc[q][nt], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < KT4; ++q) acc[q][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(S[q], B.mid, acc[q][nt], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < KT4; ++q) acc[q][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(S[q], B.hi, acc[q][nt], 0, 0, 0);
       }
     }
+    if (!more) break;
+    store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
   }
   float* out = a.out + (static_cast<long>(b) * a.nchunk + chunk) * a.K * r;
 #pragma unroll
@@ -2742,6 +2797,114 @@ __device__ __forceinline__ f32x4 mfma3h(const Split2h& A, const Split2h& B, f32x
 __device__ __forceinline__ float max8abs(const f32x4& a, const f32x4& b) {
   return fmaxf(fmaxf(fmaxf(fabsf(a[0]), fabsf(a[1])), fmaxf(fabsf(a[2]), fabsf(a[3]))),
                fmaxf(fmaxf(fabsf(b[0]), fabsf(b[1])), fmaxf(fabsf(b[2]), fabsf(b[3]))));
+}
+
+// ============================================================================
+// Gram G_b = P1_b^T P1_b of the randomised Cholesky QR (ortho.py:110, P.mT @ P in fp32) on
+// fp16x3 MFMAs, for r = 16 RB = 64 or 128.  A block owns a chunk of rows (its slab of partial
+// sums goes through reduce_slabs_kernel) and steps it 32 rows at a time: the 32 x r panel is
+// staged through LDS (row pad 2: the two 16-lane groups of a ds_read_b32 half land on
+// opposite bank halves), then every wave reads lane (t, g) = rows 8g .. 8g + 7 of column
+// 16 cb + t for every column block cb -- the A operand of block cb is the B operand of
+// block cb, so one split serves both -- and takes the panel's max |x| (the same in every
+// wave) for a power-of-two scale s.  Wave w accumulates the output rows of column blocks
+// RB/4 w .. + RB/4 - 1 against every cb: three fp16 MFMAs per 16 x 16 tile into a zero
+// accumulator, added with the step's 1/s twice (1/s^2 may underflow where the products do
+// not).  Per product the dropped lo*lo term and the fp16 rounding of lo are 2^-22 of |x s||y s|,
+// against fp32's 2^-24 per product.
+// ============================================================================
+struct GramArgs {
+  const float* p;  // batch x mp x r, contiguous (the orthonormalisation's P1 workspace)
+  float* out;      // batch x nchunk x r x r partial sums (nchunk 1: the Gram itself)
+  int mp, kchunk, nchunk;
+};
+
+template <int RB>
+__global__ void __launch_bounds__(256, 2) gram_h3_kernel(const GramArgs a) {
+  constexpr int R = 16 * RB;
+  constexpr int LD = R + 2;
+  constexpr int TA = RB / 4;             // output column blocks per wave
+  constexpr int NV = 32 * R / 4 / 256;   // 16-byte loads per thread per 32-row step
+  __shared__ __attribute__((aligned(16))) float tile[2][32 * LD];
+  const int b = blockIdx.y, kc = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, t = lane & 15, g = lane >> 4;
+  const float* __restrict__ P = a.p + static_cast<long>(b) * a.mp * R;
+  const int i_begin = kc * a.kchunk;
+  const int i_end = min(a.mp, i_begin + a.kchunk);
+  f32x4 acc[TA][RB];
+#pragma unroll
+  for (int ta = 0; ta < TA; ++ta)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[ta][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 pre[NV];
+  auto load = [&](int i0) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = tid + 256 * v, row = idx / (R / 4), c4 = idx % (R / 4);
+      pre[v] = *reinterpret_cast<const f32x4*>(P + static_cast<long>(i0 + row) * R + 4 * c4);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = tid + 256 * v, row = idx / (R / 4), c4 = idx % (R / 4);
+      f32x2* d = reinterpret_cast<f32x2*>(&tile[buf][row * LD + 4 * c4]);  // 8-byte aligned (LD even)
+      d[0] = f32x2{pre[v][0], pre[v][1]};
+      d[1] = f32x2{pre[v][2], pre[v][3]};
+    }
+  };
+  if (i_begin >= i_end) return;
+  load(i_begin);
+  store(0);
+  __syncthreads();
+  int cur = 0;
+  for (int i0 = i_begin; i0 < i_end; i0 += 32) {
+    const bool more = i0 + 32 < i_end;
+    if (more) load(i0 + 32);
+    f32x4 v[RB][2];
+    float m = 0.f;
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[cb][e >> 2][e & 3] = tile[cur][(8 * g + e) * LD + 16 * cb + t];
+      m = fmaxf(m, max8abs(v[cb][0], v[cb][1]));
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    float inv;
+    const float s = h3_scale(m, inv);
+    Split2h S[RB];
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) split2h(v[cb][0], v[cb][1], s, S[cb]);
+    // this wave's A operands (a register array indexed by the wave number would go to scratch)
+    Split2h A[TA];
+#pragma unroll
+    for (int ta = 0; ta < TA; ++ta)
+#pragma unroll
+      for (int cb = ta; cb < RB; cb += TA)
+        if (cb == wave * TA + ta) A[ta] = S[cb];
+#pragma unroll
+    for (int ta = 0; ta < TA; ++ta) {
+#pragma unroll
+      for (int cb = 0; cb < RB; ++cb) {
+        const f32x4 d = mfma3h(A[ta], S[cb], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[ta][cb][q] = fmaf(d[q] * inv, inv, acc[ta][cb][q]);
+      }
+    }
+    if (!more) break;
+    store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // lane (t, g), element q: G[16 (TA w + ta) + 4 g + q][16 cb + t]
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * R * R;
+#pragma unroll
+  for (int ta = 0; ta < TA; ++ta)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) out[(16 * (TA * wave + ta) + 4 * g + q) * R + 16 * cb + t] = acc[ta][cb][q];
 }
 
 // per-matrix max |x| of a small factor (rows x r fp32), as the float's bit pattern
@@ -4327,17 +4490,35 @@ int sketch_k(int r, float oversample) {
   return static_cast<int>(ceil(static_cast<double>(oversample) * r / 128.0)) * 128;
 }
 
-// sketch_rad_kernel: ~512 blocks over the batch (2 per CU), 16-row aligned row chunks
+// sketch_rad_kernel: ~512 blocks over the batch (2 per CU), 32-row aligned row chunks
 Geo sketch_rad_geo(int mp, int K, int batch) {
   Geo g;
   const long want = ceil_div(512L, batch > 0 ? batch : 1);
   const long maxc = ceil_div(mp, 256);
   long nc = want < maxc ? want : maxc;
   if (nc < 1) nc = 1;
-  g.kchunk = round_up(ceil_div(mp, nc), 16);
+  g.kchunk = round_up(ceil_div(mp, nc), 32);
   g.nchunk = static_cast<int>(ceil_div(mp, g.kchunk));
   g.gx = g.nchunk;
   g.out_rows = K;
+  return g;
+}
+
+// the orthonormalisation's Gram on gram_h3_kernel (r = 64 or 128, m_P % 32 == 0) instead of
+// the fp32 panel kernel
+constexpr int kGramH3 = 1;
+bool gram_h3_ok(int mp, int r) { return kGramH3 && (r == 64 || r == 128) && mp % 32 == 0; }
+// ~512 blocks over the batch (2 per CU), 32-row aligned chunks of >= 128 rows
+Geo gram_geo(int mp, int r, int batch) {
+  Geo g;
+  const long want = ceil_div(512L, batch > 0 ? batch : 1);
+  const long maxc = ceil_div(mp, 128);
+  long nc = want < maxc ? want : maxc;
+  if (nc < 1) nc = 1;
+  g.kchunk = round_up(ceil_div(mp, nc), 32);
+  g.nchunk = static_cast<int>(ceil_div(mp, g.kchunk));
+  g.gx = g.nchunk;
+  g.out_rows = r;
   return g;
 }
 
@@ -4358,7 +4539,7 @@ OrthoPlan ortho_plan(int mp, int r, int batch, float oversample) {
   p.k = sketch_k(r, oversample);
   if (p.plain_qr) return p;
   p.sk = colproj_geo(mp, p.k, batch, true);
-  p.gr = colproj_geo(mp, r, batch, true);
+  p.gr = gram_h3_ok(mp, r) ? gram_geo(mp, r, batch) : colproj_geo(mp, r, batch, true);
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -4699,12 +4880,13 @@ int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t s
 
 // dst_b = src_b R_b^-1 by forward substitution (trsm_right_kernel; factor from the INV = false
 // factor kernels)
-int launch_trsm(const float* src, float* dst, const float* fac, int mp, int r, int batch, hipStream_t st) {
+int launch_trsm(const float* src, float* dst, const float* fac, int mp, int r, int batch, hipStream_t st,
+                const uint32_t* nonzero = nullptr) {
   const dim3 grid(static_cast<unsigned>(ceil_div(mp, 256)), batch);
   switch (trsm_rt(r)) {
-    case 32: hipLaunchKernelGGL((trsm_right_kernel<32>), grid, dim3(256), 0, st, src, dst, fac, mp, r); break;
-    case 64: hipLaunchKernelGGL((trsm_right_kernel<64>), grid, dim3(256), 0, st, src, dst, fac, mp, r); break;
-    default: hipLaunchKernelGGL((trsm_right_kernel<128>), grid, dim3(256), 0, st, src, dst, fac, mp, r); break;
+    case 32: hipLaunchKernelGGL((trsm_right_kernel<32>), grid, dim3(256), 0, st, src, dst, fac, mp, r, nonzero); break;
+    case 64: hipLaunchKernelGGL((trsm_right_kernel<64>), grid, dim3(256), 0, st, src, dst, fac, mp, r, nonzero); break;
+    default: hipLaunchKernelGGL((trsm_right_kernel<128>), grid, dim3(256), 0, st, src, dst, fac, mp, r, nonzero); break;
   }
   return check_launch("trsm_right");
 }
@@ -4724,6 +4906,7 @@ int run_sketch_rad(const float* P, int mp, int K, int r, int batch, uint64_t see
   a.K = K;
   a.kchunk = g.kchunk;
   a.nchunk = g.nchunk;
+  a.vec = (r % 4 == 0 && aligned16(P)) ? 1 : 0;
   const dim3 grid(static_cast<unsigned>(g.nchunk), batch);
   auto go = [&](auto KTc, auto NTc) {
     constexpr int KT = decltype(KTc)::value, NT = decltype(NTc)::value;
@@ -5203,10 +5386,11 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int mp = d->transposed ? d->n : d->m;
   const int r = d->r;
-  // the fix-up of P rides on the last solve when it is the LDS solve of an fp32 P; elsewhere
-  // (plain QR, other r, bf16 rounding) pfix_kernel runs after the orthonormalisation
-  const bool fuse_fix = nonzero != nullptr && d->m_dtype == DION_DTYPE_F32 && (r == 32 || r == 64) && mp > r &&
-                        aligned16(P);
+  // the fix-up of P rides on the last solve of an fp32 P (the LDS solve at r = 32 / 64 with
+  // an aligned P, else trsm_right_kernel); elsewhere (plain QR, bf16 rounding first)
+  // pfix_kernel runs after the orthonormalisation
+  const bool fuse_fix = nonzero != nullptr && d->m_dtype == DION_DTYPE_F32 && mp > r;
+  const bool lds_fix = fuse_fix && (r == 32 || r == 64) && aligned16(P);
   for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
     const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
     float* Pb = P + static_cast<long>(b0) * mp * r;
@@ -5256,14 +5440,25 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     rc = launch_trsm(Pb, p1, fac, mp, r, nb, st);
     if (rc != DION_OK) return rc;
     // (4) Gram = P1^T P1
-    rc = run_panel(0, mp, r, r, nb, p1, nullptr, 0, 0.f, gm, gslab, plan.gr, st);
+    if (gram_h3_ok(mp, r)) {
+      const GramArgs ga{p1, plan.gr.nchunk > 1 ? gslab : gm, mp, plan.gr.kchunk, plan.gr.nchunk};
+      if (r == 64)
+        hipLaunchKernelGGL((gram_h3_kernel<4>), dim3(plan.gr.nchunk, nb), dim3(256), 0, st, ga);
+      else
+        hipLaunchKernelGGL((gram_h3_kernel<8>), dim3(plan.gr.nchunk, nb), dim3(256), 0, st, ga);
+      rc = check_launch("gram_h3");
+      if (rc == DION_OK && plan.gr.nchunk > 1)
+        rc = launch_reduce(gm, gslab, plan.gr.nchunk, static_cast<long>(r) * r, nb, st);
+    } else {
+      rc = run_panel(0, mp, r, r, nb, p1, nullptr, 0, 0.f, gm, gslab, plan.gr, st);
+    }
     if (rc != DION_OK) return rc;
     // (5) R2 = chol_upper(Gram)
     rc = launch_chol_inv(gm, fac, r, nb, st, false);
     if (rc != DION_OK) return rc;
     (void)r2;
     // (6) P = P1 R2^-1 (back into the caller's buffer), with the fix-up and pass B's split
-    if (fuse_fix || p_split != nullptr) {
+    if (lds_fix || p_split != nullptr) {
       TrsmArgs ta{p1, Pb, fac, fuse_fix ? nonzero + b0 : nullptr,
                   p_split != nullptr ? static_cast<f16x8*>(p_split) + static_cast<long>(b0) * mp * r / 4 : nullptr,
                   static_cast<long>(mp) * r / 4, mp, d->transposed ? 1 : 0};
@@ -5274,7 +5469,7 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
         hipLaunchKernelGGL((trsm_lds_kernel<32, true>), grid, dim3(64 * kTrsmWaves), 0, st, ta);
       rc = check_launch("trsm_lds(final)");
     } else {
-      rc = launch_trsm(p1, Pb, fac, mp, r, nb, st);
+      rc = launch_trsm(p1, Pb, fac, mp, r, nb, st, fuse_fix ? nonzero + b0 : nullptr);
     }
     if (rc != DION_OK) return rc;
   }

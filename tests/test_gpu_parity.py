@@ -674,3 +674,38 @@ def test_deferred_ef_pending_p_at_the_unit_bound(m, n, r):
     assert maxrel(M, Mref) <= 1e-6, maxrel(M, Mref)
     Xo = Mref.t() if transposed else Mref
     assert maxrel(P[0], Xo @ Q.double()) <= 1e-5
+
+
+# ---------------------------------------------------------------------------------------------- Gram
+@pytest.mark.parametrize("mp,r,decades", [(4096, 64, 0), (4096, 64, 3), (2048, 128, 0), (2048, 128, 3),
+                                          (6144, 128, 1)])
+def test_orthonormalize_h3_gram_matches_oracle(mp, r, decades):
+    """The Gram of the randomised Cholesky QR runs on fp16x3 MFMAs at r = 64 / 128 and
+    m_P % 32 == 0 (gram_h3_kernel): with the same sketch the orthonormalised P matches the
+    oracle's fp32 arithmetic (dion/ortho.py:71-123) up to column signs, and P^T P = I to fp32
+    level, on P whose columns span `decades` decades of scale."""
+    from megatron_dion_amd.codec import HipDionCodec
+
+    dev = _dev()
+    B = 3
+    gen = torch.Generator().manual_seed(mp + r + decades)
+    U = torch.linalg.qr(torch.randn(B, mp, r, generator=gen, dtype=torch.float64))[0]
+    V = torch.linalg.qr(torch.randn(B, r, r, generator=gen, dtype=torch.float64))[0]
+    s = torch.logspace(0, -decades, r, dtype=torch.float64)
+    P0 = ((U * s) @ V.transpose(1, 2) * 1e-2).float()
+    k = O.sketch_rows(r)
+    sk = torch.randn(B, k, mp, generator=gen) * math.sqrt(1.0 / k)
+    codec = HipDionCodec(dev)
+    P = P0.to(dev)
+    codec.orthonormalize(P, mp, mp // 2, False, seed=7, sketch=sk.to(dev))
+    torch.cuda.synchronize()
+    got = P.cpu()
+    ref = torch.cat([O.orthogonalize(P0[b:b + 1], 1.25, sketch=sk[b:b + 1]) for b in range(B)]).float()
+    worst_p, worst_i = 0.0, 0.0
+    for b in range(B):
+        worst_p = max(worst_p, maxrel(sign_align(got[b], ref[b]), ref[b]))
+        G = got[b].double().t() @ got[b].double()
+        worst_i = max(worst_i, (G - torch.eye(r, dtype=torch.float64)).abs().max().item())
+    print(f"mp={mp} r={r} decades={decades}: P maxrel vs oracle {worst_p:.3e}, |P^T P - I| {worst_i:.3e}")
+    assert worst_i <= 2e-6, worst_i
+    assert worst_p <= 1e-5 * 10 ** decades, worst_p
