@@ -113,7 +113,8 @@ class TimedCodec:
 
     def __getattr__(self, item):
         fn = getattr(self.inner, item)
-        if item not in ("project_p", "project_p_ef", "orthonormalize", "project_r", "fixup_colnorm", "ef_apply"):
+        if item not in ("project_p", "project_p_ef", "orthonormalize", "project_r", "project_r_fixup", "fixup_colnorm",
+                        "ef_apply"):
             return fn
 
         def wrapped(*args, **kwargs):
@@ -128,6 +129,8 @@ class TimedCodec:
             key = item
             if item == "ef_apply" and args[0] is None:
                 key = "ef_apply_w"
+            if item == "project_r_fixup":
+                key = "project_r"  # pass B with the fix-up on its reduction (W = 1, fp32 state)
             transposed = None
             if key in BYTES_PER_ELEM:
                 transposed = bool(args[5] if item == "project_p_ef" else args[-1])

@@ -43,7 +43,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 14
+#define DION_ABI_VERSION 15
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -218,6 +218,16 @@ int dion_orthonormalize_fused(const DionBatchDesc* desc, float* P, const float* 
 int dion_project_r_split(const DionBatchDesc* desc, const float* const* M, const float* P,
                          const void* p_split, float* R, const uint32_t* m_absmax, void* ws,
                          size_t ws_bytes, dion_stream_t stream);
+/*
+ * dion_project_r_fixup: dion_project_r_split, then dion_fixup_colnorm with P = NULL (the P
+ * half done by dion_orthonormalize_fused), bitwise; the fix-up's first phase rides on pass
+ * B's split-K reduction.  fp32 state only (DION_E_UNSUPPORTED otherwise, nothing enqueued);
+ * scratch = dion_workspace_bytes(DION_OP_PROJECT_R), which includes the fix-up's partials.
+ */
+int dion_project_r_fixup(const DionBatchDesc* desc, const float* const* M, const float* P,
+                         const void* p_split, float* R, const uint32_t* m_absmax, float* const* Q,
+                         const uint32_t* nonzero, float eps, void* ws, size_t ws_bytes,
+                         dion_stream_t stream);
 
 /*
  * fix_all_zero_or_nan (kernels.py:157-204) + column normalisation

@@ -68,6 +68,7 @@ class HipDionCodec:
 
     name = "hip"
     fuses_p_fixup = True  # orthonormalize(fix_nonzero=...) + fixup_colnorm(P=None)
+    fuses_r_fixup = True  # project_r_fixup: project_r + fixup_colnorm(P=None) in one call
 
     def __init__(self, device: Optional[torch.device] = None):
         self.lib = _lib.load()
@@ -291,6 +292,25 @@ class HipDionCodec:
                                            None if nonzero is None else nonzero.data_ptr(),
                                            ws.data_ptr(), ws.numel(), self._stream())
         _lib.check(rc, "dion_project_r")
+
+    def project_r_fixup(self, momentums: List[torch.Tensor], P: torch.Tensor, R: torch.Tensor,
+                        qs: List[torch.Tensor], nonzero: torch.Tensor, eps: float, transposed: bool,
+                        p_split: Optional[torch.Tensor] = None) -> None:
+        """project_r then fixup_colnorm(P=None, ...) in one call (fp32 state; the W = 1 path
+        after orthonormalize(fix_nonzero=...)): the fix-up's first phase rides on pass B's
+        split-K reduction.  runtime.py:1476-1477, kernels.py:157-210, 279-290."""
+        B = len(momentums)
+        if B == 0:
+            return
+        m, n = self._check_batch(momentums, momentums[0].dtype)
+        r = int(P.shape[2])
+        d = self._desc(B, m, n, r, transposed, M=momentums[0])
+        ws = self.workspace(d, _lib.OP_PROJECT_R)
+        rc = self.lib.dion_project_r_fixup(ctypes.byref(d), _ptrs(momentums), P.data_ptr(),
+                                           None if p_split is None else p_split.data_ptr(), R.data_ptr(),
+                                           nonzero.data_ptr(), _ptrs(qs), nonzero.data_ptr(), float(eps),
+                                           ws.data_ptr(), ws.numel(), self._stream())
+        _lib.check(rc, "dion_project_r_fixup")
 
     def fixup_colnorm(self, P: Optional[torch.Tensor], R: torch.Tensor, qs: List[torch.Tensor],
                       nonzero: torch.Tensor, eps: float, m: int, n: int, transposed: bool) -> None:

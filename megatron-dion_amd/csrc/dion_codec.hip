@@ -1362,6 +1362,44 @@ __global__ void __launch_bounds__(256) colnorm_apply_kernel(const FixArgs a) {
   }
 }
 
+// phase 1 fused with pass B's split-K reduction (dion_project_r_fixup): R = the sum of the
+// slabs in reduce_slabs_kernel's order, then fixup_partial_kernel's fix and chunk partials, in
+// its thread mapping and order (bitwise the two kernels; one launch and one pass over R fewer)
+__global__ void __launch_bounds__(256) reduce_fix_partial_kernel(const FixArgs a, const float* __restrict__ slab,
+                                                                 int nslab) {
+  __shared__ float red[256];
+  const int b = blockIdx.y, ch = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int r = a.r, nq = a.nq, tpc = a.tpc;
+  const long per_entry = static_cast<long>(nq) * r;
+  const bool zero = (a.nonzero[b] == 0u);
+  float* R = a.R + b * per_entry;
+  const float* S = slab + b * nslab * per_entry;
+  const float* Q = a.q[b];
+  const int c = tid % r, p = tid / r;
+  const int row0 = ch * a.rows_per_chunk;
+  const int row1 = min(nq, row0 + a.rows_per_chunk);
+  float ss = 0.f;
+  if (p < tpc) {
+    for (int row = row0 + p; row < row1; row += tpc) {
+      const long idx = static_cast<long>(row) * r + c;
+      float v = 0.f;
+      for (int k = 0; k < nslab; ++k) v += S[k * per_entry + idx];
+      const float qv = a.q_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(Q)[idx]) : Q[idx];
+      v = zero ? nan_to_num(qv) : nan_to_num(v);
+      R[idx] = v;
+      ss += v * v;
+    }
+  }
+  red[tid] = ss;
+  __syncthreads();
+  if (tid < r) {
+    float s2 = 0.f;
+    for (int k = 0; k < tpc; ++k) s2 += red[k * r + tid];
+    a.part[(static_cast<long>(b) * a.nchunk + ch) * r + tid] = s2;
+  }
+}
+
 // FS column norm, first half: the chunk partials of fixup_partial_kernel summed in fixed order
 __global__ void __launch_bounds__(256) colsum_reduce_kernel(const FixArgs a, float* __restrict__ colsum) {
   const int b = blockIdx.x;
@@ -2119,20 +2157,23 @@ __global__ void __launch_bounds__(NT) chol_reg_kernel(const float* __restrict__ 
 //   x_j = (p_j - sum_{k<j} R_kj x_k) * (1 / R_jj)
 // with the subtractions in k order (right-looking: once x_k is final, every later x_j takes
 // its fused term).  R (the factor kernels' padded RT x RT layout plus reciprocal diagonal)
-// is read with wave-uniform addresses: from global memory for RT <= 64 (scalar loads), from a
-// per-block LDS copy for RT = 128 (uniform global loads of the 64 KB factor thrash the scalar
-// cache: 361 us per 16-matrix group); the vector traffic is the row in and out.  Columns past r
-// are zero and stay zero.  In place (src == dst) is allowed.
+// is read with wave-uniform addresses from a per-block LDS copy (broadcast reads).  Scalar
+// (s_load) reads of the factor measured faster ALONE at RT <= 64 (fc1 group 76.5 vs 130 us,
+// scripts/ubench/trsm_ab.hip) but slower inside the two-stream Llama step (456.5 / 457.8 GiB/s
+// with LDS factors against 450.6 / 451.5, same box, profiles/r05/k_ab_and_solves.txt), where the
+// solves share the scalar caches and L2 with the streaming kernels; at RT = 128 scalar reads
+// thrash the scalar cache outright (2272 vs 176 us per fc1-size launch, even with the factor
+// read in three 16 KB blocks).  The vector traffic is the row in and out.  Columns past r are
+// zero and stay zero.  In place (src == dst) is allowed.
 // ============================================================================
 #ifndef DION_TRSM_LDS_MIN_RT
-#define DION_TRSM_LDS_MIN_RT 128  // the smallest padded order whose solve stages the factor in LDS
+#define DION_TRSM_LDS_MIN_RT 32  // the smallest padded order whose solve stages the factor in LDS
 #endif
 template <int RT>
 __global__ void __launch_bounds__(256) trsm_right_kernel(const float* __restrict__ src, float* __restrict__ dst,
                                                          const float* __restrict__ Rf, int mp, int r,
                                                          const uint32_t* __restrict__ nonzero) {
-  // RT <= 64: the factor by wave-uniform global (scalar) loads; from LDS it measured slower
-  // alone (fc1 group 79.5 vs 129 us, scripts/ubench/trsm_ab.hip, profiles/r05/i_trsm_variants.txt)
+  // DION_TRSM_LDS_MIN_RT (a dev build option for A/B runs): below it, scalar factor loads
   constexpr bool kLds = RT >= DION_TRSM_LDS_MIN_RT;
   __shared__ f32x4 Rs4[kLds ? (RT * RT + RT) / 4 : 1];
   const int b = blockIdx.y;
@@ -4585,6 +4626,11 @@ bool psplit_ok(const DionBatchDesc* d) {
   return colproj_fast_ok(d->m, d->n, d->r) && colh3_ok(d->m, d->n, d->r);
 }
 
+// the fix-up partials of dion_project_r_fixup at the end of the pass-B workspace
+size_t fix_part_bytes(int nq, int r, int batch) {
+  return (sizeof(float) * static_cast<size_t>(batch) * ceil_div(nq, kFixRows) * r + 255) / 256 * 256;
+}
+
 // one absmax_kernel launch over `groups` groups of nb matrices (AbsMaxArgs order)
 void launch_absmax(AbsMaxArgs& ma, int groups, hipStream_t st) {
   long most = 0;
@@ -4637,7 +4683,7 @@ int launch_reduce(float* out, const float* slab, int nchunk, long per_entry, int
 int run_projection(bool row_mode, int rows, int cols, int r, int batch, const void* const* G, float* const* M,
                    const float* const* thin, long ld_m, long ld_g, int gdt, float* out, uint32_t* nonzero,
                    void* ws, size_t ws_bytes, hipStream_t st, const uint32_t* mabs = nullptr,
-                   const f16x8* thin_split = nullptr) {
+                   const f16x8* thin_split = nullptr, const FixArgs* fix = nullptr) {
   bool fast = row_mode ? rowproj_fast_ok(rows, cols, r) : colproj_fast_ok(rows, cols, r);
   fast = fast && (ld_m % 8) == 0 && (gdt == DION_DTYPE_NONE || (ld_g % 8) == 0);
   for (int b = 0; b < batch && fast; ++b)
@@ -4762,6 +4808,18 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     });
   });
   if (rc != DION_OK) return rc;
+  if (fix != nullptr) {
+    // dion_project_r_fixup: the fix-up's first phase rides on the split-K reduction
+    if (geo.nchunk > 1)
+      hipLaunchKernelGGL(reduce_fix_partial_kernel, dim3(fix->nchunk, batch), dim3(256), 0, st, *fix,
+                         static_cast<const float*>(ws), geo.nchunk);
+    else
+      hipLaunchKernelGGL(fixup_partial_kernel, dim3(fix->nchunk, batch), dim3(256), 0, st, *fix);
+    rc = check_launch("fixup_partial(pass B)");
+    if (rc != DION_OK) return rc;
+    hipLaunchKernelGGL(colnorm_apply_kernel, dim3(fix->nchunk, batch), dim3(256), 0, st, *fix);
+    return check_launch("fixup_colnorm(pass B)");
+  }
   if (geo.nchunk > 1)
     return launch_reduce(out, static_cast<const float*>(ws), geo.nchunk, static_cast<long>(geo.out_rows) * r, batch, st);
   return DION_OK;
@@ -5083,8 +5141,9 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
           const size_t nh = slab_bytes(colh3_geo(d->m, d->n, chunk, d->r), chunk, d->r);
           if (nh > n) n = nh;
         }
-        if (op == DION_OP_PROJECT_R)
-          n = (n + 255) / 256 * 256 + thin_presplit_bytes(row_mode ? d->n : d->m, d->r, chunk);
+        if (op == DION_OP_PROJECT_R)  // + the fix-up partials of dion_project_r_fixup
+          n = (n + 255) / 256 * 256 + thin_presplit_bytes(row_mode ? d->n : d->m, d->r, chunk) + 256 +
+              fix_part_bytes(nq, d->r, chunk);
         break;
       }
       case DION_OP_PROJECT_P_EF: {
@@ -5362,6 +5421,56 @@ int dion_project_r_split(const DionBatchDesc* d, const float* const* M, const fl
                         m_absmax != nullptr ? m_absmax + b0 : nullptr,
                         p_split != nullptr ? static_cast<const f16x8*>(p_split) + static_cast<long>(b0) * mp * d->r / 4
                                            : nullptr);
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
+int dion_project_r_fixup(const DionBatchDesc* d, const float* const* M, const float* P, const void* p_split,
+                         float* R, const uint32_t* m_absmax, float* const* Q, const uint32_t* nonzero, float eps,
+                         void* ws, size_t ws_bytes, dion_stream_t stream) {
+  int rc = validate(d);
+  if (rc != DION_OK) return rc;
+  if (M == nullptr || P == nullptr || R == nullptr || Q == nullptr || nonzero == nullptr)
+    return fail(DION_E_INVALID, "null argument");
+  if (d->m_dtype != DION_DTYPE_F32) return fail(DION_E_UNSUPPORTED, "dion_project_r_fixup: fp32 state only");
+  if (d->batch == 0) return DION_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int mp = d->transposed ? d->n : d->m;
+  const int nq = d->transposed ? d->m : d->n;
+  const int r = d->r;
+  const long ld_m = ldv(d->ld_m, d->n);
+  const int nb0 = d->batch < MAXB ? d->batch : MAXB;
+  const size_t pbytes = fix_part_bytes(nq, r, nb0);
+  if (ws == nullptr || ws_bytes < pbytes)
+    return fail(DION_E_WORKSPACE, "project_r_fixup needs %zu more workspace bytes", pbytes);
+  const size_t proj_bytes = (ws_bytes - pbytes) / 256 * 256;
+  float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + proj_bytes);
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    const float* thin[MAXB];
+    FixArgs fa;
+    memset(&fa, 0, sizeof(fa));
+    for (int b = 0; b < nb; ++b) {
+      thin[b] = P + static_cast<long>(b0 + b) * mp * r;
+      if (Q[b0 + b] == nullptr) return fail(DION_E_INVALID, "null Q at %d", b0 + b);
+      fa.q[b] = Q[b0 + b];
+    }
+    fa.R = R + static_cast<long>(b0) * nq * r;
+    fa.part = part;
+    fa.nonzero = nonzero + b0;
+    fa.nq = nq;
+    fa.r = r;
+    fa.tpc = 256 / r;
+    fa.rows_per_chunk = kFixRows;
+    fa.nchunk = static_cast<int>(ceil_div(nq, kFixRows));
+    fa.eps = eps;
+    rc = run_projection(d->transposed != 0, d->m, d->n, r, nb, nullptr, const_cast<float* const*>(M + b0), thin, ld_m,
+                        0, DION_DTYPE_NONE, fa.R, nullptr, ws, proj_bytes, st,
+                        m_absmax != nullptr ? m_absmax + b0 : nullptr,
+                        p_split != nullptr ? static_cast<const f16x8*>(p_split) + static_cast<long>(b0) * mp * r / 4
+                                           : nullptr,
+                        &fa);
     if (rc != DION_OK) return rc;
   }
   return DION_OK;

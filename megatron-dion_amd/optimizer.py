@@ -373,7 +373,8 @@ class MegatronDion(Optimizer):
         return loss
 
     # phases the fused kernels fold into another phase's record (PhaseClock)
-    _FUSED_PHASES = {"grad_momentum": "p_matmul", "error_feedback": "apply_update or the next p_matmul"}
+    _FUSED_PHASES = {"grad_momentum": "p_matmul", "error_feedback": "apply_update or the next p_matmul",
+                     "q_normalize": "ortho_r"}
 
     def _report_profile(self, t0) -> None:
         """algorithm.py:170-218 with HIP-event phase times: one synchronise, then the per-label sums

@@ -390,6 +390,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
                              state_dtype=sdt)
 
     p_fixed = False
+    r_fixed = False  # W = 1: pass B also did the fix-up and column norm (project_r_fixup)
     if W > 1 and kch:
         rank = dist.get_rank(group)
         mine = P[rank * kch:(rank + 1) * kch]
@@ -484,12 +485,20 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         if phase_marks:
             yield "stream"
         R = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
-        codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero,
-                        **({} if split is None else {"p_split": split}))
+        if p_fixed and getattr(codec, "fuses_r_fixup", False):
+            # pass B with the fix-up and column norm (R's half) riding on its reduction
+            r_fixed = True
+            codec.project_r_fixup(list(momentums[:real]), P, R, list(Qs[:real]), nonzero,
+                                  float(optimizer.defaults["epsilon"]), transposed,
+                                  **({} if split is None else {"p_split": split}))
+        else:
+            codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero,
+                            **({} if split is None else {"p_split": split}))
 
     clock.mark("ortho_r")
     eps = float(optimizer.defaults["epsilon"])
-    codec.fixup_colnorm(None if (W == 1 and p_fixed) else P, R, list(Qs[:real]), nonzero, eps, m, n, transposed)
+    if not r_fixed:
+        codec.fixup_colnorm(None if (W == 1 and p_fixed) else P, R, list(Qs[:real]), nonzero, eps, m, n, transposed)
     clock.mark("q_normalize")
 
     grp = optim_groups[0] or {}

@@ -14,6 +14,7 @@ from . import dion_oracle as O
 class OracleCodec:
     name = "oracle-cpu"
     fuses_p_fixup = True  # orthonormalize(fix_nonzero=...) + fixup_colnorm(P=None)
+    fuses_r_fixup = True  # project_r_fixup = project_r + fixup_colnorm(P=None)
 
     def __init__(self, sketch_lookup=None, hyper_eps=1e-8, deferred=False):
         self.sketch_lookup = sketch_lookup  # fn(P (1, m_P, r)) -> sketch (1, k, m_P) or None
@@ -81,6 +82,11 @@ class OracleCodec:
         for b, M in enumerate(momentums):
             X = M.mT if transposed else M
             R[b] = X.mT @ P[b].to(X.dtype)
+
+    def project_r_fixup(self, momentums, P, R, qs, nonzero, eps, transposed, p_split=None):
+        self.project_r(momentums, P, R, transposed, nonzero=nonzero)
+        m, n = momentums[0].shape[-2:]
+        self.fixup_colnorm(None, R, qs, nonzero, eps, m, n, transposed)
 
     def fixup_colnorm(self, P, R, qs, nonzero, eps, m, n, transposed):
         B = len(qs)

@@ -19,9 +19,9 @@ sys.path.insert(0, ROOT)
 MODES = {
     "base": (),
     "no_ortho": ("orthonormalize",),
-    "no_passb": ("project_r",),
+    "no_passb": ("project_r", "project_r_fixup"),
     "no_update": ("ef_apply",),
-    "no_fixup": ("fixup_colnorm",),
+    "no_fixup": ("fixup_colnorm",),  # the W = 1 fp32 path fixes inside project_r_fixup
     "no_passa": ("project_p_ef", "project_p"),
     "only_streaming": ("orthonormalize", "fixup_colnorm"),
 }

@@ -709,3 +709,41 @@ def test_orthonormalize_h3_gram_matches_oracle(mp, r, decades):
     print(f"mp={mp} r={r} decades={decades}: P maxrel vs oracle {worst_p:.3e}, |P^T P - I| {worst_i:.3e}")
     assert worst_i <= 2e-6, worst_i
     assert worst_p <= 1e-5 * 10 ** decades, worst_p
+
+
+# ---------------------------------------------------------------------------------------------- pass B + fix-up
+@pytest.mark.parametrize("m,n,r", [(1024, 768, 64), (768, 1024, 64), (1280, 640, 128), (640, 1280, 128),
+                                   (544, 480, 32), (2048, 4096, 64)])
+def test_project_r_fixup_is_project_r_then_fixup(m, n, r):
+    """dion_project_r_fixup (the fix-up's first phase on pass B's split-K reduction) is bitwise
+    dion_project_r_split followed by dion_fixup_colnorm(P = NULL), with a zero entry (nonzero 0:
+    R takes nan_to_num(Q)) and a NaN in one momentum."""
+    from megatron_dion_amd.codec import HipDionCodec
+
+    dev = _dev()
+    transposed = m < n
+    mp, nq = (n, m) if transposed else (m, n)
+    B = 4
+    gen = torch.Generator().manual_seed(m + n + r)
+    Ms = [(torch.randn(m, n, generator=gen) * 1e-2).to(dev) for _ in range(B)]
+    Ms[2][5, 7] = float("nan")
+    P = torch.linalg.qr(torch.randn(B, mp, r, generator=gen))[0].to(dev).contiguous()
+    Q0 = [torch.randn(nq, r, generator=gen).to(dev) for _ in range(B)]
+    # pass A's flags: max |M_b| as float bits (the fixed-scale pass B), 0 = an all-zero entry
+    amax = torch.stack([M.nan_to_num(nan=0.0).abs().max() for M in Ms]).float().cpu()
+    nz = amax.view(torch.int32).clone()
+    nz[1] = 0
+    nz = nz.to(dev)
+    codec = HipDionCodec(dev)
+    R1 = torch.empty(B, nq, r, device=dev)
+    Q1 = [q.clone() for q in Q0]
+    codec.project_r(Ms, P, R1, transposed, nonzero=nz)
+    codec.fixup_colnorm(None, R1, Q1, nz, 1e-8, m, n, transposed)
+    R2 = torch.empty(B, nq, r, device=dev)
+    Q2 = [q.clone() for q in Q0]
+    codec.project_r_fixup(Ms, P, R2, Q2, nz, 1e-8, transposed)
+    torch.cuda.synchronize()
+    assert torch.equal(R1.cpu(), R2.cpu())
+    for a, b in zip(Q1, Q2):
+        assert torch.equal(a.cpu(), b.cpu())
+    assert torch.isfinite(R2).all()
