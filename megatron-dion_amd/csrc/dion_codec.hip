@@ -2948,6 +2948,174 @@ __global__ void __launch_bounds__(256, 2) gram_h3_kernel(const GramArgs a) {
       for (int q = 0; q < 4; ++q) out[(16 * (TA * wave + ta) + 4 * g + q) * R + 16 * cb + t] = acc[ta][cb][q];
 }
 
+// ============================================================================
+// The two triangular solves as GEMMs with the explicit inverse, X_b = P_b T_b, T_b = R_b^-1 (the
+// r x r upper-triangular inverses that sketch_qr_inv_kernel / chol_inv_kernel write with INV),
+// on fp16x3 MFMAs.  The solve kernels above run one row per lane and read every factor value
+// once per row (2 080 reads per row at r = 64, from LDS or the scalar cache): LDS- or
+// scalar-cache-bound at 2-8x the time of the row traffic, and they hold the CUs the streaming
+// kernels of the other stream need.  Here a wave takes 16 rows per MFMA tile: Xt = Tt Pt on
+// v_mfma_f32_16x16x32_f16 (A = T^T: lane (t, g) holds T[32 j + 8 g + e][16 i + t]; B = P^T: lane
+// (t, g) holds P[row t][32 j + 8 g + e]; D lane (t, g): X[row t][16 i + 4 g + q]), three products
+// (hi hi, hi lo, lo hi), T split with one power-of-two scale per column and P with one per row,
+// zero blocks of T skipped.  The rounding differs from substitution's (the product, not the
+// k-ordered fma chain); numpy over 0-8 decades of conditioning puts the final P's error at
+// 0.6-1.6x the fp32 substitution's.
+//   RT <= 64 (IMG): each wave's 64 rows are staged by LDS-DMA as in trsm_lds_kernel, X goes back
+//   into the image, and the epilogue (coalesced store, FINAL fix-up, pass-B split) is that
+//   kernel's.  RT = 128: operands straight from HBM (32 B per lane and k-step), X stored as
+//   16-byte row pieces, FINAL fix-up only (no pass-B split at r = 128).
+// ============================================================================
+constexpr int kTgWavesImg = 2, kTgWavesDirect = 4;
+
+template <int RT, bool FINAL>
+__global__ void __launch_bounds__(64 * (RT <= 64 ? kTgWavesImg : kTgWavesDirect), RT <= 64 ? 3 : 2)
+tsolve_mfma_kernel(const TrsmArgs a) {
+  static_assert(RT == 32 || RT == 64 || RT == 128, "tsolve_mfma_kernel: r = 32, 64 or 128");
+  constexpr bool IMG = RT <= 64;
+  constexpr int NW = IMG ? kTgWavesImg : kTgWavesDirect;
+  constexpr int CH = RT / 4;   // 16-B chunks per row
+  constexpr int KS = RT / 32;  // 32-wide k-steps
+  constexpr int NT = RT / 16;  // 16-wide output column tiles
+  constexpr int LDT = RT + 4;  // T^T row pitch: lanes t of a ds_read_b128 group land 4 banks apart
+  __shared__ f32x4 img[IMG ? NW : 1][IMG ? 64 * CH : 1];
+  __shared__ __attribute__((aligned(16))) float Tt[RT * LDT];
+  __shared__ float scol[RT], icol[RT];
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(tid >> 6)), lane = tid & 63;
+  const int t = lane & 15, g = lane >> 4;
+  const int mp = a.mp;
+  // T^T into LDS (T row-major: coalesced reads, transposed writes), then per column of T its
+  // max |x| and power-of-two scale (a NaN column -- a failed factorisation -- stays NaN)
+  {
+    const float* Tg = a.fac + static_cast<long>(b) * RT * RT;
+    for (int idx = tid; idx < RT * RT; idx += 64 * NW) {
+      const int k = idx / RT, n = idx % RT;
+      Tt[n * LDT + k] = Tg[idx];
+    }
+    __syncthreads();
+    for (int n = tid; n < RT; n += 64 * NW) {
+      float m = 0.f;
+      for (int k = 0; k <= n; ++k) m = fmaxf(m, fabsf(Tt[n * LDT + k]));
+      float inv;
+      scol[n] = h3_scale(m, inv);
+      icol[n] = inv;
+    }
+    __syncthreads();
+  }
+  const long row0 = static_cast<long>(blockIdx.x) * (64 * NW) + wave * 64;
+  const int nrows = static_cast<int>(min(static_cast<long>(64), static_cast<long>(mp) - row0));
+  if (nrows <= 0) return;
+  const float* src = a.src + (static_cast<long>(b) * mp + row0) * RT;
+  float* dst = a.dst + (static_cast<long>(b) * mp + row0) * RT;
+  f32x4* w = img[IMG ? wave : 0];
+  if constexpr (IMG) {
+    const char* s = reinterpret_cast<const char*>(src);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int slot = 64 * i + lane, row = slot / CH, cp = slot % CH;
+      if (row < nrows) glds16<false>(s, static_cast<uint32_t>((row * CH + (cp ^ trsm_swz<RT>(row))) * 16), lds_off(&w[64 * i]));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  const bool zero = FINAL && a.nonzero != nullptr && a.nonzero[b] == 0u;
+  for (int tile = 0; tile < 4; ++tile) {
+    if (16 * tile >= nrows) break;
+    const int row = 16 * tile + t;
+    const bool valid = row < nrows;
+    // this lane's B operand: P[row][32 j + 8 g .. + 7] for every k-step j
+    f32x4 v[KS][2];
+#pragma unroll
+    for (int j = 0; j < KS; ++j) {
+      const int c0 = 8 * j + 2 * g;
+      if constexpr (IMG) {
+        v[j][0] = valid ? w[row * CH + (c0 ^ trsm_swz<RT>(row))] : f32x4{0.f, 0.f, 0.f, 0.f};
+        v[j][1] = valid ? w[row * CH + ((c0 + 1) ^ trsm_swz<RT>(row))] : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        const f32x4* p = reinterpret_cast<const f32x4*>(src + static_cast<long>(row) * RT);
+        v[j][0] = valid ? p[c0] : f32x4{0.f, 0.f, 0.f, 0.f};
+        v[j][1] = valid ? p[c0 + 1] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    // the row's max |x| (lanes t, t + 16, t + 32, t + 48 hold row t) and its scale
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < KS; ++j) m = fmaxf(m, max8abs(v[j][0], v[j][1]));
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float irow;
+    const float srow = h3_scale(m, irow);
+    Split2h B[KS];
+#pragma unroll
+    for (int j = 0; j < KS; ++j) split2h(v[j][0], v[j][1], srow, B[j]);
+    f32x4 x[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      f32x4 acc{0.f, 0.f, 0.f, 0.f};
+      const int n = 16 * i + t;
+      const float sc = scol[n];
+#pragma unroll
+      for (int j = 0; j < KS; ++j) {
+        if (32 * j > 16 * i + 15) break;  // T[k][n] = 0 for k > n
+        const f32x4* tp = reinterpret_cast<const f32x4*>(&Tt[n * LDT + 32 * j + 8 * g]);
+        Split2h A;
+        split2h(tp[0], tp[1], sc, A);
+        acc = mfma3h(A, B[j], acc);
+      }
+      const f32x4 ic = *reinterpret_cast<const f32x4*>(&icol[16 * i + 4 * g]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float y = (acc[q] * irow) * ic[q];
+        if constexpr (FINAL) y = zero ? 0.f : (a.nonzero != nullptr ? nan_to_num(y) : y);
+        x[i][q] = y;
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        if constexpr (IMG)
+          w[row * CH + ((4 * i + g) ^ trsm_swz<RT>(row))] = x[i];
+        else
+          reinterpret_cast<f32x4*>(dst + static_cast<long>(row) * RT)[4 * i + g] = x[i];
+      }
+    }
+  }
+  if constexpr (IMG) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    f32x4* d = reinterpret_cast<f32x4*>(dst);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int slot = 64 * i + lane, row = slot / CH, cp = slot % CH;
+      if (row < nrows) d[row * CH + (cp ^ trsm_swz<RT>(row))] = w[slot];
+    }
+    if constexpr (FINAL) {
+      if (a.psplit != nullptr) {
+        constexpr int RB = RT / 16;
+        const float* wf = reinterpret_cast<const float*>(w);
+        f16x8* out = a.psplit + b * a.pstride;
+#pragma unroll
+        for (int u = 0; u < 2 * RB; ++u) {
+          const int q = u / RB, cb = u % RB;
+          if (32 * q >= nrows) break;
+          float vv[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int rr = 32 * q + (a.kmap == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3));
+            const int col = 16 * cb + t;
+            vv[e] = wf[(rr * CH + ((col >> 2) ^ trsm_swz<RT>(rr))) * 4 + (col & 3)];
+          }
+          Split2h sp;
+          split2h(f32x4{vv[0], vv[1], vv[2], vv[3]}, f32x4{vv[4], vv[5], vv[6], vv[7]}, kPSplitScale, sp);
+          const long grp = (row0 / 32 + q) * RB + cb;
+          out[grp * 128 + lane] = sp.hi;
+          out[grp * 128 + 64 + lane] = sp.lo;
+        }
+      }
+    }
+  }
+}
+
 // per-matrix max |x| of a small factor (rows x r fp32), as the float's bit pattern
 // (non-negative floats order like their bits; a NaN sorts above inf)
 struct AbsMaxArgs {
@@ -4936,6 +5104,34 @@ int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t s
   return check_launch("chol_inv");
 }
 
+// the orthonormalisation's two solves as GEMMs with the explicit inverses (tsolve_mfma_kernel)
+// for r = 32, 64, 128 (a dev build option for A/B runs until measured in the step)
+#ifndef DION_TSOLVE_GEMM
+#define DION_TSOLVE_GEMM 0
+#endif
+bool tsolve_gemm_ok(int mp, int r) { return DION_TSOLVE_GEMM && (r == 32 || r == 64 || r == 128) && mp > r; }
+
+int launch_tsolve(const float* src, float* dst, const float* T, int mp, int r, int batch, hipStream_t st, bool final_,
+                  const uint32_t* nonzero, f16x8* psplit, long pstride, int kmap) {
+  TrsmArgs ta{src, dst, T, nonzero, psplit, pstride, mp, kmap};
+  auto go = [&](auto RTc, auto Fc) {
+    constexpr int RT = decltype(RTc)::value;
+    constexpr bool F = decltype(Fc)::value;
+    constexpr int NW = RT <= 64 ? kTgWavesImg : kTgWavesDirect;
+    hipLaunchKernelGGL((tsolve_mfma_kernel<RT, F>), dim3(static_cast<unsigned>(ceil_div(mp, 64 * NW)), batch),
+                       dim3(64 * NW), 0, st, ta);
+    return check_launch("tsolve_mfma");
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  switch (r) {
+    case 32: return final_ ? go(std::integral_constant<int, 32>{}, T_{}) : go(std::integral_constant<int, 32>{}, F_{});
+    case 64: return final_ ? go(std::integral_constant<int, 64>{}, T_{}) : go(std::integral_constant<int, 64>{}, F_{});
+    case 128: return final_ ? go(std::integral_constant<int, 128>{}, T_{}) : go(std::integral_constant<int, 128>{}, F_{});
+  }
+  return fail(DION_E_UNSUPPORTED, "tsolve r=%d", r);
+}
+
 // dst_b = src_b R_b^-1 by forward substitution (trsm_right_kernel; factor from the INV = false
 // factor kernels)
 int launch_trsm(const float* src, float* dst, const float* fac, int mp, int r, int batch, hipStream_t st,
@@ -5542,11 +5738,14 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     if (rc != DION_OK) return rc;
     float* fac = reinterpret_cast<float*>(base + plan.off_inv);
     float* p1 = reinterpret_cast<float*>(base + plan.off_p1);
-    // (2) R1 = qr(S P).R, (3) P1 = P R1^-1 by forward substitution (into workspace)
-    rc = launch_sketch_qr_inv(sp, fac, K, r, nb, st, false);
+    // (2) R1 = qr(S P).R, (3) P1 = P R1^-1 (into workspace): by forward substitution, or as
+    // the GEMM P T1 with the explicit inverse T1 (tsolve_mfma_kernel)
+    const bool gemm = tsolve_gemm_ok(mp, r);
+    rc = launch_sketch_qr_inv(sp, fac, K, r, nb, st, gemm);
     if (rc != DION_OK) return rc;
     (void)r1;
-    rc = launch_trsm(Pb, p1, fac, mp, r, nb, st);
+    rc = gemm ? launch_tsolve(Pb, p1, fac, mp, r, nb, st, false, nullptr, nullptr, 0, 0)
+              : launch_trsm(Pb, p1, fac, mp, r, nb, st);
     if (rc != DION_OK) return rc;
     // (4) Gram = P1^T P1
     if (gram_h3_ok(mp, r)) {
@@ -5563,11 +5762,15 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     }
     if (rc != DION_OK) return rc;
     // (5) R2 = chol_upper(Gram)
-    rc = launch_chol_inv(gm, fac, r, nb, st, false);
+    rc = launch_chol_inv(gm, fac, r, nb, st, gemm);
     if (rc != DION_OK) return rc;
     (void)r2;
     // (6) P = P1 R2^-1 (back into the caller's buffer), with the fix-up and pass B's split
-    if (lds_fix || p_split != nullptr) {
+    if (gemm) {
+      rc = launch_tsolve(p1, Pb, fac, mp, r, nb, st, true, fuse_fix ? nonzero + b0 : nullptr,
+                         p_split != nullptr ? static_cast<f16x8*>(p_split) + static_cast<long>(b0) * mp * r / 4 : nullptr,
+                         static_cast<long>(mp) * r / 4, d->transposed ? 1 : 0);
+    } else if (lds_fix || p_split != nullptr) {
       TrsmArgs ta{p1, Pb, fac, fuse_fix ? nonzero + b0 : nullptr,
                   p_split != nullptr ? static_cast<f16x8*>(p_split) + static_cast<long>(b0) * mp * r / 4 : nullptr,
                   static_cast<long>(mp) * r / 4, mp, d->transposed ? 1 : 0};
