@@ -2966,6 +2966,35 @@ __global__ void __launch_bounds__(256, 2) gram_h3_kernel(const GramArgs a) {
 //   kernel's.  RT = 128: operands straight from HBM (32 B per lane and k-step), X stored as
 //   16-byte row pieces, FINAL fix-up only (no pass-B split at r = 128).
 // ============================================================================
+// T_b = F_b^-1 for the padded upper-triangular factor F_b of the factor kernels (RT x RT, then
+// its RT reciprocal diagonal entries: the INV = false output of sketch_qr_inv_kernel and
+// chol_reg_kernel), the operand of tsolve_mfma_kernel.  One block per matrix, thread c owns
+// column c and runs its back substitution, x_i = (d_ic - sum_{i < k <= c} F_ik x_k) (1/F_ii) for
+// i = c .. 0 (x_i = 0 for i > c), k ascending, fp32; the factor row is a broadcast LDS read and
+// the column lives in LDS (thread-private, consecutive banks across threads).  A NaN diagonal
+// (a failed factorisation) makes its column and every later one NaN, as the substitution
+// would.  Numpy over 0-6 decades: the final P within 0.8-1.0x the error of an fp64 inverse
+// (DESIGN.md section 4).
+template <int RT>
+__global__ void __launch_bounds__(RT) tri_inv_kernel(const float* __restrict__ F, float* __restrict__ T) {
+  __shared__ __attribute__((aligned(16))) float Fs[RT * RT + RT];
+  __shared__ float Xs[RT * RT];  // Xs[k RT + c] = x_k of column c
+  const int b = blockIdx.x, c = threadIdx.x;
+  {
+    const f32x4* src = reinterpret_cast<const f32x4*>(F + static_cast<long>(b) * (RT * RT + RT));
+    for (int i = c; i < (RT * RT + RT) / 4; i += RT) reinterpret_cast<f32x4*>(Fs)[i] = src[i];
+    __syncthreads();
+  }
+  for (int i = RT - 1; i >= 0; --i) {
+    float acc = (i == c) ? 1.f : 0.f;
+#pragma unroll 8
+    for (int k = i + 1; k <= c; ++k) acc = fmaf(-Fs[i * RT + k], Xs[k * RT + c], acc);
+    Xs[i * RT + c] = (i <= c) ? acc * Fs[RT * RT + i] : 0.f;
+  }
+  float* out = T + static_cast<long>(b) * RT * RT;
+  for (int i = 0; i < RT; ++i) out[i * RT + c] = Xs[i * RT + c];
+}
+
 constexpr int kTgWavesImg = 2, kTgWavesDirect = 4;
 
 template <int RT, bool FINAL>
@@ -5087,7 +5116,8 @@ int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t s
   if (!inv) {
     switch (trsm_rt(r)) {
       case 32: hipLaunchKernelGGL((chol_reg_kernel<32>), dim3(batch), dim3(256), 0, st, G, Uinv, r); break;
-      case 64: hipLaunchKernelGGL((chol_reg_kernel<64>), dim3(batch), dim3(256), 0, st, G, Uinv, r); break;
+      // 512 threads: 39.8 vs 53.0 us per 16-matrix launch, bitwise the same (scripts/ubench/chol_ab.hip)
+      case 64: hipLaunchKernelGGL((chol_reg_kernel<64, 512>), dim3(batch), dim3(512), 0, st, G, Uinv, r); break;
       default: hipLaunchKernelGGL((chol_reg_kernel<128, 1024>), dim3(batch), dim3(1024), 0, st, G, Uinv, r); break;
     }
     return check_launch("chol");
@@ -5104,12 +5134,25 @@ int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t s
   return check_launch("chol_inv");
 }
 
-// the orthonormalisation's two solves as GEMMs with the explicit inverses (tsolve_mfma_kernel)
-// for r = 32, 64, 128 (a dev build option for A/B runs until measured in the step)
+// the orthonormalisation's two solves as GEMMs with the explicit inverses (tri_inv_kernel +
+// tsolve_mfma_kernel) for r = 32, 64, 128; 0 (a dev build option) keeps the substitution
+// kernels.  Same-box Llama 460.6 / 449.8 -> 465.8 / 455.2 GiB/s, Mixtral 350.0 -> 352.3 with the
+// inverses from the factor kernels (profiles/r05/m_solves_gemm_ab.txt); the solves alone beside a streaming copy:
+// r = 64 8.4 vs 33.7 us marginal per fc1 group, r = 128 41.2 vs 105.9 (scripts/ubench/trsm_conc.hip)
 #ifndef DION_TSOLVE_GEMM
-#define DION_TSOLVE_GEMM 0
+#define DION_TSOLVE_GEMM 1
 #endif
 bool tsolve_gemm_ok(int mp, int r) { return DION_TSOLVE_GEMM && (r == 32 || r == 64 || r == 128) && mp > r; }
+
+int launch_tri_inv(const float* F, float* T, int r, int batch, hipStream_t st) {
+  switch (r) {
+    case 32: hipLaunchKernelGGL((tri_inv_kernel<32>), dim3(batch), dim3(32), 0, st, F, T); break;
+    case 64: hipLaunchKernelGGL((tri_inv_kernel<64>), dim3(batch), dim3(64), 0, st, F, T); break;
+    case 128: hipLaunchKernelGGL((tri_inv_kernel<128>), dim3(batch), dim3(128), 0, st, F, T); break;
+    default: return fail(DION_E_UNSUPPORTED, "tri_inv r=%d", r);
+  }
+  return check_launch("tri_inv");
+}
 
 int launch_tsolve(const float* src, float* dst, const float* T, int mp, int r, int batch, hipStream_t st, bool final_,
                   const uint32_t* nonzero, f16x8* psplit, long pstride, int kmap) {
@@ -5741,10 +5784,10 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     // (2) R1 = qr(S P).R, (3) P1 = P R1^-1 (into workspace): by forward substitution, or as
     // the GEMM P T1 with the explicit inverse T1 (tsolve_mfma_kernel)
     const bool gemm = tsolve_gemm_ok(mp, r);
-    rc = launch_sketch_qr_inv(sp, fac, K, r, nb, st, gemm);
+    rc = launch_sketch_qr_inv(sp, fac, K, r, nb, st, false);
+    if (rc == DION_OK && gemm) rc = launch_tri_inv(fac, r1, r, nb, st);  // T1 = R1^-1
     if (rc != DION_OK) return rc;
-    (void)r1;
-    rc = gemm ? launch_tsolve(Pb, p1, fac, mp, r, nb, st, false, nullptr, nullptr, 0, 0)
+    rc = gemm ? launch_tsolve(Pb, p1, r1, mp, r, nb, st, false, nullptr, nullptr, 0, 0)
               : launch_trsm(Pb, p1, fac, mp, r, nb, st);
     if (rc != DION_OK) return rc;
     // (4) Gram = P1^T P1
@@ -5762,12 +5805,13 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     }
     if (rc != DION_OK) return rc;
     // (5) R2 = chol_upper(Gram)
-    rc = launch_chol_inv(gm, fac, r, nb, st, gemm);
+    rc = launch_chol_inv(gm, fac, r, nb, st, false);
+    if (rc == DION_OK && gemm) rc = launch_tri_inv(fac, r1, r, nb, st);  // T2 = R2^-1
     if (rc != DION_OK) return rc;
     (void)r2;
     // (6) P = P1 R2^-1 (back into the caller's buffer), with the fix-up and pass B's split
     if (gemm) {
-      rc = launch_tsolve(p1, Pb, fac, mp, r, nb, st, true, fuse_fix ? nonzero + b0 : nullptr,
+      rc = launch_tsolve(p1, Pb, r1, mp, r, nb, st, true, fuse_fix ? nonzero + b0 : nullptr,
                          p_split != nullptr ? static_cast<f16x8*>(p_split) + static_cast<long>(b0) * mp * r / 4 : nullptr,
                          static_cast<long>(mp) * r / 4, d->transposed ? 1 : 0);
     } else if (lds_fix || p_split != nullptr) {
