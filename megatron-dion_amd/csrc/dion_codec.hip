@@ -1098,9 +1098,9 @@ __device__ __forceinline__ void write_padded_factor(const float* Rs, int rld, in
   for (int j = tid; j < rt; j += nt) O[rt * rt + j] = j < r ? 1.f / Rs[j * rld + j] : 1.f;
 }
 
-template <int RPL, int CPW, typename XT, bool INV = true>
-__global__ void __launch_bounds__(256) sketch_qr_inv_kernel(const float* __restrict__ SP, float* __restrict__ Rinv,
-                                                            int K, int r, int rt = 0) {
+template <int RPL, int CPW, typename XT, bool INV = true, int NWQ = 4>
+__global__ void __launch_bounds__(64 * NWQ) sketch_qr_inv_kernel(const float* __restrict__ SP, float* __restrict__ Rinv,
+                                                                 int K, int r, int rt = 0) {
   extern __shared__ __attribute__((aligned(16))) char qsm[];
   const int rld = r + 1;
   float* vbuf = reinterpret_cast<float*>(qsm);         // 2 x 256
@@ -1118,15 +1118,15 @@ __global__ void __launch_bounds__(256) sketch_qr_inv_kernel(const float* __restr
   for (int s = 0; s < RPL; ++s)
 #pragma unroll
     for (int cc = 0; cc < CPW; ++cc) {
-      const int row = lane + 64 * s, col = w + 4 * cc;
+      const int row = lane + 64 * s, col = w + NWQ * cc;
       A[s][cc] = (row < K && col < r) ? A0[static_cast<long>(row) * r + col] : 0.f;
     }
-  const int n_w = (r > w) ? (r - w + 3) / 4 : 0;
+  const int n_w = (r > w) ? (r - w + NWQ - 1) / NWQ : 0;
   int consumed = 0;
   __syncthreads();
   for (int j = 0; j < r; ++j) {
     const int buf = j & 1;
-    if ((j & 3) == w) {
+    if (j % NWQ == w) {
       float xs[RPL];
       float ss = 0.f;
       float alpha_l = 0.f;
@@ -2970,8 +2970,9 @@ __global__ void __launch_bounds__(256, 2) gram_h3_kernel(const GramArgs a) {
 // its RT reciprocal diagonal entries: the INV = false output of sketch_qr_inv_kernel and
 // chol_reg_kernel), the operand of tsolve_mfma_kernel.  One block per matrix, thread c owns
 // column c and runs its back substitution, x_i = (d_ic - sum_{i < k <= c} F_ik x_k) (1/F_ii) for
-// i = c .. 0 (x_i = 0 for i > c), k ascending, fp32; the factor row is a broadcast LDS read and
-// the column lives in LDS (thread-private, consecutive banks across threads).  A NaN diagonal
+// i = c .. 0 (x_i = 0 for i > c), fp32, the k-sum in eight interleaved partial sums; the factor
+// row is a broadcast LDS read and the column lives in LDS (thread-private, consecutive banks
+// across threads).  A NaN diagonal
 // (a failed factorisation) makes its column and every later one NaN, as the substitution
 // would.  Numpy over 0-6 decades: the final P within 0.8-1.0x the error of an fp64 inverse
 // (DESIGN.md section 4).
@@ -2986,10 +2987,16 @@ __global__ void __launch_bounds__(RT) tri_inv_kernel(const float* __restrict__ F
     __syncthreads();
   }
   for (int i = RT - 1; i >= 0; --i) {
-    float acc = (i == c) ? 1.f : 0.f;
-#pragma unroll 8
-    for (int k = i + 1; k <= c; ++k) acc = fmaf(-Fs[i * RT + k], Xs[k * RT + c], acc);
-    Xs[i * RT + c] = (i <= c) ? acc * Fs[RT * RT + i] : 0.f;
+    // eight independent partial sums (k mod 8): the loads of a step are in flight together
+    // instead of one dependent fma chain waiting on each LDS read
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k0 = i + 1; k0 <= c; k0 += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 + u <= c) acc[u] = fmaf(-Fs[i * RT + k0 + u], Xs[(k0 + u) * RT + c], acc[u]);
+    }
+    const float sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    Xs[i * RT + c] = (i <= c) ? (((i == c) ? 1.f : 0.f) + sum) * Fs[RT * RT + i] : 0.f;
   }
   float* out = T + static_cast<long>(b) * RT * RT;
   for (int i = 0; i < RT; ++i) out[i * RT + c] = Xs[i * RT + c];
