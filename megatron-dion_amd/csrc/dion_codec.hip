@@ -2968,38 +2968,44 @@ __global__ void __launch_bounds__(256, 2) gram_h3_kernel(const GramArgs a) {
 // ============================================================================
 // T_b = F_b^-1 for the padded upper-triangular factor F_b of the factor kernels (RT x RT, then
 // its RT reciprocal diagonal entries: the INV = false output of sketch_qr_inv_kernel and
-// chol_reg_kernel), the operand of tsolve_mfma_kernel.  One block per matrix, thread c owns
-// column c and runs its back substitution, x_i = (d_ic - sum_{i < k <= c} F_ik x_k) (1/F_ii) for
-// i = c .. 0 (x_i = 0 for i > c), fp32, the k-sum in eight interleaved partial sums; the factor
-// row is a broadcast LDS read and the column lives in LDS (thread-private, consecutive banks
-// across threads).  A NaN diagonal
-// (a failed factorisation) makes its column and every later one NaN, as the substitution
-// would.  Numpy over 0-6 decades: the final P within 0.8-1.0x the error of an fp64 inverse
-// (DESIGN.md section 4).
+// chol_reg_kernel), the operand of tsolve_mfma_kernel.  One block per matrix; column c is
+// back-substituted by TIP adjacent lanes, x_i = (d_ic - sum_{i < k <= c} F_ik x_k) (1/F_ii) for
+// i = c .. 0 (x_i = 0 for i > c), fp32: lane p of the column sums the k = i + 1 + p (mod TIP)
+// terms and the partial sums meet by xor shuffles (every lane gets the same x_i); the factor
+// row is a broadcast LDS read, the column lives in LDS (column-major, padded).  A NaN diagonal (a failed
+// factorisation) makes its column and every later one NaN, as the substitution would.  Numpy
+// over 0-6 decades: the final P within 0.8-1.0x the error of an fp64 inverse (DESIGN.md
+// section 4).  One lane per column measured 55 / 185 us per 16-matrix launch at r = 64 / 128
+// (one-stream profile, profiles/r05/n_gemm_default.txt); eight interleaved sums per lane 116 / 470.
 template <int RT>
-__global__ void __launch_bounds__(RT) tri_inv_kernel(const float* __restrict__ F, float* __restrict__ T) {
+constexpr int tri_inv_tip() { return RT >= 128 ? 8 : 16; }
+template <int RT>
+__global__ void __launch_bounds__(RT * tri_inv_tip<RT>()) tri_inv_kernel(const float* __restrict__ F,
+                                                                           float* __restrict__ T) {
+  constexpr int TIP = tri_inv_tip<RT>();
+  constexpr int NT = RT * TIP;
   __shared__ __attribute__((aligned(16))) float Fs[RT * RT + RT];
-  __shared__ float Xs[RT * RT];  // Xs[k RT + c] = x_k of column c
-  const int b = blockIdx.x, c = threadIdx.x;
+  constexpr int LDX = RT + TIP;   // Xs[c LDX + k] = x_k of column c: the TIP lanes of a column
+  __shared__ float Xs[RT * LDX];  // read consecutive k, and columns sit TIP banks apart
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int c = tid / TIP, p = tid % TIP;
   {
     const f32x4* src = reinterpret_cast<const f32x4*>(F + static_cast<long>(b) * (RT * RT + RT));
-    for (int i = c; i < (RT * RT + RT) / 4; i += RT) reinterpret_cast<f32x4*>(Fs)[i] = src[i];
+    for (int i = tid; i < (RT * RT + RT) / 4; i += NT) reinterpret_cast<f32x4*>(Fs)[i] = src[i];
     __syncthreads();
   }
   for (int i = RT - 1; i >= 0; --i) {
-    // eight independent partial sums (k mod 8): the loads of a step are in flight together
-    // instead of one dependent fma chain waiting on each LDS read
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int k0 = i + 1; k0 <= c; k0 += 8) {
+    float acc = 0.f;
+    for (int k = i + 1 + p; k <= c; k += TIP) acc = fmaf(-Fs[i * RT + k], Xs[c * LDX + k], acc);
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (k0 + u <= c) acc[u] = fmaf(-Fs[i * RT + k0 + u], Xs[(k0 + u) * RT + c], acc[u]);
-    }
-    const float sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-    Xs[i * RT + c] = (i <= c) ? (((i == c) ? 1.f : 0.f) + sum) * Fs[RT * RT + i] : 0.f;
+    for (int o = 1; o < TIP; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    const float x = (i <= c) ? (((i == c) ? 1.f : 0.f) + acc) * Fs[RT * RT + i] : 0.f;
+    if (p == 0) Xs[c * LDX + i] = x;
+    __builtin_amdgcn_wave_barrier();  // the column's lanes share a wave: LDS in order
   }
+  __syncthreads();
   float* out = T + static_cast<long>(b) * RT * RT;
-  for (int i = 0; i < RT; ++i) out[i * RT + c] = Xs[i * RT + c];
+  for (int idx = tid; idx < RT * RT; idx += NT) out[idx] = Xs[(idx % RT) * LDX + idx / RT];
 }
 
 constexpr int kTgWavesImg = 2, kTgWavesDirect = 4;
@@ -5092,10 +5098,16 @@ int launch_sketch_qr_inv(const float* SP, float* Rinv, int K, int r, int batch, 
     constexpr int CPWv = decltype(CPWc)::value;
     using XTv = typename decltype(XTc)::type;
     if (!inv) {
-      int rc = allow_lds(sketch_qr_inv_kernel<RPLv, CPWv, XTv, false>, lds);
+      // more waves per matrix where each wave keeps >= 8 columns (the column arithmetic and
+      // its reductions are the same whichever wave owns the column: bitwise the same factor;
+      // K 128 / r 64: 62.0 -> 51.1 us, K 256 / r 128: 233.2 -> 166.9 us per 16 matrices,
+      // scripts/ubench/qr_ab.hip, profiles/r05/o_qr_tri_inv.txt)
+      constexpr int NWQ = CPWv >= 32 ? 16 : (CPWv >= 16 ? 8 : 4);
+      constexpr int CPWq = CPWv * 4 / NWQ;
+      int rc = allow_lds(sketch_qr_inv_kernel<RPLv, CPWq, XTv, false, NWQ>, lds);
       if (rc != DION_OK) return rc;
-      hipLaunchKernelGGL((sketch_qr_inv_kernel<RPLv, CPWv, XTv, false>), dim3(batch), dim3(256), lds, st, SP, Rinv,
-                         K, r, trsm_rt(r));
+      hipLaunchKernelGGL((sketch_qr_inv_kernel<RPLv, CPWq, XTv, false, NWQ>), dim3(batch), dim3(64 * NWQ), lds, st, SP,
+                         Rinv, K, r, trsm_rt(r));
       return check_launch("sketch_qr");
     }
     int rc = allow_lds(sketch_qr_inv_kernel<RPLv, CPWv, XTv>, lds);
@@ -5153,9 +5165,9 @@ bool tsolve_gemm_ok(int mp, int r) { return DION_TSOLVE_GEMM && (r == 32 || r ==
 
 int launch_tri_inv(const float* F, float* T, int r, int batch, hipStream_t st) {
   switch (r) {
-    case 32: hipLaunchKernelGGL((tri_inv_kernel<32>), dim3(batch), dim3(32), 0, st, F, T); break;
-    case 64: hipLaunchKernelGGL((tri_inv_kernel<64>), dim3(batch), dim3(64), 0, st, F, T); break;
-    case 128: hipLaunchKernelGGL((tri_inv_kernel<128>), dim3(batch), dim3(128), 0, st, F, T); break;
+    case 32: hipLaunchKernelGGL((tri_inv_kernel<32>), dim3(batch), dim3(32 * tri_inv_tip<32>()), 0, st, F, T); break;
+    case 64: hipLaunchKernelGGL((tri_inv_kernel<64>), dim3(batch), dim3(64 * tri_inv_tip<64>()), 0, st, F, T); break;
+    case 128: hipLaunchKernelGGL((tri_inv_kernel<128>), dim3(batch), dim3(128 * tri_inv_tip<128>()), 0, st, F, T); break;
     default: return fail(DION_E_UNSUPPORTED, "tri_inv r=%d", r);
   }
   return check_launch("tri_inv");

@@ -71,13 +71,13 @@ void sweep() {
     constexpr int RT = R;
     float* dT;
     CKU(hipMalloc(&dT, static_cast<size_t>(B) * RT * RT * 4));
-    hipLaunchKernelGGL((tri_inv_kernel<RT>), dim3(B), dim3(RT), 0, 0, dF, dT);
+    hipLaunchKernelGGL((tri_inv_kernel<RT>), dim3(B), dim3(RT * tri_inv_tip<RT>()), 0, 0, dF, dT);
     CKU(hipDeviceSynchronize());
     hipEvent_t e0, e1;
     CKU(hipEventCreate(&e0));
     CKU(hipEventCreate(&e1));
     CKU(hipEventRecord(e0));
-    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((tri_inv_kernel<RT>), dim3(B), dim3(RT), 0, 0, dF, dT);
+    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((tri_inv_kernel<RT>), dim3(B), dim3(RT * tri_inv_tip<RT>()), 0, 0, dF, dT);
     CKU(hipEventRecord(e1));
     CKU(hipEventSynchronize(e1));
     float ms;
