@@ -1048,6 +1048,28 @@ __global__ void __launch_bounds__(256) householder_qr_kernel(const float* __rest
   }
 }
 
+// the back substitution itself, for a block of nt threads (TIP lanes per column, TIP adjacent
+// lanes of one wave): F upper-triangular n x n at F[i ldf + k] (LDS), dinv[i] = 1 / F[i][i]
+// (LDS), Xs the n x ldx column scratch (LDS, ldx = n + TIP), out the n x n row-major inverse
+template <int TIP>
+__device__ __forceinline__ void tri_inv_cols(const float* F, int ldf, const float* dinv, float* Xs, int ldx, int n,
+                                             float* __restrict__ out, int tid, int nt) {
+  const int c = tid / TIP, p = tid % TIP;
+  const bool act = c < n;
+  for (int i = n - 1; i >= 0; --i) {
+    float acc = 0.f;
+    if (act)
+      for (int k = i + 1 + p; k <= c; k += TIP) acc = fmaf(-F[i * ldf + k], Xs[c * ldx + k], acc);
+#pragma unroll
+    for (int o = 1; o < TIP; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    const float x = (act && i <= c) ? (((i == c) ? 1.f : 0.f) + acc) * dinv[i] : 0.f;
+    if (act && p == 0) Xs[c * ldx + i] = x;
+    __builtin_amdgcn_wave_barrier();  // the column's lanes share a wave: LDS in order
+  }
+  __syncthreads();
+  for (int idx = tid; idx < n * n; idx += nt) out[idx] = Xs[(idx % n) * ldx + idx / n];
+}
+
 // ============================================================================
 // Small-factor kernels of the randomised Cholesky QR, one block per matrix.
 //
@@ -1098,7 +1120,7 @@ __device__ __forceinline__ void write_padded_factor(const float* Rs, int rld, in
   for (int j = tid; j < rt; j += nt) O[rt * rt + j] = j < r ? 1.f / Rs[j * rld + j] : 1.f;
 }
 
-template <int RPL, int CPW, typename XT, bool INV = true, int NWQ = 4>
+template <int RPL, int CPW, typename XT, bool INV = true, int NWQ = 4, bool TINV = false>
 __global__ void __launch_bounds__(64 * NWQ) sketch_qr_inv_kernel(const float* __restrict__ SP, float* __restrict__ Rinv,
                                                                  int K, int r, int rt = 0) {
   extern __shared__ __attribute__((aligned(16))) char qsm[];
@@ -1200,6 +1222,15 @@ __global__ void __launch_bounds__(64 * NWQ) sketch_qr_inv_kernel(const float* __
       trail(std::integral_constant<int, (CPW / 4 > 0 ? CPW / 4 : 1)>{});
   }
   __syncthreads();
+  if constexpr (TINV) {
+    // R^-1 in fp32 by tri_inv_cols (8 lanes per column: r = 8 NWQ), straight after the QR; the
+    // reflector buffer holds the reciprocal diagonal, Xs the column scratch (r x (r + 8) floats)
+    for (int j = tid; j < r; j += blockDim.x) vbuf[j] = 1.f / Rs[j * rld + j];
+    __syncthreads();
+    tri_inv_cols<8>(Rs, rld, vbuf, reinterpret_cast<float*>(Xs), r + 8, r, Rinv + static_cast<long>(b) * r * r, tid,
+                    blockDim.x);
+    return;
+  }
   if constexpr (!INV) {
     write_padded_factor(Rs, rld, r, rt, Rinv + static_cast<long>(b) * (rt * rt + rt), tid, blockDim.x);
     return;
@@ -2101,11 +2132,15 @@ __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_st
 // turns their P columns into NaN (cholesky_ex does not raise; the fix-up's nan_to_num zeroes
 // them, ortho.py:113 / kernels.py:157-204).
 // ============================================================================
-template <int RP, int NT = 256>
+template <int RP, int NT = 256, bool TINV = false>
 __global__ void __launch_bounds__(NT) chol_reg_kernel(const float* __restrict__ G_in, float* __restrict__ Fout,
                                                       int r) {
   constexpr int NG = NT / RP, RPT = RP / NG;
   __shared__ float row[2][RP];
+  // TINV: the factor kept in LDS and inverted in fp32 right after (tri_inv_cols, NG lanes per
+  // column); Fout then receives R^-1 (RP x RP) instead of the padded factor
+  __shared__ float Fs[TINV ? RP * RP + RP : 1];
+  __shared__ float Xs[TINV ? RP * (RP + NG) : 1];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int c = tid % RP, g = tid / RP;
@@ -2135,19 +2170,29 @@ __global__ void __launch_bounds__(NT) chol_reg_kernel(const float* __restrict__ 
     const float ujj = sqrtf(d);
     const float inv = 1.f / ujj;
     const float uc = row[buf][c] * inv;
-    if (g == j % NG) O[j * RP + c] = c < j ? 0.f : (c == j ? ujj : uc);
-    if (tid == 0) O[RP * RP + j] = inv;
+    if constexpr (TINV) {
+      if (g == j % NG) Fs[j * RP + c] = c < j ? 0.f : (c == j ? ujj : uc);
+      if (tid == 0) Fs[RP * RP + j] = inv;
+    } else {
+      if (g == j % NG) O[j * RP + c] = c < j ? 0.f : (c == j ? ujj : uc);
+      if (tid == 0) O[RP * RP + j] = inv;
+    }
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int i = g + NG * q;
       if (i > j) a[q] -= (row[buf][i] * inv) * uc;
     }
   }
+  float* F = TINV ? Fs : O;
   for (int idx = tid; idx < (RP - jf) * RP; idx += NT) {
     const int i = jf + idx / RP, cc = idx % RP;
-    O[i * RP + cc] = (i == cc) ? __builtin_nanf("") : 0.f;
+    F[i * RP + cc] = (i == cc) ? __builtin_nanf("") : 0.f;
   }
-  for (int j = jf + tid; j < RP; j += NT) O[RP * RP + j] = __builtin_nanf("");
+  for (int j = jf + tid; j < RP; j += NT) F[RP * RP + j] = __builtin_nanf("");
+  if constexpr (TINV) {
+    __syncthreads();
+    tri_inv_cols<NG>(Fs, RP, Fs + RP * RP, Xs, RP + NG, RP, Fout + static_cast<long>(b) * RP * RP, tid, NT);
+  }
 }
 
 // ============================================================================
@@ -2975,8 +3020,11 @@ __global__ void __launch_bounds__(256, 2) gram_h3_kernel(const GramArgs a) {
 // row is a broadcast LDS read, the column lives in LDS (column-major, padded).  A NaN diagonal (a failed
 // factorisation) makes its column and every later one NaN, as the substitution would.  Numpy
 // over 0-6 decades: the final P within 0.8-1.0x the error of an fp64 inverse (DESIGN.md
-// section 4).  One lane per column measured 55 / 185 us per 16-matrix launch at r = 64 / 128
-// (one-stream profile, profiles/r05/n_gemm_default.txt); eight interleaved sums per lane 116 / 470.
+// section 4).  Per 16-matrix launch at r = 64 / 128: one lane per column 55 / 185 us (one-stream
+// profile, profiles/r05/n_gemm_default.txt), eight interleaved sums per lane 116 / 470, 8-16 lanes
+// per column 23.2 / 71.5 (scripts/ubench/qr_ab.hip, profiles/r05/p_tri_inv_lanes.txt).  In the
+// orthonormalisation it runs fused into the QR and Cholesky kernels (TINV); the kernel stays for
+// the microbenchmark.
 template <int RT>
 constexpr int tri_inv_tip() { return RT >= 128 ? 8 : 16; }
 template <int RT>
@@ -2984,28 +3032,16 @@ __global__ void __launch_bounds__(RT * tri_inv_tip<RT>()) tri_inv_kernel(const f
                                                                            float* __restrict__ T) {
   constexpr int TIP = tri_inv_tip<RT>();
   constexpr int NT = RT * TIP;
-  __shared__ __attribute__((aligned(16))) float Fs[RT * RT + RT];
   constexpr int LDX = RT + TIP;   // Xs[c LDX + k] = x_k of column c: the TIP lanes of a column
+  __shared__ __attribute__((aligned(16))) float Fs[RT * RT + RT];
   __shared__ float Xs[RT * LDX];  // read consecutive k, and columns sit TIP banks apart
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int c = tid / TIP, p = tid % TIP;
   {
     const f32x4* src = reinterpret_cast<const f32x4*>(F + static_cast<long>(b) * (RT * RT + RT));
     for (int i = tid; i < (RT * RT + RT) / 4; i += NT) reinterpret_cast<f32x4*>(Fs)[i] = src[i];
     __syncthreads();
   }
-  for (int i = RT - 1; i >= 0; --i) {
-    float acc = 0.f;
-    for (int k = i + 1 + p; k <= c; k += TIP) acc = fmaf(-Fs[i * RT + k], Xs[c * LDX + k], acc);
-#pragma unroll
-    for (int o = 1; o < TIP; o <<= 1) acc += __shfl_xor(acc, o, 64);
-    const float x = (i <= c) ? (((i == c) ? 1.f : 0.f) + acc) * Fs[RT * RT + i] : 0.f;
-    if (p == 0) Xs[c * LDX + i] = x;
-    __builtin_amdgcn_wave_barrier();  // the column's lanes share a wave: LDS in order
-  }
-  __syncthreads();
-  float* out = T + static_cast<long>(b) * RT * RT;
-  for (int idx = tid; idx < RT * RT; idx += NT) out[idx] = Xs[(idx % RT) * LDX + idx / RT];
+  tri_inv_cols<TIP>(Fs, RT, Fs + RT * RT, Xs, LDX, RT, T + static_cast<long>(b) * RT * RT, tid, NT);
 }
 
 constexpr int kTgWavesImg = 2, kTgWavesDirect = 4;
@@ -5088,15 +5124,28 @@ int allow_lds(K kernel, size_t bytes) {
 
 // inv: R^-1 (r x r, the distributed RCQR's exchange format); else the padded factor for
 // trsm_right_kernel (factor_floats(r) per matrix)
-int launch_sketch_qr_inv(const float* SP, float* Rinv, int K, int r, int batch, hipStream_t st, bool inv = true) {
+int launch_sketch_qr_inv(const float* SP, float* Rinv, int K, int r, int batch, hipStream_t st, bool inv = true,
+                         bool tinv = false) {
   if (K > 256 || r > 128 || r > K) return fail(DION_E_UNSUPPORTED, "sketch QR %dx%d", K, r);
   const bool dbl = r <= 64;
-  const size_t lds = ((sizeof(float) * (520 + static_cast<size_t>(r) * (r + 1)) + 15) / 16) * 16 +
-                     (dbl ? sizeof(double) : sizeof(float)) * static_cast<size_t>(r) * r;
+  const size_t base_lds = ((sizeof(float) * (520 + static_cast<size_t>(r) * (r + 1)) + 15) / 16) * 16;
+  const size_t lds = base_lds + std::max((dbl ? sizeof(double) : sizeof(float)) * static_cast<size_t>(r) * r,
+                                         tinv ? sizeof(float) * static_cast<size_t>(r) * (r + 8) : size_t(0));
   auto go = [&](auto RPLc, auto CPWc, auto XTc) {
     constexpr int RPLv = decltype(RPLc)::value;
     constexpr int CPWv = decltype(CPWc)::value;
     using XTv = typename decltype(XTc)::type;
+    if (tinv) {
+      // the fp32 inverse fused after the QR (the GEMM solves): 8 lanes per column, r = 8 NWQ
+      constexpr int NWQ = CPWv >= 32 ? 16 : (CPWv >= 16 ? 8 : 4);
+      constexpr int CPWq = CPWv * 4 / NWQ;
+      if (r * 8 != 64 * NWQ) return fail(DION_E_UNSUPPORTED, "fused sketch-QR inverse at r=%d", r);
+      int rc = allow_lds(sketch_qr_inv_kernel<RPLv, CPWq, XTv, false, NWQ, true>, lds);
+      if (rc != DION_OK) return rc;
+      hipLaunchKernelGGL((sketch_qr_inv_kernel<RPLv, CPWq, XTv, false, NWQ, true>), dim3(batch), dim3(64 * NWQ), lds,
+                         st, SP, Rinv, K, r, 0);
+      return check_launch("sketch_qr(inverse)");
+    }
     if (!inv) {
       // more waves per matrix where each wave keeps >= 8 columns (the column arithmetic and
       // its reductions are the same whichever wave owns the column: bitwise the same factor;
@@ -5127,7 +5176,18 @@ int launch_sketch_qr_inv(const float* SP, float* Rinv, int K, int r, int batch, 
   return go(std::integral_constant<int, 4>{}, std::integral_constant<int, 32>{}, F{});
 }
 
-int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t st, bool inv = true) {
+int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t st, bool inv = true,
+                    bool tinv = false) {
+  if (tinv) {
+    // the GEMM solves: Cholesky + fp32 inverse in one launch (r = RP only)
+    switch (r) {
+      case 32: hipLaunchKernelGGL((chol_reg_kernel<32, 256, true>), dim3(batch), dim3(256), 0, st, G, Uinv, r); break;
+      case 64: hipLaunchKernelGGL((chol_reg_kernel<64, 512, true>), dim3(batch), dim3(512), 0, st, G, Uinv, r); break;
+      case 128: hipLaunchKernelGGL((chol_reg_kernel<128, 1024, true>), dim3(batch), dim3(1024), 0, st, G, Uinv, r); break;
+      default: return fail(DION_E_UNSUPPORTED, "fused Cholesky inverse at r=%d", r);
+    }
+    return check_launch("chol(inverse)");
+  }
   const bool dbl = r <= 96;
   const size_t lds = ((sizeof(float) * (static_cast<size_t>(r) * (r + 1) + r + 4) + 15) / 16) * 16 +
                      (dbl ? sizeof(double) : sizeof(float)) * static_cast<size_t>(r) * r;
@@ -5803,8 +5863,8 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     // (2) R1 = qr(S P).R, (3) P1 = P R1^-1 (into workspace): by forward substitution, or as
     // the GEMM P T1 with the explicit inverse T1 (tsolve_mfma_kernel)
     const bool gemm = tsolve_gemm_ok(mp, r);
-    rc = launch_sketch_qr_inv(sp, fac, K, r, nb, st, false);
-    if (rc == DION_OK && gemm) rc = launch_tri_inv(fac, r1, r, nb, st);  // T1 = R1^-1
+    // gemm: T1 = R1^-1 written by the QR kernel itself (r1)
+    rc = gemm ? launch_sketch_qr_inv(sp, r1, K, r, nb, st, false, true) : launch_sketch_qr_inv(sp, fac, K, r, nb, st, false);
     if (rc != DION_OK) return rc;
     rc = gemm ? launch_tsolve(Pb, p1, r1, mp, r, nb, st, false, nullptr, nullptr, 0, 0)
               : launch_trsm(Pb, p1, fac, mp, r, nb, st);
@@ -5824,8 +5884,8 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     }
     if (rc != DION_OK) return rc;
     // (5) R2 = chol_upper(Gram)
-    rc = launch_chol_inv(gm, fac, r, nb, st, false);
-    if (rc == DION_OK && gemm) rc = launch_tri_inv(fac, r1, r, nb, st);  // T2 = R2^-1
+    // gemm: T2 = R2^-1 written by the Cholesky kernel itself (r1)
+    rc = gemm ? launch_chol_inv(gm, r1, r, nb, st, false, true) : launch_chol_inv(gm, fac, r, nb, st, false);
     if (rc != DION_OK) return rc;
     (void)r2;
     // (6) P = P1 R2^-1 (back into the caller's buffer), with the fix-up and pass B's split
