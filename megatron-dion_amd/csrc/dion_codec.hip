@@ -2304,6 +2304,7 @@ struct TrsmArgs {
   f16x8* psplit;              // FINAL: pass-B split of P (null: none)
   long pstride;               // f16x8 units per matrix of psplit
   int mp, kmap;
+  float* gram;                // tsolve_mfma_kernel GRAM: (batch, gridDim.x, RT, RT) partial Grams of X
 };
 
 constexpr int kTrsmWaves = 2;  // 128-row blocks: 2 x 16 KB row images
@@ -3046,10 +3047,11 @@ __global__ void __launch_bounds__(RT * tri_inv_tip<RT>()) tri_inv_kernel(const f
 
 constexpr int kTgWavesImg = 2, kTgWavesDirect = 4;
 
-template <int RT, bool FINAL>
+template <int RT, bool FINAL, bool GRAM = false>
 __global__ void __launch_bounds__(64 * (RT <= 64 ? kTgWavesImg : kTgWavesDirect), RT <= 64 ? 3 : 2)
 tsolve_mfma_kernel(const TrsmArgs a) {
   static_assert(RT == 32 || RT == 64 || RT == 128, "tsolve_mfma_kernel: r = 32, 64 or 128");
+  static_assert(!GRAM || (RT <= 64 && !FINAL), "tsolve_mfma_kernel: the fused Gram is for the first solve at r <= 64");
   constexpr bool IMG = RT <= 64;
   constexpr int NW = IMG ? kTgWavesImg : kTgWavesDirect;
   constexpr int CH = RT / 4;   // 16-B chunks per row
@@ -3082,7 +3084,16 @@ tsolve_mfma_kernel(const TrsmArgs a) {
     }
     __syncthreads();
   }
-  const long row0 = static_cast<long>(blockIdx.x) * (64 * NW) + wave * 64;
+  constexpr int RB = RT / 16;
+  f32x4 gacc[GRAM ? RB : 1][GRAM ? RB : 1];
+  if constexpr (GRAM) {
+#pragma unroll
+    for (int ta = 0; ta < RB; ++ta)
+#pragma unroll
+      for (int cb = 0; cb < RB; ++cb) gacc[ta][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // one 64-row chunk of this wave: stage, solve, store (and, GRAM, add X^T X of the chunk)
+  auto chunk = [&](const long row0) {
   const int nrows = static_cast<int>(min(static_cast<long>(64), static_cast<long>(mp) - row0));
   if (nrows <= 0) return;
   const float* src = a.src + (static_cast<long>(b) * mp + row0) * RT;
@@ -3098,8 +3109,8 @@ tsolve_mfma_kernel(const TrsmArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   const bool zero = FINAL && a.nonzero != nullptr && a.nonzero[b] == 0u;
-  for (int tile = 0; tile < 4; ++tile) {
-    if (16 * tile >= nrows) break;
+  float xmax = 0.f;  // GRAM: max |X| over the chunk's rows, the Gram's split scale
+  auto tile_body = [&](const int tile) {
     const int row = 16 * tile + t;
     const bool valid = row < nrows;
     // this lane's B operand: P[row][32 j + 8 g .. + 7] for every k-step j
@@ -3147,6 +3158,7 @@ tsolve_mfma_kernel(const TrsmArgs a) {
         float y = (acc[q] * irow) * ic[q];
         if constexpr (FINAL) y = zero ? 0.f : (a.nonzero != nullptr ? nan_to_num(y) : y);
         x[i][q] = y;
+        if constexpr (GRAM) xmax = valid ? fmaxf(xmax, fabsf(y)) : xmax;
       }
     }
     if (valid) {
@@ -3157,6 +3169,19 @@ tsolve_mfma_kernel(const TrsmArgs a) {
         else
           reinterpret_cast<f32x4*>(dst + static_cast<long>(row) * RT)[4 * i + g] = x[i];
       }
+    }
+  };
+  if constexpr (GRAM) {
+    // one tile at a time: the unrolled tile loop beside the Gram accumulators needs > 256 VGPRs
+#pragma unroll 1
+    for (int tile = 0; tile < 4; ++tile) {
+      if (16 * tile >= nrows) break;
+      tile_body(tile);
+    }
+  } else {
+    for (int tile = 0; tile < 4; ++tile) {
+      if (16 * tile >= nrows) break;
+      tile_body(tile);
     }
   }
   if constexpr (IMG) {
@@ -3190,6 +3215,83 @@ tsolve_mfma_kernel(const TrsmArgs a) {
           out[grp * 128 + 64 + lane] = sp.lo;
         }
       }
+    }
+    if constexpr (GRAM) {
+      // X^T X of the chunk from the image, as gram_h3_kernel but with one scale for the chunk
+      // (its max |X|, from the solve): lane (t, g) splits rows 8 g .. + 7 of column 16 cb + t
+      // of each 32-row k-step (the A operand of block cb is the B operand of block cb); rows
+      // past nrows count as zero
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) xmax = fmaxf(xmax, __shfl_xor(xmax, o, 64));
+      float inv;
+      const float sc = h3_scale(xmax, inv);
+      const float* wf = reinterpret_cast<const float*>(w);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (32 * ks >= nrows) break;
+        Split2h S[RB];
+#pragma unroll
+        for (int cb = 0; cb < RB; ++cb) {
+          f32x4 v[2];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int rr = 32 * ks + 8 * g + e, col = 16 * cb + t;
+            v[e >> 2][e & 3] = rr < nrows ? wf[(rr * CH + ((col >> 2) ^ trsm_swz<RT>(rr))) * 4 + (col & 3)] : 0.f;
+          }
+          split2h(v[0], v[1], sc, S[cb]);
+        }
+        // the block upper triangle only (cb >= ta): chol_reg_kernel reads G on and above the
+        // diagonal; the lower tiles are written as zeros
+#pragma unroll
+        for (int ta = 0; ta < RB; ++ta)
+#pragma unroll
+          for (int cb = ta; cb < RB; ++cb) {
+            const f32x4 d = mfma3h(S[ta], S[cb], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gacc[ta][cb][q] = fmaf(d[q] * inv, inv, gacc[ta][cb][q]);
+          }
+      }
+    }
+  }
+  };
+  if constexpr (!GRAM) {
+    chunk(static_cast<long>(blockIdx.x) * (64 * NW) + wave * 64);
+  } else {
+    // persistent over the rows: block x of gridDim.x takes the 64 NW-row steps x, x + gridDim.x, ..
+    for (long base = static_cast<long>(blockIdx.x) * (64 * NW); base < mp; base += static_cast<long>(gridDim.x) * (64 * NW))
+      chunk(base + wave * 64);
+    // the waves' partial Grams summed through LDS (the image of wave 1), then one slab per block:
+    // lane (t, g), element q of tile (ta, cb) = G[16 ta + 4 g + q][16 cb + t]
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(img[IMG ? NW - 1 : 0]);
+    for (int wv = NW - 1; wv >= 1; --wv) {
+      if (wave == wv) {
+#pragma unroll
+        for (int ta = 0; ta < RB; ++ta)
+#pragma unroll
+          for (int cb = ta; cb < RB; ++cb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[((ta * RB + cb) * 4 + q) * 64 + lane] = gacc[ta][cb][q];
+      }
+      __syncthreads();
+      if (wave == 0) {
+#pragma unroll
+        for (int ta = 0; ta < RB; ++ta)
+#pragma unroll
+          for (int cb = ta; cb < RB; ++cb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gacc[ta][cb][q] += red[((ta * RB + cb) * 4 + q) * 64 + lane];
+      }
+      __syncthreads();
+    }
+    if (wave == 0) {
+      float* go = a.gram + (static_cast<long>(b) * gridDim.x + blockIdx.x) * RT * RT;
+#pragma unroll
+      for (int ta = 0; ta < RB; ++ta)
+#pragma unroll
+        for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) go[(16 * ta + 4 * g + q) * RT + 16 * cb + t] = cb >= ta ? gacc[ta][cb][q] : 0.f;
     }
   }
 }
@@ -4820,6 +4922,23 @@ struct OrthoPlan {
   size_t off_sk_slab, off_sp, off_r1, off_gslab, off_g, off_r2, off_inv, off_p1, total;
 };
 
+// the orthonormalisation's two solves as GEMMs with the explicit inverses (tri_inv_kernel +
+// tsolve_mfma_kernel) for r = 32, 64, 128; 0 (a dev build option) keeps the substitution
+// kernels.  Same-box Llama 460.6 / 449.8 -> 465.8 / 455.2 GiB/s, Mixtral 350.0 -> 352.3 with the
+// inverses from the factor kernels (profiles/r05/m_solves_gemm_ab.txt); the solves alone beside a streaming copy:
+// r = 64 8.4 vs 33.7 us marginal per fc1 group, r = 128 41.2 vs 105.9 (scripts/ubench/trsm_conc.hip)
+#ifndef DION_TSOLVE_GEMM
+#define DION_TSOLVE_GEMM 1
+#endif
+bool tsolve_gemm_ok(int mp, int r) { return DION_TSOLVE_GEMM && (r == 32 || r == 64 || r == 128) && mp > r; }
+
+// persistent blocks of the first solve + Gram per matrix (tsolve_mfma_kernel GRAM)
+int tgram_chunks(int mp, int batch) {
+  const long steps = ceil_div(mp, 64 * kTgWavesImg);
+  const long want = ceil_div(1024L, batch > 0 ? batch : 1);
+  return static_cast<int>(steps < want ? steps : want);
+}
+
 OrthoPlan ortho_plan(int mp, int r, int batch, float oversample) {
   OrthoPlan p{};
   p.plain_qr = (mp <= r);
@@ -4838,7 +4957,10 @@ OrthoPlan ortho_plan(int mp, int r, int batch, float oversample) {
   p.off_sk_slab = take(std::max(slab_bytes(p.sk, batch, r), rad_slab));
   p.off_sp = take(sizeof(float) * static_cast<size_t>(batch) * p.k * r);
   p.off_r1 = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
-  p.off_gslab = take(slab_bytes(p.gr, batch, r));
+  p.off_gslab = take(std::max(slab_bytes(p.gr, batch, r),
+                              tsolve_gemm_ok(mp, r) && r <= 64
+                                  ? sizeof(float) * static_cast<size_t>(batch) * tgram_chunks(mp, batch) * r * r
+                                  : size_t(0)));
   p.off_g = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
   p.off_r2 = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
   p.off_inv = take(sizeof(float) * static_cast<size_t>(batch) * std::max(static_cast<size_t>(r) * r, factor_floats(r)));
@@ -5213,15 +5335,6 @@ int launch_chol_inv(const float* G, float* Uinv, int r, int batch, hipStream_t s
   return check_launch("chol_inv");
 }
 
-// the orthonormalisation's two solves as GEMMs with the explicit inverses (tri_inv_kernel +
-// tsolve_mfma_kernel) for r = 32, 64, 128; 0 (a dev build option) keeps the substitution
-// kernels.  Same-box Llama 460.6 / 449.8 -> 465.8 / 455.2 GiB/s, Mixtral 350.0 -> 352.3 with the
-// inverses from the factor kernels (profiles/r05/m_solves_gemm_ab.txt); the solves alone beside a streaming copy:
-// r = 64 8.4 vs 33.7 us marginal per fc1 group, r = 128 41.2 vs 105.9 (scripts/ubench/trsm_conc.hip)
-#ifndef DION_TSOLVE_GEMM
-#define DION_TSOLVE_GEMM 1
-#endif
-bool tsolve_gemm_ok(int mp, int r) { return DION_TSOLVE_GEMM && (r == 32 || r == 64 || r == 128) && mp > r; }
 
 int launch_tri_inv(const float* F, float* T, int r, int batch, hipStream_t st) {
   switch (r) {
@@ -5231,6 +5344,21 @@ int launch_tri_inv(const float* F, float* T, int r, int batch, hipStream_t st) {
     default: return fail(DION_E_UNSUPPORTED, "tri_inv r=%d", r);
   }
   return check_launch("tri_inv");
+}
+
+// the first solve with the Gram of its output folded in (r = 32 / 64: tsolve_mfma_kernel GRAM):
+// persistent blocks, one partial Gram per block into `gram` (batch x tgram_chunks x r x r)
+int launch_tsolve_gram(const float* src, float* dst, const float* T, int mp, int r, int batch, float* gram,
+                       hipStream_t st) {
+  TrsmArgs ta{src, dst, T, nullptr, nullptr, 0, mp, 0, gram};
+  const dim3 grid(static_cast<unsigned>(tgram_chunks(mp, batch)), batch);
+  if (r == 64)
+    hipLaunchKernelGGL((tsolve_mfma_kernel<64, false, true>), grid, dim3(64 * kTgWavesImg), 0, st, ta);
+  else if (r == 32)
+    hipLaunchKernelGGL((tsolve_mfma_kernel<32, false, true>), grid, dim3(64 * kTgWavesImg), 0, st, ta);
+  else
+    return fail(DION_E_UNSUPPORTED, "tsolve+Gram r=%d", r);
+  return check_launch("tsolve_mfma(gram)");
 }
 
 int launch_tsolve(const float* src, float* dst, const float* T, int mp, int r, int batch, hipStream_t st, bool final_,
@@ -5866,11 +5994,21 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     // gemm: T1 = R1^-1 written by the QR kernel itself (r1)
     rc = gemm ? launch_sketch_qr_inv(sp, r1, K, r, nb, st, false, true) : launch_sketch_qr_inv(sp, fac, K, r, nb, st, false);
     if (rc != DION_OK) return rc;
-    rc = gemm ? launch_tsolve(Pb, p1, r1, mp, r, nb, st, false, nullptr, nullptr, 0, 0)
-              : launch_trsm(Pb, p1, fac, mp, r, nb, st);
+    // gemm at r <= 64: the solve also sums P1^T P1 (upper block triangle) per block
+    const bool tgram = gemm && r <= 64;
+    if (tgram) {
+      const int nck = tgram_chunks(mp, nb);
+      rc = launch_tsolve_gram(Pb, p1, r1, mp, r, nb, nck > 1 ? gslab : gm, st);
+      if (rc == DION_OK && nck > 1) rc = launch_reduce(gm, gslab, nck, static_cast<long>(r) * r, nb, st);
+    } else {
+      rc = gemm ? launch_tsolve(Pb, p1, r1, mp, r, nb, st, false, nullptr, nullptr, 0, 0)
+                : launch_trsm(Pb, p1, fac, mp, r, nb, st);
+    }
     if (rc != DION_OK) return rc;
     // (4) Gram = P1^T P1
-    if (gram_h3_ok(mp, r)) {
+    if (tgram) {
+      // done by the solve
+    } else if (gram_h3_ok(mp, r)) {
       const GramArgs ga{p1, plan.gr.nchunk > 1 ? gslab : gm, mp, plan.gr.kchunk, plan.gr.nchunk};
       if (r == 64)
         hipLaunchKernelGGL((gram_h3_kernel<4>), dim3(plan.gr.nchunk, nb), dim3(256), 0, st, ga);
