@@ -4932,7 +4932,13 @@ struct OrthoPlan {
 #endif
 bool tsolve_gemm_ok(int mp, int r) { return DION_TSOLVE_GEMM && (r == 32 || r == 64 || r == 128) && mp > r; }
 
-// persistent blocks of the first solve + Gram per matrix (tsolve_mfma_kernel GRAM)
+// the first GEMM solve summing the Gram of its output (tsolve_mfma_kernel GRAM, r <= 64): off.
+// Alone it beats solve + gram_h3_kernel (58.3 vs 39.6 + 27.1 us per Llama group, one stream), in
+// the two-stream step it loses (Llama 469.5 / 469.2 -> 464.9 / 466.8 GiB/s, same box,
+// profiles/r05/r_tsolve_gram.txt): its persistent blocks hold 50 KB of LDS each for the whole
+// solve, beside the other stream's streaming kernel.
+constexpr bool kTsolveGram = false;
+// persistent blocks of the first solve + Gram per matrix
 int tgram_chunks(int mp, int batch) {
   const long steps = ceil_div(mp, 64 * kTgWavesImg);
   const long want = ceil_div(1024L, batch > 0 ? batch : 1);
@@ -4958,7 +4964,7 @@ OrthoPlan ortho_plan(int mp, int r, int batch, float oversample) {
   p.off_sp = take(sizeof(float) * static_cast<size_t>(batch) * p.k * r);
   p.off_r1 = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
   p.off_gslab = take(std::max(slab_bytes(p.gr, batch, r),
-                              tsolve_gemm_ok(mp, r) && r <= 64
+                              kTsolveGram && tsolve_gemm_ok(mp, r) && r <= 64
                                   ? sizeof(float) * static_cast<size_t>(batch) * tgram_chunks(mp, batch) * r * r
                                   : size_t(0)));
   p.off_g = take(sizeof(float) * static_cast<size_t>(batch) * r * r);
@@ -5995,7 +6001,7 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     rc = gemm ? launch_sketch_qr_inv(sp, r1, K, r, nb, st, false, true) : launch_sketch_qr_inv(sp, fac, K, r, nb, st, false);
     if (rc != DION_OK) return rc;
     // gemm at r <= 64: the solve also sums P1^T P1 (upper block triangle) per block
-    const bool tgram = gemm && r <= 64;
+    const bool tgram = kTsolveGram && gemm && r <= 64;
     if (tgram) {
       const int nck = tgram_chunks(mp, nb);
       rc = launch_tsolve_gram(Pb, p1, r1, mp, r, nb, nck > 1 ? gslab : gm, st);
