@@ -3047,12 +3047,22 @@ __global__ void __launch_bounds__(RT * tri_inv_tip<RT>()) tri_inv_kernel(const f
 
 constexpr int kTgWavesImg = 2, kTgWavesDirect = 4;
 
+// the LDS row image (IMG) only where the epilogue needs whole rows: the final solve's pass-B
+// split and the fused Gram; the first solve reads and writes HBM directly with 17 KB of LDS per
+// block instead of 50 KB (DION_TSOLVE_DIRECT_FIRST, a dev build option for A/B runs)
+#ifndef DION_TSOLVE_DIRECT_FIRST
+#define DION_TSOLVE_DIRECT_FIRST 1
+#endif
+template <int RT, bool FINAL, bool GRAM>
+constexpr bool tsolve_img() { return RT <= 64 && (FINAL || GRAM || !DION_TSOLVE_DIRECT_FIRST); }
+
 template <int RT, bool FINAL, bool GRAM = false>
-__global__ void __launch_bounds__(64 * (RT <= 64 ? kTgWavesImg : kTgWavesDirect), RT <= 64 ? 3 : 2)
+__global__ void __launch_bounds__(64 * (tsolve_img<RT, FINAL, GRAM>() ? kTgWavesImg : kTgWavesDirect),
+                                  (tsolve_img<RT, FINAL, GRAM>() ? 3 : 2))
 tsolve_mfma_kernel(const TrsmArgs a) {
   static_assert(RT == 32 || RT == 64 || RT == 128, "tsolve_mfma_kernel: r = 32, 64 or 128");
   static_assert(!GRAM || (RT <= 64 && !FINAL), "tsolve_mfma_kernel: the fused Gram is for the first solve at r <= 64");
-  constexpr bool IMG = RT <= 64;
+  constexpr bool IMG = tsolve_img<RT, FINAL, GRAM>();
   constexpr int NW = IMG ? kTgWavesImg : kTgWavesDirect;
   constexpr int CH = RT / 4;   // 16-B chunks per row
   constexpr int KS = RT / 32;  // 32-wide k-steps
@@ -5373,7 +5383,7 @@ int launch_tsolve(const float* src, float* dst, const float* T, int mp, int r, i
   auto go = [&](auto RTc, auto Fc) {
     constexpr int RT = decltype(RTc)::value;
     constexpr bool F = decltype(Fc)::value;
-    constexpr int NW = RT <= 64 ? kTgWavesImg : kTgWavesDirect;
+    constexpr int NW = tsolve_img<RT, F, false>() ? kTgWavesImg : kTgWavesDirect;
     hipLaunchKernelGGL((tsolve_mfma_kernel<RT, F>), dim3(static_cast<unsigned>(ceil_div(mp, 64 * NW)), batch),
                        dim3(64 * NW), 0, st, ta);
     return check_launch("tsolve_mfma");

@@ -149,7 +149,7 @@ void run_rt(int mp, const f32x4* cx, f32x4* cy, long cn, float tcopy, hipStream_
     if (R == 64 && v == 3) hipLaunchKernelGGL(trsm_scalar_kernel, grid, dim3(256), 0, s, dP, dO, dR, mp);
     if ((R == 64 && v == 4) || (R == 128 && v == 1)) {
       TrsmArgs ta{dP, dO, dT, nullptr, nullptr, 0, mp, 0};
-      constexpr int NW = R <= 64 ? kTgWavesImg : kTgWavesDirect;
+      constexpr int NW = tsolve_img<R, false, false>() ? kTgWavesImg : kTgWavesDirect;
       hipLaunchKernelGGL((tsolve_mfma_kernel<R, false>), dim3(static_cast<unsigned>((mp + 64 * NW - 1) / (64 * NW)), B),
                          dim3(64 * NW), 0, s, ta);
     }
