@@ -3047,11 +3047,13 @@ __global__ void __launch_bounds__(RT * tri_inv_tip<RT>()) tri_inv_kernel(const f
 
 constexpr int kTgWavesImg = 2, kTgWavesDirect = 4;
 
-// the LDS row image (IMG) only where the epilogue needs whole rows: the final solve's pass-B
-// split and the fused Gram; the first solve reads and writes HBM directly with 17 KB of LDS per
-// block instead of 50 KB (DION_TSOLVE_DIRECT_FIRST, a dev build option for A/B runs)
+// DION_TSOLVE_DIRECT_FIRST (a dev build option, off): the first solve at r <= 64 without the
+// LDS row image, straight from HBM with 17 KB of LDS per block instead of 50 KB.  Alone and
+// beside a streaming copy it is faster (fc1 group 26.5 vs 38.9 us; marginal 1.9 vs 8.4 us,
+// scripts/ubench/trsm_conc.hip), in the step it is within noise (Llama 470.8 / 470.7 against
+// 471.4 / 472.6 GiB/s, Mixtral 372.9 against 371.7, same box, profiles/r05/t_direct_first.txt)
 #ifndef DION_TSOLVE_DIRECT_FIRST
-#define DION_TSOLVE_DIRECT_FIRST 1
+#define DION_TSOLVE_DIRECT_FIRST 0
 #endif
 template <int RT, bool FINAL, bool GRAM>
 constexpr bool tsolve_img() { return RT <= 64 && (FINAL || GRAM || !DION_TSOLVE_DIRECT_FIRST); }
