@@ -901,6 +901,24 @@ __global__ void __launch_bounds__(256, RB >= 8 ? 1 : 2) colproj_fast_kernel(cons
   }
 }
 
+// sum_k p[k stride] for k = 0 .. n - 1, added in k order (the fixed order the slab reductions
+// promise), with eight loads in flight instead of one dependent load per add: these partial-
+// sum chains (pass B's split-K slabs, the column-norm partials: 64 of them per Llama column)
+// were latency-bound, one L2 round trip per term
+__device__ __forceinline__ float ordered_sum_strided(const float* __restrict__ p, long stride, int n) {
+  float v = 0.f;
+  int k = 0;
+  for (; k + 8 <= n; k += 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = p[(k + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += t[u];
+  }
+  for (; k < n; ++k) v += p[k * stride];
+  return v;
+}
+
 // out[b][e] = sum_k slab[b][k][e] in fixed k order.
 __global__ void __launch_bounds__(256) reduce_slabs_kernel(float* __restrict__ out,
                                                            const float* __restrict__ slab, int nchunk,
@@ -911,9 +929,7 @@ __global__ void __launch_bounds__(256) reduce_slabs_kernel(float* __restrict__ o
     const long b = idx / per_entry;
     const long e = idx - b * per_entry;
     const float* s = slab + b * nchunk * per_entry + e;
-    float v = 0.f;
-    for (int k = 0; k < nchunk; ++k) v += s[k * per_entry];
-    out[idx] = v;
+    out[idx] = ordered_sum_strided(s, per_entry, nchunk);
   }
 }
 
@@ -1365,9 +1381,8 @@ __global__ void __launch_bounds__(256) colnorm_apply_kernel(const FixArgs a) {
   const int tid = threadIdx.x;
   const int r = a.r, nq = a.nq, tpc = a.tpc;
   if (tid < r) {
-    float s = 0.f;
     const float* pp = a.part + static_cast<long>(b) * a.nchunk * r + tid;
-    for (int k = 0; k < a.nchunk; ++k) s += pp[static_cast<long>(k) * r];
+    const float s = ordered_sum_strided(pp, r, a.nchunk);
     denom[tid] = sqrtf(s) + a.eps;
   }
   __syncthreads();
@@ -1414,8 +1429,7 @@ __global__ void __launch_bounds__(256) reduce_fix_partial_kernel(const FixArgs a
   if (p < tpc) {
     for (int row = row0 + p; row < row1; row += tpc) {
       const long idx = static_cast<long>(row) * r + c;
-      float v = 0.f;
-      for (int k = 0; k < nslab; ++k) v += S[k * per_entry + idx];
+      float v = ordered_sum_strided(S + idx, per_entry, nslab);
       const float qv = a.q_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(Q)[idx]) : Q[idx];
       v = zero ? nan_to_num(qv) : nan_to_num(v);
       R[idx] = v;
