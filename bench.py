@@ -332,10 +332,10 @@ def main():
     ap.add_argument("--layers", type=int, default=0, help="layers of the workload (0 = its default); "
                                                           "fewer only for debugging")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=2, help="HIP streams for independent batches (N=1 path)")
+    ap.add_argument("--streams", type=int, default=3, help="HIP streams for independent batches (N=1 path)")
     ap.add_argument("--probe-steps", type=int, default=2, help="single-stream steps timed per kernel for `roofline`")
     ap.add_argument("--coalesce", type=int, default=16, help="matrices per launch group at N = 1")
-    ap.add_argument("--lookahead", type=int, default=0,
+    ap.add_argument("--lookahead", type=int, default=2,
                     help="N = 1 software pipeline depth (groups whose pass A runs before a pass B); 0 = two "
                          "alternating streams")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),

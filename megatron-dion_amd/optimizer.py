@@ -47,8 +47,8 @@ class MegatronDion(Optimizer):
                  elementwise_lr_scale: float = 1.0, scale_mode: str = "spectral",
                  extra_scale_factor: float = 0.2, split_qkv: bool = False, split_linear: bool = False,
                  max_concurrent_tasks: Optional[int] = None, *, codec=None, sketch_seed: int = 0,
-                 coalesce_local: bool = True, local_streams: int = 2, coalesce_max_entries: int = 16,
-                 defer_error_feedback: bool = True, pipeline_lookahead: int = 0):
+                 coalesce_local: bool = True, local_streams: int = 3, coalesce_max_entries: int = 16,
+                 defer_error_feedback: bool = True, pipeline_lookahead: int = 2):
         if isinstance(params, (list, tuple)):
             for pg in params:
                 if isinstance(pg, dict) and "wd_mult" in pg:

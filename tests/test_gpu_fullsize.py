@@ -1,8 +1,9 @@
 """Full-size GPU parity of the bench configurations (`pytest -m gpu`).
 
 The optimizer runs EXACTLY as bench.py runs it -- MegatronDion's defaults (deferred
-error feedback), launch groups of up to 16 matrices (`coalesce_max_entries=16`), two
-alternating HIP streams (`local_streams=2`) -- on the BASELINE configs' real shapes, and
+error feedback; the pipelined schedule: two streaming HIP streams and a latency stream,
+lookahead 2), launch groups of up to 16 matrices (`coalesce_max_entries=16`) -- on the
+BASELINE configs' real shapes, and
 its W, M (after flush_error_feedback) and Q are compared with the CPU oracle
 (oracle/dion_oracle.py, pinned to the reference's golden captures) step by step, with
 explicit sketches (Q up to column signs, tests/_metrics.q_err: a sketch-QR pivot within rounding
@@ -110,7 +111,7 @@ def _run_vs_oracle(label, shapes, r, steps, check=None, generated=False):
             host[name] = p.detach().cpu().clone()
     rf = r / min(min(m, n) for _, m, n in shapes)
     opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01, rank_fraction=rf,
-                           coalesce_max_entries=16, local_streams=2)
+                           coalesce_max_entries=16)
     assert opt._defer_ef, "the bench configuration is the default: deferred error feedback"
     attach_dp_routing(opt, named)
     hyper = O.DionHyper(rank_fraction=rf)

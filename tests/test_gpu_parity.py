@@ -586,7 +586,7 @@ def test_pipelined_two_stream_schedule_is_bit_identical(deferred):
     ref = _run_schedule(shapes, 64, 3, local_streams=1, **kw)
     # (streams, lookahead): 3 and 4 streams put the pipelined schedule's groups on 2 and 3
     # streaming streams (cross-stream hand-offs, per-stream workspaces)
-    for ns, la in ((2, 2), (2, 0), (3, 1), (4, 1), (3, 0), (4, 0)):
+    for ns, la in ((3, 2), (2, 2), (2, 0), (3, 1), (4, 1), (3, 0), (4, 0)):
         got = _run_schedule(shapes, 64, 3, local_streams=ns, pipeline_lookahead=la, **kw)
         for i, (a, b) in enumerate(zip(got, ref)):
             for k in range(3):
