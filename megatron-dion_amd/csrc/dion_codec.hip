@@ -4,9 +4,11 @@
 // /root/reference/megatron/core/optimizer/):
 //   rowproj_kernel / colproj_kernel  dion/runtime.py:1560-1616 (M += G, P = M Q),
 //                                     dion/runtime.py:1476-1477 (R = M^T P)
-//   sketch/gram colproj (panel mode), householder_qr_kernel,
-//   trsm_kernel                       dion/ortho.py:71-123 (randomised Cholesky QR)
-//   fixup_colnorm_kernel, pfix_kernel dion/kernels.py:157-210, 279-290
+//   sketch_rad_kernel, sketch_qr_inv_kernel, gram_h3_kernel, chol_reg_kernel,
+//   tsolve_mfma_kernel (explicit-inverse solves; trsm_* substitution kernels for other r)
+//                                     dion/ortho.py:71-123 (randomised Cholesky QR)
+//   fixup_partial / colnorm_apply / reduce_fix_partial, pfix_kernel
+//                                     dion/kernels.py:157-210, 279-290
 //   ef_update_kernel                  dion/kernels.py:54-154, 229-276;
 //                                     dion/runtime.py:1105-1113
 //
