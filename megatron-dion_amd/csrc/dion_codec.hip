@@ -4817,6 +4817,10 @@ bool colproj_fast_ok(int rows, int cols, int r) { return cols % 256 == 0 && rows
 // rank_stream_kernel: rows (or columns) one block streams, waves per block, X tiles in flight
 // (measured fastest of (NW, D) in {4, 8} x {2, 3} on the Llama set, round 2)
 constexpr int kRankStreamLen = DION_RSL;
+// r > 64: rows per update block (DION_RSL128, a dev build option; measured in round 5 call AC)
+#ifndef DION_RSL128
+#define DION_RSL128 512
+#endif
 constexpr int kRankNW = 8;
 constexpr int kRankD = 2;
 // r = 128 (RU 8): one X tile in flight -- 135 VGPRs, 3 waves per SIMD, against D 2's 202 at 2.
@@ -6361,7 +6365,7 @@ int dion_ef_apply(const DionBatchDesc* d, float* const* M, float* const* W, cons
     if (M == nullptr && !split_ok)
       return fail(DION_E_UNSUPPORTED, "weight-only update needs the rank-update kernel (%dx%d r=%d)", d->m, d->n, r);
     if (split_ok) {
-      const int s_len = kRankStreamLen;
+      const int s_len = r > 64 ? DION_RSL128 : kRankStreamLen;
       for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1 && W == nullptr) break;
         if (pass == 0 && M == nullptr) continue;
