@@ -4817,7 +4817,8 @@ bool colproj_fast_ok(int rows, int cols, int r) { return cols % 256 == 0 && rows
 // rank_stream_kernel: rows (or columns) one block streams, waves per block, X tiles in flight
 // (measured fastest of (NW, D) in {4, 8} x {2, 3} on the Llama set, round 2)
 constexpr int kRankStreamLen = DION_RSL;
-// r > 64: rows per update block (DION_RSL128, a dev build option; measured in round 5 call AC)
+// r > 64: rows per update block (DION_RSL128, a dev build option): Mixtral 376.0-376.5 -> 381.0-382.0
+// GiB/s against 256 (profiles/r05/ac_rsl128.txt)
 #ifndef DION_RSL128
 #define DION_RSL128 512
 #endif
