@@ -43,7 +43,7 @@ extern "C" {
 
 typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 
-#define DION_ABI_VERSION 15
+#define DION_ABI_VERSION 16
 
 #define DION_OK 0
 #define DION_E_INVALID (-1)     /* bad descriptor / null pointer / misuse       */
@@ -65,8 +65,9 @@ typedef struct ihipStream_t* dion_stream_t; /* == hipStream_t */
 #define DION_OP_GRAD_SUM_SQ 7  /* dion_grad_sum_sq (only batch, m, n, g_dtype, ld_g used) */
 #define DION_OP_DORTHO 8       /* dion_dortho_sketch / dion_dortho_gram (row-sharded P)   */
 #define DION_OP_PSPLIT 9       /* not scratch: bytes of the p_split buffer of
-                                  dion_orthonormalize_fused / dion_project_r_split;
-                                  DION_E_UNSUPPORTED: no fused split for this shape        */
+                                  dion_orthonormalize_fused / dion_pfix_split /
+                                  dion_project_r_split; DION_E_UNSUPPORTED: no fused split
+                                  for this shape                                           */
 
 typedef struct DionBatchDesc {
   int32_t batch;      /* matrices in this call (all the same shape)            */
@@ -197,15 +198,16 @@ int dion_project_r(const DionBatchDesc* desc, const float* const* M, const float
 
 /*
  * The W = 1 path with fewer passes over P (same results as dion_orthonormalize,
- * dion_project_r and dion_fixup_colnorm in that order, for every input those reach:
- * an orthonormalised P is NaN only in whole columns, and a whole NaN column gives
- * R = 0 in that column either way).
+ * dion_project_r and dion_fixup_colnorm in that order for every finite orthonormalised P:
+ * such a P is NaN only in whole columns, and a whole NaN column gives R = 0 in that column
+ * either way; see dion_pfix_split for a P the Cholesky QR made infinite).
  * dion_orthonormalize_fused: dion_orthonormalize, then
  *   `nonzero` (optional): the fix-up of P, P_b <- z ? 0 : nan_to_num(P_b) (in the last
  *     solve's epilogue where it can; dion_fixup_colnorm is then called with P = NULL);
  *   `p_split` (optional, DION_OP_PSPLIT bytes, 16-byte aligned): the fp16x3 limbs of the
  *     final P in pass B's operand layout on the fixed scale 2^14 (|P| <= 1: orthonormal
- *     columns), written by the last solve; DION_E_UNSUPPORTED (nothing enqueued) when
+ *     columns), written by the last solve (r = 32 / 64; at r = 128 by one split launch after
+ *     it); DION_E_UNSUPPORTED (nothing enqueued) when
  *     DION_OP_PSPLIT is unsupported for this desc.
  * dion_project_r_split: dion_project_r reading P's limbs from `p_split` (NULL: as
  *   dion_project_r); a pass B whose h3 kernel does not run for these pointers ignores it.
@@ -218,6 +220,25 @@ int dion_orthonormalize_fused(const DionBatchDesc* desc, float* P, const float* 
 int dion_project_r_split(const DionBatchDesc* desc, const float* const* M, const float* P,
                          const void* p_split, float* R, const uint32_t* m_absmax, void* ws,
                          size_t ws_bytes, dion_stream_t stream);
+/*
+ * dion_pfix_split (ABI 16): the P half of the fix-up and pass B's split of P for a P that was
+ * orthonormalised elsewhere -- the W > 1 replicated path, where the owner rank orthonormalises
+ * an entry, every rank receives it by all-gather and the zero test is each rank's own
+ * momentum (kernels.py:181-188 on the local M_batch; runtime.py:1379-1496):
+ *   `nonzero` (optional): P_b <- nonzero[b] == 0 ? 0 : nan_to_num(P_b), in place;
+ *   `p_split` (optional, DION_OP_PSPLIT bytes, 16-byte aligned): the fp16x3 limbs of the
+ *     (fixed) P in pass B's operand layout on the fixed scale 2^14, as dion_orthonormalize_fused
+ *     writes them, for dion_project_r_split; DION_E_UNSUPPORTED (nothing enqueued) when
+ *     DION_OP_PSPLIT is unsupported for this desc.
+ * fp32 state only.  P must be orthonormal or zero per column (|x| < 2) for the split to hold:
+ * an orthonormalised P that is infinite somewhere (a degenerate, e.g. row-sparse, P whose
+ * Cholesky QR overflows) gives an inf hi limb and a NaN lo limb, so that column of R is fixed
+ * to 0, where the unfused dion_project_r rescales; the reference's step is not finite there
+ * either (nan_to_num turns the infinity into FLT_MAX before the update).  The same holds for
+ * the split of dion_orthonormalize_fused.
+ */
+int dion_pfix_split(const DionBatchDesc* desc, float* P, const uint32_t* nonzero, void* p_split,
+                    dion_stream_t stream);
 /*
  * dion_project_r_fixup: dion_project_r_split, then dion_fixup_colnorm with P = NULL (the P
  * half done by dion_orthonormalize_fused), bitwise; the fix-up's first phase rides on pass

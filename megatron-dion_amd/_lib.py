@@ -57,7 +57,7 @@ def source_build_id(roots=SOURCES) -> str | None:
             h.update(fh.read())
         h.update(b"\0")
     return h.hexdigest()[:16]
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 DION_OK = 0
 DION_E_INVALID = -1
@@ -97,6 +97,7 @@ EXPORTED = (
     "dion_project_r",
     "dion_project_r_split",
     "dion_project_r_fixup",
+    "dion_pfix_split",
     "dion_fixup_colnorm",
     "dion_fixup_colsum",
     "dion_colnorm_apply",
@@ -159,6 +160,7 @@ _SIGNATURES = {
     "dion_project_r_split": ([_DESC, _PP, _P, _P, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_project_r_fixup": ([_DESC, _PP, _P, _P, _P, _P, _PP, _P, ctypes.c_float, _P, ctypes.c_size_t, _P],
                              ctypes.c_int),
+    "dion_pfix_split": ([_DESC, _P, _P, _P, _P], ctypes.c_int),
     "dion_fixup_colnorm": ([_DESC, _P, _P, _PP, _P, ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_fixup_colsum": ([_DESC, _P, _P, _PP, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "dion_colnorm_apply": ([_DESC, _P, _PP, _P, ctypes.c_float, _P], ctypes.c_int),

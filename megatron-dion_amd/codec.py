@@ -221,6 +221,21 @@ class HipDionCodec:
             return None
         return torch.empty((int(B), int(ok)), dtype=torch.uint8, device=self.device)
 
+    def pfix_split(self, P: torch.Tensor, m: int, n: int, transposed: bool, nonzero: Optional[torch.Tensor],
+                   p_split: Optional[torch.Tensor]) -> None:
+        """The fix-up's P half with this rank's zero test and pass B's fixed-scale split of P (the
+        W > 1 path after the all-gather of the owners' orthonormalised P).  kernels.py:181-188."""
+        B, _, r = P.shape
+        if B == 0:
+            return
+        if not P.is_contiguous() or P.dtype != torch.float32:
+            raise RuntimeError("[DION_BAD_FACTOR] pfix_split needs a contiguous fp32 (batch, rows, r) P")
+        d = self._desc(B, m, n, r, transposed)
+        _lib.check(self.lib.dion_pfix_split(ctypes.byref(d), P.data_ptr(),
+                                            None if nonzero is None else nonzero.data_ptr(),
+                                            None if p_split is None else p_split.data_ptr(), self._stream()),
+                   "dion_pfix_split")
+
     # ------------------------------------------------------------ distributed RCQR
     # the per-rank pieces of dion/ortho.py:682-834 (P row-sharded over the TP group); the
     # caller runs the collectives between them (runtime.distributed_orthonormalize)

@@ -3381,19 +3381,24 @@ __global__ void __launch_bounds__(256) absmax_kernel(const AbsMaxArgs a) {
 struct Presplit16Args {
   const float* src[MAXB];
   f16x8* dst;
-  const uint32_t* amax;  // (batch,) max |x| bits
-  float* inv_scale;      // (batch,) 1 / s, written by the blocks of x = 0
+  const uint32_t* amax;  // (batch,) max |x| bits; null: the fixed scale 2^14 of an orthonormal P
+  float* inv_scale;      // (batch,) 1 / s, written by the blocks of x = 0 (with amax only)
   long stride;           // f16x8 units per matrix
   int rows, r, kmap, layout;
+  const uint32_t* fix;   // layout 0 only (dion_pfix_split): P_b <- fix[b] == 0 ? 0 : nan_to_num(P_b)
+                         // in place before the split (null: src is only read)
 };
 
 __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a) {
   const int b = blockIdx.y;
   const float* __restrict__ src = a.src[b];
   if (src == nullptr) return;
-  float inv;
-  const float s = h3_scale(__uint_as_float(a.amax[b]), inv);
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.inv_scale[b] = inv;
+  float s = kPSplitScale;
+  if (a.amax != nullptr) {
+    float inv;
+    s = h3_scale(__uint_as_float(a.amax[b]), inv);
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.inv_scale[b] = inv;
+  }
   const long items = static_cast<long>(a.rows) * a.r / 8;
   const long item = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
   if (item >= items) return;
@@ -3409,6 +3414,18 @@ __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a)
     for (int e = 0; e < 8; ++e) {
       const int k = a.kmap == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
       v[e] = src[(blk * 32 + k) * a.r + 16 * cb + t];
+    }
+    if (a.fix != nullptr) {
+      // the fix-up's P half (kernels.py:185-188) with this rank's zero test: every element of
+      // P is one (unit, lane, e) of the layout, so each is rewritten exactly once
+      const bool zero = a.fix[b] == 0u;
+      float* __restrict__ dst = const_cast<float*>(src);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = a.kmap == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
+        v[e] = zero ? 0.f : nan_to_num(v[e]);
+        dst[(blk * 32 + k) * a.r + 16 * cb + t] = v[e];
+      }
     }
   } else {
     const int KK = a.r / 32;
@@ -5024,13 +5041,36 @@ int launch_pfix(float* P, const uint32_t* nonzero, long per_entry, int batch, hi
 // or 64, m_P > r (the Cholesky QR path), m_P a multiple of 32, and run_projection's h3 shape
 // conditions for the orientation (the layout / ld / alignment conditions are checked per call:
 // a pass B that cannot use the split ignores it).
+// r = 128 (round 6): the final solve has no LDS row image there, so the split is one
+// fixed-scale presplit16_kernel launch after it (launch_psplit_fixed), which still spares pass
+// B its absmax and measured-scale split.
 bool psplit_ok(const DionBatchDesc* d) {
-  if (d->m_dtype != DION_DTYPE_F32 || !(d->r == 32 || d->r == 64)) return false;
+  if (d->m_dtype != DION_DTYPE_F32 || !(d->r == 32 || d->r == 64 || d->r == 128)) return false;
   const bool tr = d->transposed != 0;
   const int mp = tr ? d->n : d->m;
   if (mp <= d->r || mp % 32 != 0) return false;
   if (tr) return kPbH3r && rowproj_fast_ok(d->m, d->n, d->r) && d->m % (16 * kRBE * kPbRNW) == 0;
   return colproj_fast_ok(d->m, d->n, d->r) && colh3_ok(d->m, d->n, d->r);
+}
+
+// pass B's fp16x3 split of nb orthonormal P_b (m_P x r, contiguous from P) on the fixed scale
+// 2^14 into `out` (layout 0, pass B's kmap), with the fix-up of P in place first when `fix` is
+// given (presplit16_kernel with amax = null)
+int launch_psplit_fixed(float* P, int mp, int r, int nb, const uint32_t* fix, f16x8* out, int kmap,
+                        hipStream_t st) {
+  Presplit16Args pa;
+  memset(&pa, 0, sizeof(pa));
+  for (int b = 0; b < nb; ++b) pa.src[b] = P + static_cast<long>(b) * mp * r;
+  pa.dst = out;
+  pa.stride = static_cast<long>(mp) * r / 4;
+  pa.rows = mp;
+  pa.r = r;
+  pa.kmap = kmap;
+  pa.layout = 0;
+  pa.fix = fix;
+  const dim3 pgrid(static_cast<unsigned>(ceil_div(static_cast<long>(mp) * r / 8, 256)), nb);
+  hipLaunchKernelGGL(presplit16_kernel, pgrid, dim3(256), 0, st, pa);
+  return check_launch("presplit16(fixed)");
 }
 
 // the fix-up partials of dion_project_r_fixup at the end of the pass-B workspace
@@ -5961,6 +6001,28 @@ int dion_project_r_fixup(const DionBatchDesc* d, const float* const* M, const fl
   return DION_OK;
 }
 
+int dion_pfix_split(const DionBatchDesc* d, float* P, const uint32_t* nonzero, void* p_split, dion_stream_t stream) {
+  int rc = validate(d);
+  if (rc != DION_OK) return rc;
+  if (P == nullptr || (nonzero == nullptr && p_split == nullptr)) return fail(DION_E_INVALID, "null argument");
+  if (d->m_dtype != DION_DTYPE_F32) return fail(DION_E_UNSUPPORTED, "dion_pfix_split: fp32 state only");
+  if (p_split != nullptr && (!psplit_ok(d) || !aligned16(P) || !aligned16(p_split)))
+    return fail(DION_E_UNSUPPORTED, "no fused pass-B split for %dx%d r=%d", d->m, d->n, d->r);
+  if (d->batch == 0) return DION_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int mp = d->transposed ? d->n : d->m;
+  const int r = d->r;
+  if (p_split == nullptr) return launch_pfix(P, nonzero, static_cast<long>(mp) * r, d->batch, st);
+  for (int b0 = 0; b0 < d->batch; b0 += MAXB) {
+    const int nb = d->batch - b0 < MAXB ? d->batch - b0 : MAXB;
+    rc = launch_psplit_fixed(P + static_cast<long>(b0) * mp * r, mp, r, nb, nonzero != nullptr ? nonzero + b0 : nullptr,
+                             static_cast<f16x8*>(p_split) + static_cast<long>(b0) * mp * r / 4, d->transposed ? 1 : 0,
+                             st);
+    if (rc != DION_OK) return rc;
+  }
+  return DION_OK;
+}
+
 int dion_orthonormalize(const DionBatchDesc* d, float* P, const float* sketch, uint64_t seed, float oversample,
                         void* ws, size_t ws_bytes, dion_stream_t stream) {
   return dion_orthonormalize_fused(d, P, sketch, seed, oversample, nullptr, nullptr, ws, ws_bytes, stream);
@@ -6070,7 +6132,7 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
       rc = launch_tsolve(p1, Pb, r1, mp, r, nb, st, true, fuse_fix ? nonzero + b0 : nullptr,
                          p_split != nullptr ? static_cast<f16x8*>(p_split) + static_cast<long>(b0) * mp * r / 4 : nullptr,
                          static_cast<long>(mp) * r / 4, d->transposed ? 1 : 0);
-    } else if (lds_fix || p_split != nullptr) {
+    } else if (lds_fix || (p_split != nullptr && r <= 64)) {
       TrsmArgs ta{p1, Pb, fac, fuse_fix ? nonzero + b0 : nullptr,
                   p_split != nullptr ? static_cast<f16x8*>(p_split) + static_cast<long>(b0) * mp * r / 4 : nullptr,
                   static_cast<long>(mp) * r / 4, mp, d->transposed ? 1 : 0};
@@ -6083,6 +6145,10 @@ int dion_orthonormalize_fused(const DionBatchDesc* d, float* P, const float* ske
     } else {
       rc = launch_trsm(p1, Pb, fac, mp, r, nb, st, fuse_fix ? nonzero + b0 : nullptr);
     }
+    if (rc != DION_OK) return rc;
+    if (p_split != nullptr && r == 128)  // no row image in the r = 128 solve: split after it
+      rc = launch_psplit_fixed(Pb, mp, r, nb, nullptr, static_cast<f16x8*>(p_split) + static_cast<long>(b0) * mp * r / 4,
+                               d->transposed ? 1 : 0, st);
     if (rc != DION_OK) return rc;
   }
   // ortho.py:123: the fp32 result is cast back to P's dtype

@@ -418,7 +418,8 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         yield
         work.wait()
         R = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
-        codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero)
+        p_fixed, r_fixed = _replicated_pass_b(optimizer, codec, momentums, Qs, P, R, nonzero, real, m, n, transposed,
+                                              bf16_state, use_low_rank)
         if use_low_rank:
             work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
             yield
@@ -453,7 +454,8 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
             work.wait()
         P = P[:B]
         R = torch.zeros((B, nq, r), dtype=torch.float32, device=dev)
-        codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero)
+        p_fixed, r_fixed = _replicated_pass_b(optimizer, codec, momentums, Qs, P, R, nonzero, real, m, n, transposed,
+                                              bf16_state, use_low_rank)
         if use_low_rank:
             work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
             yield
@@ -498,7 +500,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     clock.mark("ortho_r")
     eps = float(optimizer.defaults["epsilon"])
     if not r_fixed:
-        codec.fixup_colnorm(None if (W == 1 and p_fixed) else P, R, list(Qs[:real]), nonzero, eps, m, n, transposed)
+        codec.fixup_colnorm(None if p_fixed else P, R, list(Qs[:real]), nonzero, eps, m, n, transposed)
     clock.mark("q_normalize")
 
     grp = optim_groups[0] or {}
@@ -963,6 +965,33 @@ def _record_pending(state, P_b, R_b, alpha, transposed: bool) -> None:
     M = dict.get(state, "momentum")
     dict.__setitem__(state, _PENDING_EF, (P_b, R_b, alpha, weakref.ref(M) if M is not None else None,
                                           bool(transposed)))
+
+
+def _replicated_pass_b(optimizer, codec, momentums, Qs, P, R, nonzero, real, m, n, transposed, bf16_state,
+                       use_low_rank):
+    """Pass B of a W > 1 ddp batch once every rank holds the gathered, orthonormalised P.
+
+    fp32 state (round 6): the W = 1 tail's savings where the exchange allows them.  The owner
+    rank orthonormalised each entry, but the fix-up's zero test is this rank's own momentum
+    (kernels.py:181-188 on the local M_batch), so the P half of the fix-up runs here, after
+    the all-gather, in one launch with pass B's fixed-scale split of P (dion_pfix_split): pass B
+    then needs no absmax / split of P and the fix-up no pass over P.  With low-rank sync R is
+    averaged before the fix-up (runtime.py:1478-1496), so the R half stays a separate call;
+    without it (the dense branch) it rides on pass B as at W = 1 (project_r_fixup).
+    Returns (p_fixed, r_fixed)."""
+    moms = list(momentums[:real])
+    if bf16_state or not hasattr(codec, "pfix_split"):
+        codec.project_r(moms, P, R, transposed, nonzero=nonzero)
+        return False, False
+    split = codec.psplit_buffer(real, m, n, int(R.shape[2]), transposed) if hasattr(codec, "psplit_buffer") else None
+    codec.pfix_split(P[:real], m, n, transposed, nonzero[:real], split)
+    kw = {} if split is None else {"p_split": split}
+    if not use_low_rank and getattr(codec, "fuses_r_fixup", False):
+        codec.project_r_fixup(moms, P, R, list(Qs[:real]), nonzero, float(optimizer.defaults["epsilon"]), transposed,
+                              **kw)
+        return True, True
+    codec.project_r(moms, P, R, transposed, nonzero=nonzero, **kw)
+    return True, False
 
 
 def _fused_kw(fix, split, i0, i1) -> dict:

@@ -52,6 +52,13 @@ class OracleCodec:
             if fix_nonzero is not None:           # the fused fix-up (kernels.py:185-188)
                 P[b] = torch.zeros_like(P[b]) if int(fix_nonzero[b]) == 0 else P[b].nan_to_num()
 
+    def pfix_split(self, P, m, n, transposed, nonzero, p_split):
+        # the fix-up's P half with this rank's zero test (kernels.py:185-188); no split on CPU
+        if nonzero is not None:
+            B = P.shape[0]
+            zero = (nonzero[:B] == 0).view(B, 1, 1)
+            P.copy_(torch.where(zero, torch.zeros_like(P), P.nan_to_num()))
+
     # distributed RCQR pieces (dion/ortho.py:682-834): the reference's arithmetic, with the
     # triangular solves as products with the explicit inverses the codec interface passes on
     def dortho_sketch(self, P, m, n, transposed, seed, row_offset, oversample, SP, sketch=None):

@@ -194,6 +194,29 @@ def test_config4_schedule_w4_w8_hip_matches_oracle(world):
     assert sorted(chunks) == sorted([k, k, k, k, 0]), chunks
 
 
+def _mixtral_scaled():
+    """Config 5's expert shapes / 16 (fc1 1792 x 256, fc2 256 x 896 transposed; r = 128 =
+    rank_fraction 0.5 of the short side), 16 matrices per shape (one rank-major group of 16 / W
+    full batches) and 3 more fc1 (a padded batch after its group)."""
+    out = []
+    for name, m, n, extra in (("linear_fc1", 1792, 256, 3), ("linear_fc2", 256, 896, 0)):
+        out += [(f"experts.{i}.{name}.weight", m, n) for i in range(16 + extra)]
+    return out
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_config5_schedule_r128_w4_w8_hip_matches_oracle(world):
+    """Config 5's replicated schedule at r = 128 (the Mixtral experts at DP = W, what one GPU can
+    run of it): gloo ranks on cuda:0, rank-major groups with the r = 128 kernels (LDS-DMA pass A,
+    the fixed-scale pass-B split after the all-gather), deferred EF; HIP codec against the oracle
+    codec, W / M / Q / dW <= the bars, W and Q bit-identical on all ranks."""
+    shapes = _mixtral_scaled()
+    worst, chunks = _run_and_check(shapes, 128, 2, low_rank=True, world=world,
+                                   opt_kw=dict(coalesce_max_entries=16))
+    k = 16 // world
+    assert sorted(chunks) == sorted([k, k, 0]), chunks
+
+
 def test_w2_llama_fc1_fc2_rank_major_hip_matches_oracle():
     # the first and the last matrix of each shape: the two ends of a rank-major group
     _run_and_check(LLAMA_FC, 64, 2, low_rank=True, check=[LLAMA_FC[0][0], LLAMA_FC[3][0], LLAMA_FC[4][0],

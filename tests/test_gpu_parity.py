@@ -708,7 +708,10 @@ def test_orthonormalize_h3_gram_matches_oracle(mp, r, decades):
         worst_i = max(worst_i, (G - torch.eye(r, dtype=torch.float64)).abs().max().item())
     print(f"mp={mp} r={r} decades={decades}: P maxrel vs oracle {worst_p:.3e}, |P^T P - I| {worst_i:.3e}")
     assert worst_i <= 2e-6, worst_i
-    assert worst_p <= 1e-5 * 10 ** decades, worst_p
+    # bars near the measured worst case (rounds 5-6: 9.4e-7 - 2.0e-6 at 0-1 decades, 2.8e-5 -
+    # 4.8e-5 at 3 decades, the problem's own conditioning), so a real loss of precision in the
+    # fp16x3 Gram or the explicit-inverse solves fails (was 1e-5 * 10**decades)
+    assert worst_p <= (5e-6 if decades <= 1 else 1.5e-4), worst_p
 
 
 # ---------------------------------------------------------------------------------------------- pass B + fix-up
