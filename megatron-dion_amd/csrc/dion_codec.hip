@@ -3324,8 +3324,17 @@ tsolve_mfma_kernel(const TrsmArgs a) {
   }
 }
 
-// per-matrix max |x| of a small factor (rows x r fp32), as the float's bit pattern
-// (non-negative floats order like their bits; a NaN sorts above inf)
+// per-matrix max |x| of a small factor (rows x r fp32) over its FINITE values, as the float's
+// bit pattern (non-negative floats order like their bits).  A non-finite value counts as 0: it
+// turns its own products non-finite whatever the scale, and left in the max (a NaN's bits sort
+// above inf's) it would push the scale to 2^-114 and flush every finite product of the matrix
+// to zero -- a P with one NaN column (a failed Cholesky pivot) then lost all of its R instead of
+// that column (round 6, tests/test_gpu_fused_tail.py).
+__device__ __forceinline__ uint32_t finite_abs_bits(float x) {
+  const uint32_t b = __float_as_uint(x) & 0x7FFFFFFFu;
+  return b < 0x7F800000u ? b : 0u;
+}
+
 struct AbsMaxArgs {
   const float* src[3 * MAXB];  // group-major: matrix b of group k at k * nb + b (null: skipped)
   uint32_t* out;               // (groups * nb,) zero-initialised, same order
@@ -3354,15 +3363,15 @@ __global__ void __launch_bounds__(256) absmax_kernel(const AbsMaxArgs a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) m = max(m, __float_as_uint(v[u][q]) & 0x7FFFFFFFu);
+          for (int q = 0; q < 4; ++q) m = max(m, finite_abs_bits(v[u][q]));
       }
       for (; i < n4; i += stride) {
         const f32x4 v = s4[i];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) m = max(m, __float_as_uint(v[q]) & 0x7FFFFFFFu);
+        for (int q = 0; q < 4; ++q) m = max(m, finite_abs_bits(v[q]));
       }
     } else {
-      for (; i < count; i += stride) m = max(m, __float_as_uint(src[i]) & 0x7FFFFFFFu);
+      for (; i < count; i += stride) m = max(m, finite_abs_bits(src[i]));
     }
   }
 #pragma unroll

@@ -280,6 +280,33 @@ def reduces_p_over_fs(config) -> bool:
     return (not tr and dim == 1) or (tr and dim == 0)
 
 
+def reduce_in_state_dtype(kind, out, op, group, bf16_state, inp=None, idx=None):
+    """A reduction of a P / R buffer over `group`, yielding while it is in flight.
+
+    With bf16 state the fp32 buffer holds bf16 values and the collective runs on a bf16 copy of
+    it: the reference reduces its bf16 tensors themselves (runtime.py:1428-1434, 1485-1491,
+    1729-1795), so the backend rounds after every hop, in its own order, and the same backend
+    gives the reference's bits (tests/golden f6 / f7: gloo's ring order at FS = 4; the
+    correctly rounded fp32 sum differs from it by an ulp of the partial sums).  It also halves
+    the bytes on the wire.  kind: "rs" reduce_scatter_tensor(out, inp), "ar" all_reduce(out),
+    "arc" all_reduce_coalesced of out[i] for i in idx (in place)."""
+    if bf16_state:
+        src = (inp if kind == "rs" else out).to(torch.bfloat16)
+        dst = torch.empty(out.shape, dtype=torch.bfloat16, device=out.device) if kind == "rs" else src
+    else:
+        src, dst = (inp if kind == "rs" else out), out
+    if kind == "rs":
+        work = dist.reduce_scatter_tensor(dst, src, op=op, group=group, async_op=True)
+    elif kind == "ar":
+        work = dist.all_reduce(dst, op=op, group=group, async_op=True)
+    else:
+        work = dist.all_reduce_coalesced([dst[i] for i in idx], op=op, group=group, async_op=True)
+    yield
+    work.wait()
+    if bf16_state:
+        out.copy_(dst)
+
+
 def split_range(size: int, world: int, rank: int):
     """dion/ortho.py:247-259: contiguous shard [start, end) of `rank`, remainder on the first ranks."""
     base, rem = size // world, size % world
@@ -364,7 +391,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     Qs, commit_qs = _qs_in_state_dtype(list(Qs), real, momentums[0].dtype)
     # bf16 momentum and Q (the speedrun's DionMixedPrecisionConfig): P and R stay fp32
     # buffers of bf16 values; the kernels round where the reference's bf16 tensors round,
-    # and an averaging collective is followed by the same rounding (round_bf16)
+    # and an averaging collective runs on bf16 copies (reduce_in_state_dtype)
     sdt = momentums[0].dtype
     bf16_state = sdt == torch.bfloat16
 
@@ -396,11 +423,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         mine = P[rank * kch:(rank + 1) * kch]
         P_own = torch.empty((kch, mp, r), dtype=torch.float32, device=dev)
         if use_low_rank:
-            work = dist.reduce_scatter_tensor(P_own, P, op=dist.ReduceOp.AVG, group=group, async_op=True)
-            yield
-            work.wait()
-            if bf16_state:
-                codec.round_bf16(P_own)
+            yield from reduce_in_state_dtype("rs", P_own, dist.ReduceOp.AVG, group, bf16_state, inp=P)
         else:
             P_own.copy_(mine)
         clock.mark("p_reduce")
@@ -421,11 +444,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         p_fixed, r_fixed = _replicated_pass_b(optimizer, codec, momentums, Qs, P, R, nonzero, real, m, n, transposed,
                                               bf16_state, use_low_rank)
         if use_low_rank:
-            work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
-            yield
-            work.wait()
-            if bf16_state:
-                codec.round_bf16(R)
+            yield from reduce_in_state_dtype("ar", R, dist.ReduceOp.AVG, group, bf16_state)
     elif W > 1:
         rank = dist.get_rank(group)
         padded = (B + W - 1) // W * W
@@ -436,12 +455,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
             P_single = torch.empty((1, mp, r), dtype=torch.float32, device=dev)
             if use_low_rank:
                 # runtime.py:1428-1434: reduce-scatter(avg) hands entry start+rank to this rank
-                work = dist.reduce_scatter_tensor(P_single, chunk, op=dist.ReduceOp.AVG, group=group,
-                                                  async_op=True)
-                yield
-                work.wait()
-                if bf16_state:
-                    codec.round_bf16(P_single)
+                yield from reduce_in_state_dtype("rs", P_single, dist.ReduceOp.AVG, group, bf16_state, inp=chunk)
             else:
                 P_single.copy_(chunk[rank:rank + 1])
             idx = start + rank
@@ -457,11 +471,7 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
         p_fixed, r_fixed = _replicated_pass_b(optimizer, codec, momentums, Qs, P, R, nonzero, real, m, n, transposed,
                                               bf16_state, use_low_rank)
         if use_low_rank:
-            work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
-            yield
-            work.wait()
-            if bf16_state:
-                codec.round_bf16(R)
+            yield from reduce_in_state_dtype("ar", R, dist.ReduceOp.AVG, group, bf16_state)
     else:
         # W = 1, fp32 state: the last solve of the orthonormalisation also fixes P (the fix-up's
         # P half, kernels.py:185-188: an orthonormalised P is NaN only in whole columns, whose R
@@ -588,17 +598,9 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     clock.mark("p_matmul")
     # reduce-scatter(sum): this rank receives entry fs_rank summed over the FS shards
     P_own = torch.empty((1, mp, r), dtype=torch.float32, device=dev)
-    work = dist.reduce_scatter_tensor(P_own, P, op=dist.ReduceOp.SUM, group=fs_group, async_op=True)
-    yield
-    work.wait()
-    if bf16_state:
-        codec.round_bf16(P_own)
-    if use_low_rank and rworld > 1:
-        work = dist.all_reduce(P_own, op=dist.ReduceOp.AVG, group=rgroup, async_op=True)  # runtime.py:367-369
-        yield
-        work.wait()
-        if bf16_state:
-            codec.round_bf16(P_own)
+    yield from reduce_in_state_dtype("rs", P_own, dist.ReduceOp.SUM, fs_group, bf16_state, inp=P)
+    if use_low_rank and rworld > 1:  # runtime.py:367-369
+        yield from reduce_in_state_dtype("ar", P_own, dist.ReduceOp.AVG, rgroup, bf16_state)
     clock.mark("p_reduce")
     own = indices[fs_rank]
     if own >= real or dist_metas[own] is None:
@@ -620,11 +622,7 @@ def _fs_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     R = torch.zeros((B, nq, r), dtype=torch.float32, device=dev)
     codec.project_r(list(momentums[:real]), P, R, transposed, nonzero=nonzero)
     if use_low_rank and rworld > 1:
-        work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=rgroup, async_op=True)
-        yield
-        work.wait()
-        if bf16_state:
-            codec.round_bf16(R)
+        yield from reduce_in_state_dtype("ar", R, dist.ReduceOp.AVG, rgroup, bf16_state)
     clock.mark("ortho_r")
     colsum = torch.empty((real, r), dtype=torch.float32, device=dev)
     codec.fixup_colsum(P, R, list(Qs[:real]), nonzero, colsum, m, n, transposed)
@@ -711,20 +709,10 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     for coll in tuple(getattr(batch_collectives, "fs_p_collectives", None) or ()):
         if coll.process_group is not None and int(coll.world_size) > 1:
             idx = [int(i) for i in coll.indices]
-            work = (dist.all_reduce(P, op=dist.ReduceOp.SUM, group=coll.process_group, async_op=True)
-                    if idx == list(range(B)) else
-                    dist.all_reduce_coalesced([P[i] for i in idx], op=dist.ReduceOp.SUM, group=coll.process_group,
-                                              async_op=True))
-            yield
-            work.wait()
-            if bf16_state:
-                codec.round_bf16(P)
+            yield from reduce_in_state_dtype("ar" if idx == list(range(B)) else "arc", P, dist.ReduceOp.SUM,
+                                             coll.process_group, bf16_state, idx=idx)
     if use_low_rank and W > 1:
-        work = dist.all_reduce(P, op=dist.ReduceOp.AVG, group=group, async_op=True)
-        yield
-        work.wait()
-        if bf16_state:
-            codec.round_bf16(P)
+        yield from reduce_in_state_dtype("ar", P, dist.ReduceOp.AVG, group, bf16_state)
     clock.mark("p_reduce")
     yield from distributed_orthonormalize(optimizer, P, real, m, n, transposed, batch_group.ortho_group, dist_metas,
                                           batch_cache_key, sketches)
@@ -735,17 +723,9 @@ def _tp_batch_update(optimizer, params, momentums, Qs, configs, dist_metas, opti
     if real < B:
         R[real:].zero_()
     rsum = batch_collectives.tp_r_collectives[0]
-    work = dist.all_reduce(R, op=dist.ReduceOp.SUM, group=rsum.process_group, async_op=True)
-    yield
-    work.wait()
-    if bf16_state:
-        codec.round_bf16(R)
+    yield from reduce_in_state_dtype("ar", R, dist.ReduceOp.SUM, rsum.process_group, bf16_state)
     if use_low_rank and W > 1:
-        work = dist.all_reduce(R, op=dist.ReduceOp.AVG, group=group, async_op=True)
-        yield
-        work.wait()
-        if bf16_state:
-            codec.round_bf16(R)
+        yield from reduce_in_state_dtype("ar", R, dist.ReduceOp.AVG, group, bf16_state)
     clock.mark("ortho_r")
     eps = float(optimizer.defaults["epsilon"])
     qgroup = getattr(batch_group, "q_norm_group", None)

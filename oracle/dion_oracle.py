@@ -329,15 +329,21 @@ def _fs_batch_gen(per_rank: List[List[DionMatrix]], real: int, hyper: DionHyper,
         (q_norm_group, :994-1001) [yield]; Q_k = R_k / (sqrt(sum) + eps)
       weight update of its shard with the GLOBAL shape's scaled LR (:1056-1090)
 
-    per_rank[k] holds rank k's B = W entries (padded entries carry zero G/M/Q); the reduce-
-    scatter sums in rank order.  `sketch_fn(rank, entry, P)`."""
+    per_rank[k] holds rank k's B = W entries (padded entries carry zero G/M/Q).  The reduce-
+    scatter sums in the order of the reference's collective on gloo, a ring: the chunk rank j
+    receives is p_{j-1} + p_{j-2} + ... + p_j, rounded in P's dtype after every hop (found from
+    the reference's FS = 4 bf16 captures f6 / f7, every element: scripts/dev/r06/fs4_reduce_order.py;
+    at FS = 2 it is the one addition).  `sketch_fn(rank, entry, P)`."""
     W = len(per_rank)
     B = len(per_rank[0])
     idx_of = list(indices) if indices is not None else list(range(W))
     proj = [_project(mats) for mats in per_rank]
-    P_sum = proj[0][2].clone()
-    for k in range(1, W):
-        P_sum = P_sum + proj[k][2]
+    P_sum = torch.empty_like(proj[0][2])
+    for j in range(B):
+        acc = proj[(j - 1) % W][2][j].clone()
+        for t in range(2, W + 1):
+            acc = acc + proj[(j - t) % W][2][j]
+        P_sum[j] = acc
     yield                                                   # reduce-scatter in flight
     P_ortho = torch.zeros_like(P_sum)
     for k in range(W):

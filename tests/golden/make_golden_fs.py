@@ -43,6 +43,13 @@ CASES = [
     dict(name="f4_fs2_bf16_cols", mats=[("a", 64, 48, 1), ("b", 64, 48, 1)], rf=1 / 6, steps=2, bf16=True),
     dict(name="f5_fs2_bf16_mixed", mats=[("u", 80, 51, 1), ("v", 80, 51, 1), ("w", 72, 56, 0)], rf=0.25,
          steps=2, bf16=True),
+    # round 6: the speedrun's FS = 4 itself with bf16 state, where the reduce-scatter of the bf16
+    # partial P sums four terms (the reference's collective rounds per hop, in its own order):
+    # a full batch of 4 column-sharded matrices + a padded batch, and uneven + row-sharded mixed
+    dict(name="f6_fs4_bf16_cols", mats=[("a", 64, 48, 1), ("b", 64, 48, 1), ("c", 64, 48, 1), ("d", 64, 48, 1),
+                                        ("e", 64, 48, 1)], rf=1 / 6, steps=2, bf16=True, world=4),
+    dict(name="f7_fs4_bf16_mixed", mats=[("u", 80, 51, 1), ("v", 80, 51, 1), ("w", 72, 56, 0)], rf=0.25,
+         steps=2, bf16=True, world=4),
 ]
 HYPER = dict(lr=0.01, mu=0.95, weight_decay=0.01, epsilon=1e-8, rcqr_oversample=1.25,
              scale_mode="spectral", extra_scale_factor=0.2)
@@ -198,11 +205,11 @@ def main():
             manifest = json.load(fh)
         manifest["cases"] = [c for c in manifest["cases"] if c["name"] not in only]
     port = 29711
-    world = 2
     for case in CASES:
         port += 1
         if only and case["name"] not in only:
             continue
+        world = int(case.get("world", 2))
         with tempfile.TemporaryDirectory() as tmp:
             paths = [os.path.join(tmp, f"rank{r}") for r in range(world)]
             ctx = mp.get_context("spawn")

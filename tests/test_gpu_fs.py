@@ -30,9 +30,10 @@ def _need_gpu():
 
 
 @pytest.mark.parametrize("name", ["f1_fs2_cols", "f2_fs2_rows_pad", "f3_fs2_uneven_mixed", "f4_fs2_bf16_cols",
-                                  "f5_fs2_bf16_mixed"])
+                                  "f5_fs2_bf16_mixed", "f6_fs4_bf16_cols", "f7_fs4_bf16_mixed"])
 @pytest.mark.parametrize("deferred", [False, True], ids=["eager_ef", "deferred_ef"])
 def test_hip_fs2_matches_reference(name, deferred):
+    # f6 / f7: FS = 4 (4 gloo ranks on cuda:0), the speedrun's bf16 state
     _need_gpu()
     res = run_fs(name, deferred=deferred, device="cuda:0")
     check_fs_results(res, name, deferred, TOL, bf16_tols=BF16_GPU_TOLS)
