@@ -4733,6 +4733,183 @@ __global__ void __launch_bounds__(64 * NW, ((RB >= 8 && !kH3Pairs) || NW >= 8) ?
           acc[rb][cb] * ps;
 }
 
+// ---- pass B, transposed (R = M P), h3, with LDS-DMA staging (round 6): rowproj_h3_kernel's
+// arithmetic (bitwise: the same products in the same order), but nothing in flight sits in
+// registers.  rowproj_h3_kernel loads a step's M into registers and needs it at once, so the
+// only latency cover is the other resident waves, each with one 4 KB step in flight during
+// its load phase; its SQ counters show the waves waiting (wait_any 0.58) at 0.65 of 8 TB/s
+// on a read-only stream.  Here every step is one unit of D slots: the wave's M tile (32 rows
+// x 32 columns, 4 KB, global_load_lds_dwordx4 straight into the transpose tile's swizzled
+// layout: chunk k of row r at r * 8 + (k ^ (r & 7)), the swizzle on the source address) and
+// the block's P split of the step (NQ x 16 B).  Units are issued in step order D - 1 steps
+// ahead; the wait that closes a step retires only the next step's unit (vector-memory
+// operations retire in issue order), so D - 2 units stay in flight across every barrier.  A
+// unit's slot is refilled at the top of the step after the one that read it, behind that
+// step's closing barrier (all waves are done with its split).  LDS: D (NW 4 KB + NQ 16 B).
+template <int RB, int NW, int D>
+__global__ void __launch_bounds__(64 * NW, 1) rowproj_h3gl_kernel(const ProjArgs a) {
+  constexpr int R = 16 * RB;
+  constexpr int NQ = RB * 2 * 64;          // f16x8 units of one step's P split
+  constexpr int NS = NQ / (64 * NW);       // split DMA loads per wave and step
+  constexpr int NU = NS + 4;               // DMA loads per wave and unit
+  static_assert(NQ % (64 * NW) == 0 && D >= 2 && D <= 4, "rowproj_h3gl_kernel geometry");
+  __shared__ f16x8 tq[D][NQ];
+  __shared__ f32x4 ms[D][NW][32 * 8];
+  const BlockXYZ blk = xcd_block();
+  const int b = blk.z;
+  const int kc = blk.y;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int row_base = blk.x * (32 * NW) + wave * 32;
+  const int j_begin = kc * a.kchunk;
+  const int j_end = min(a.cols, j_begin + a.kchunk);
+  const int nsteps = (j_end - j_begin + 31) / 32;
+  // DMA lane (row 8 q + lane / 8, slot chunk lane % 8) reads source chunk (lane % 8) ^ (lane / 8)
+  const char* Mb = reinterpret_cast<const char*>(a.m[b] + static_cast<long>(row_base) * a.ld_m);
+  const uint32_t m_off = static_cast<uint32_t>(((lane >> 3) * a.ld_m + 4 * ((lane & 7) ^ (lane >> 3))) * 4);
+  const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
+  const uint32_t u_off = static_cast<uint32_t>(tid) * 16;
+  auto issue = [&](int s, int slot) {
+    const long u0 = static_cast<long>((j_begin + 32 * s) / 32);
+#pragma unroll
+    for (int it = 0; it < NS; ++it)
+      glds16<false>(qs + u0 * NQ + it * 64 * NW, u_off, lds_off(&tq[slot][it * 64 * NW + wave * 64]));
+    const int j = j_begin + 32 * s;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      glds16<kNt != 0>(Mb + (static_cast<long>(8 * q) * a.ld_m + j) * 4, m_off, lds_off(&ms[slot][wave][q * 64]));
+  };
+  // retire every unit but the newest `ahead` (0 .. D - 2) and meet the block
+  auto wait_units = [](int ahead) {
+    if (D >= 4 && ahead >= 2)
+      gl_wait_barrier<(D >= 4 ? 2 : 0) * NU>();
+    else if (D >= 3 && ahead >= 1)
+      gl_wait_barrier<NU>();
+    else
+      gl_wait_barrier<0>();
+  };
+
+  f32x4 acc[kRBE][RB];
+#pragma unroll
+  for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint32_t mab = a.mabs != nullptr ? a.mabs[b] : kAbsUnknown;
+  float finv = 1.f;
+  const float fs = h3_scale(__uint_as_float(mab), finv);
+  const bool fixed = mab < kAbsUnknown;
+
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s)
+    if (s < nsteps) issue(s, s);
+  wait_units(min(D - 2, nsteps - 1));
+
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s % D;
+    const int nxt = s + D - 1;  // its slot (s - 1) % D was read by every wave before the last barrier
+    if (nxt < nsteps) issue(nxt, nxt % D);
+    const f32x4* xw = ms[cur][wave];
+    f32x4 X[kRBE][2];
+#pragma unroll
+    for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int r = 16 * rb + t, k = 4 * c + g;
+        X[rb][c] = xw[r * 8 + (k ^ xt_swz(r))];
+      }
+    const f16x8* tqc = tq[cur];
+    Split2h Bx[kRBE];
+    float invx[kRBE];
+    if (fixed) {
+#pragma unroll
+      for (int rb = 0; rb < kRBE; ++rb) split2h(X[rb][0], X[rb][1], fs, Bx[rb]);
+      if constexpr (RB >= 8 && kH3Pairs) {
+        // r > 64: two cb of the split P at a time (rowproj_h3_kernel's order)
+#pragma unroll
+        for (int cp = 0; cp < RB; cp += 2) {
+          Split2h A0, A1;
+          A0.hi = tqc[(cp * 2 + 0) * 64 + lane];
+          A0.lo = tqc[(cp * 2 + 1) * 64 + lane];
+          A1.hi = tqc[(cp * 2 + 2) * 64 + lane];
+          A1.lo = tqc[(cp * 2 + 3) * 64 + lane];
+#pragma unroll
+          for (int rb = 0; rb < kRBE; ++rb) {
+            acc[rb][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.lo, Bx[rb].hi, acc[rb][cp], 0, 0, 0);
+            acc[rb][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.lo, Bx[rb].hi, acc[rb][cp + 1], 0, 0, 0);
+          }
+#pragma unroll
+          for (int rb = 0; rb < kRBE; ++rb) {
+            acc[rb][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.hi, Bx[rb].lo, acc[rb][cp], 0, 0, 0);
+            acc[rb][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.hi, Bx[rb].lo, acc[rb][cp + 1], 0, 0, 0);
+          }
+#pragma unroll
+          for (int rb = 0; rb < kRBE; ++rb) {
+            acc[rb][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.hi, Bx[rb].hi, acc[rb][cp], 0, 0, 0);
+            acc[rb][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.hi, Bx[rb].hi, acc[rb][cp + 1], 0, 0, 0);
+          }
+        }
+      } else {
+        Split2h A[RB];
+#pragma unroll
+        for (int cb = 0; cb < RB; ++cb) {
+          A[cb].hi = tqc[(cb * 2 + 0) * 64 + lane];
+          A[cb].lo = tqc[(cb * 2 + 1) * 64 + lane];
+        }
+#pragma unroll
+        for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < RB; ++cb)
+            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].lo, Bx[rb].hi, acc[rb][cb], 0, 0, 0);
+#pragma unroll
+        for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < RB; ++cb)
+            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].hi, Bx[rb].lo, acc[rb][cb], 0, 0, 0);
+#pragma unroll
+        for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < RB; ++cb)
+            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].hi, Bx[rb].hi, acc[rb][cb], 0, 0, 0);
+      }
+    } else {
+      // no max |M| from pass A: a per-step scale per row, as in rowproj_h3_kernel
+#pragma unroll
+      for (int rb = 0; rb < kRBE; ++rb) {
+        float m8 = max8abs(X[rb][0], X[rb][1]);
+        m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
+        m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
+        const float sx = h3_scale(m8, invx[rb]);
+        split2h(X[rb][0], X[rb][1], sx, Bx[rb]);
+      }
+#pragma unroll
+      for (int cb = 0; cb < RB; ++cb) {
+        Split2h A;
+        A.hi = tqc[(cb * 2 + 0) * 64 + lane];
+        A.lo = tqc[(cb * 2 + 1) * 64 + lane];
+#pragma unroll
+        for (int rb = 0; rb < kRBE; ++rb) {
+          const f32x4 d = mfma3h(A, Bx[rb], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[rb][cb][q] = fmaf(d[q], invx[rb], acc[rb][cb][q]);
+        }
+      }
+    }
+    if (s + 1 < nsteps) wait_units(min(nxt, nsteps - 1) - (s + 1));
+  }
+
+  const float ps = (a.tinv != nullptr ? a.tinv[b] : kPSplitInv) * (fixed ? finv : 1.f);
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int rb = 0; rb < kRBE; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(row_base + 16 * rb + t) * R + 16 * cb + 4 * g) =
+          acc[rb][cb] * ps;
+}
+
 // ============================================================================
 // host side
 // ============================================================================
@@ -4808,6 +4985,31 @@ Geo rowproj_geo(int rows, int cols, int batch, int block_rows = 128, int target 
   return g;
 }
 
+// transposed pass B on LDS-DMA staging (rowproj_h3gl_kernel, round 6): 1 = wherever its
+// geometry fits (r = 64 / 128, rows in 32 NW-row blocks, whole 32-column steps), else
+// rowproj_h3_kernel; NW waves per block (one block per CU), D staging units (LDS
+// D (NW 4 KB + r 128 B); r = 128 keeps at most 3)
+#ifndef DION_PBR_GL
+#define DION_PBR_GL 1
+#endif
+#ifndef DION_PBR_GL_NW
+#define DION_PBR_GL_NW 8
+#endif
+#ifndef DION_PBR_GL_D
+#define DION_PBR_GL_D 3
+#endif
+#ifndef DION_TB_PBRGL
+#define DION_TB_PBRGL 1024
+#endif
+constexpr int kPbrGlNW = DION_PBR_GL_NW;
+template <int RB>
+constexpr int pbr_gl_d() { return RB >= 8 && DION_PBR_GL_D > 3 ? 3 : DION_PBR_GL_D; }
+bool pbr_gl_ok(int rows, int cols, int r) {
+  return DION_PBR_GL && (r == 64 || r == 128) && rows % (32 * kPbrGlNW) == 0 && cols % 32 == 0;
+}
+// the transposed pass B's h3 geometry (launch and workspace sizing)
+Geo pbr_geo(int rows, int cols, int batch, int r);
+
 // column projection: X rows x cols, reduce over rows
 Geo colproj_geo(int rows, int cols, int batch, bool panel, int kalign = 16) {
   Geo g;
@@ -4869,6 +5071,10 @@ constexpr int kPbRNW = 4;
 constexpr int kColH3CT = 4;
 // r > 64 (RB = 8) keeps 2 columns per lane: 4 would need 256+ VGPRs (one wave per SIMD)
 constexpr int colh3_ct(int r) { return r > 64 ? 2 : kColH3CT; }
+Geo pbr_geo(int rows, int cols, int batch, int r) {
+  return pbr_gl_ok(rows, cols, r) ? rowproj_geo(rows, cols, batch, 32 * kPbrGlNW, DION_TB_PBRGL)
+                                  : rowproj_geo(rows, cols, batch, 16 * kRBE * kPbRNW, kTbPbr);
+}
 bool colh3_ok(int rows, int cols, int r) {
   return kPbH3 && rows % 32 == 0 && cols % (16 * colh3_ct(r) * kColX6NW) == 0;
 }
@@ -5150,9 +5356,8 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
                             : (rows % 32 == 0 && cols % ((r >= 64 ? 32 : 64) * kColX6NW) == 0));
   const bool h3 = fast && gdt == DION_DTYPE_NONE &&
                   (row_mode ? (kPbH3r && rows % (16 * kRBE * kPbRNW) == 0) : colh3_ok(rows, cols, r));
-  const Geo geo = row_mode ? rowproj_geo(rows, cols, batch,
-                                         h3 ? 16 * kRBE * kPbRNW : x6 ? 64 * kRBE : (fast ? 64 * kRB : 128),
-                                         h3 ? kTbPbr : kTargetBlocks)
+  const Geo geo = row_mode ? (h3 ? pbr_geo(rows, cols, batch, r)
+                                : rowproj_geo(rows, cols, batch, x6 ? 64 * kRBE : (fast ? 64 * kRB : 128), kTargetBlocks))
                  : h3      ? colh3_geo(rows, cols, batch, r)
                  : x6      ? colx6_geo(rows, cols, batch, r)
                            : colproj_geo(rows, cols, batch, false);
@@ -5246,8 +5451,15 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
     constexpr int RB = decltype(RBc)::value;
     return dispatch_gdt(gdt, [&](auto Gc) {
       constexpr int GD = decltype(Gc)::value;
-      if (h3 && row_mode)
+      if (h3 && row_mode) {
+        if constexpr (RB == 4 || RB == 8) {
+          if (pbr_gl_ok(rows, cols, r)) {
+            hipLaunchKernelGGL((rowproj_h3gl_kernel<RB, kPbrGlNW, pbr_gl_d<RB>()>), grid, dim3(64 * kPbrGlNW), 0, st, a);
+            return check_launch("rowproj_h3gl");
+          }
+        }
         hipLaunchKernelGGL((rowproj_h3_kernel<RB, kPbRNW>), grid, dim3(64 * kPbRNW), 0, st, a);
+      }
       else if (h3)
         hipLaunchKernelGGL((colproj_h3_kernel<RB, kColX6NW, colh3_ct(16 * RB)>), grid, dim3(64 * kColX6NW), 0, st, a);
       else if (x6)
@@ -5669,6 +5881,8 @@ int dion_workspace_bytes(const DionBatchDesc* d, int op, size_t* bytes) {
           if (ne > n) n = ne;
           const size_t nh = slab_bytes(rowproj_geo(d->m, d->n, chunk, 16 * kRBE * kPbRNW, kTbPbr), chunk, d->r);
           if (nh > n) n = nh;
+          const size_t ng = slab_bytes(pbr_geo(d->m, d->n, chunk, d->r), chunk, d->r);
+          if (ng > n) n = ng;
         } else {
           const size_t nx = slab_bytes(colx6_geo(d->m, d->n, chunk, d->r), chunk, d->r);
           if (nx > n) n = nx;
