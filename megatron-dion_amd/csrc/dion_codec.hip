@@ -3649,6 +3649,196 @@ __global__ void __launch_bounds__(64 * NW, (RB >= 8 && !kH3Pairs) ? 1 : 2) colpr
           acc[c][cb] * ps;
 }
 
+// ---- pass B, not transposed (R = M^T P), h3, with LDS-DMA staging (round 6):
+// colproj_h3_kernel's arithmetic at CT columns per lane (bitwise the same products in the same
+// order), with rowproj_h3gl_kernel's staging: each step (32 rows) is one unit of D slots -- the
+// wave's M tile (32 rows x 16 CT columns, global_load_lds_dwordx4, row-major; row r sits in
+// row slot r ^ ((r >> 3) & 1), so the four 8-row groups g that one ds_read serves alternate
+// bank halves) and the block's P split of the step -- issued D - 1 steps ahead, D - 2 units in
+// flight across each step's closing barrier.  LDS: D (NW 64 CT B x 32 + r 128 B).
+template <int CT>
+__device__ __forceinline__ int colgl_rs(int r) {
+  return CT == 2 ? (r ^ ((r >> 3) & 1)) : r;  // CT = 4: a 256-B row spans all banks
+}
+
+template <int RB, int NW, int CT, int D>
+__global__ void __launch_bounds__(64 * NW, 1) colproj_h3gl_kernel(const ProjArgs a) {
+  constexpr int R = 16 * RB;
+  constexpr int NQ = RB * 2 * 64;      // f16x8 units of one step's P split
+  constexpr int NS = NQ / (64 * NW);   // split DMA loads per wave and step
+  constexpr int WC = 16 * CT;          // columns per wave
+  constexpr int RC = WC / 4;           // 16-B chunks per tile row
+  constexpr int RPI = 64 / RC;         // tile rows per DMA instruction
+  constexpr int NMI = 32 / RPI;        // DMA instructions of M per wave and step
+  constexpr int NU = NS + NMI;         // DMA loads per wave and unit
+  static_assert(NQ % (64 * NW) == 0 && D >= 2 && D <= 4 && (CT == 2 || CT == 4), "colproj_h3gl_kernel geometry");
+  typedef float vec __attribute__((ext_vector_type(CT)));
+  __shared__ f16x8 tq[D][NQ];
+  __shared__ f32x4 ms[D][NW][32 * RC];
+  const BlockXYZ blk = xcd_block_col();
+  const int b = blk.z;
+  const int kc = blk.y;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int t = lane & 15;
+  const int g = lane >> 4;
+  const int col_base = blk.x * (WC * NW) + wave * WC;
+  const int i_begin = kc * a.kchunk;
+  const int i_end = min(a.rows, i_begin + a.kchunk);
+  const int nsteps = (i_end - i_begin + 31) / 32;
+  // DMA lane: row slot q RPI + lane / RC, chunk lane % RC, loading source row colgl_rs(slot):
+  // CT = 2 (RPI 8: instruction q is the 8-row group q) swaps row pairs in odd groups
+  const char* Mb = reinterpret_cast<const char*>(a.m[b] + col_base);
+  const uint32_t m_off0 = static_cast<uint32_t>((static_cast<long>(lane / RC) * a.ld_m + 4 * (lane % RC)) * 4);
+  const uint32_t m_off1 =
+      static_cast<uint32_t>((static_cast<long>((lane / RC) ^ (CT == 2 ? 1 : 0)) * a.ld_m + 4 * (lane % RC)) * 4);
+  const u32x4* qs = static_cast<const u32x4*>(a.tsplit) + b * a.ts_stride;
+  const uint32_t u_off = static_cast<uint32_t>(tid) * 16;
+  auto issue = [&](int s, int slot) {
+    const long u0 = static_cast<long>((i_begin + 32 * s) / 32);
+#pragma unroll
+    for (int it = 0; it < NS; ++it)
+      glds16<false>(qs + u0 * NQ + it * 64 * NW, u_off, lds_off(&tq[slot][it * 64 * NW + wave * 64]));
+    const long i = i_begin + 32 * s;
+#pragma unroll
+    for (int q = 0; q < NMI; ++q)
+      glds16<kNt != 0>(Mb + (i + q * RPI) * a.ld_m * 4, (CT == 2 && (q & 1)) ? m_off1 : m_off0,
+                       lds_off(&ms[slot][wave][q * 64]));
+  };
+  auto wait_units = [](int ahead) {
+    if (D >= 4 && ahead >= 2)
+      gl_wait_barrier<(D >= 4 ? 2 : 0) * NU>();
+    else if (D >= 3 && ahead >= 1)
+      gl_wait_barrier<NU>();
+    else
+      gl_wait_barrier<0>();
+  };
+
+  f32x4 acc[CT][RB];
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb) acc[c][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint32_t mab = a.mabs != nullptr ? a.mabs[b] : kAbsUnknown;
+  float finv = 1.f;
+  const float fs = h3_scale(__uint_as_float(mab), finv);
+  const bool fixed = mab < kAbsUnknown;
+
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s)
+    if (s < nsteps) issue(s, s);
+  wait_units(min(D - 2, nsteps - 1));
+
+  // the scale mode is a template argument of the loop, as in colproj_h3_kernel (with a run-time
+  // branch inside the step the per-column scales of the CT = 2 path came out wrong: round 6)
+  auto run = [&](auto FIXc) {
+  constexpr bool FIX = decltype(FIXc)::value;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s % D;
+    const int nxt = s + D - 1;
+    if (nxt < nsteps) issue(nxt, nxt % D);
+    const float* xw = reinterpret_cast<const float*>(ms[cur][wave]);
+    vec x[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = *reinterpret_cast<const vec*>(xw + colgl_rs<CT>(8 * g + e) * WC + CT * t);
+    const f16x8* tqc = tq[cur];
+    Split2h B[CT];
+    float inv[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const f32x4 lo4{x[0][c], x[1][c], x[2][c], x[3][c]};
+      const f32x4 hi4{x[4][c], x[5][c], x[6][c], x[7][c]};
+      if constexpr (FIX) {
+        split2h(lo4, hi4, fs, B[c]);
+      } else {
+        float m8 = max8abs(lo4, hi4);
+        m8 = fmaxf(m8, __shfl_xor(m8, 16, 64));
+        m8 = fmaxf(m8, __shfl_xor(m8, 32, 64));
+        const float sc = h3_scale(m8, inv[c]);
+        split2h(lo4, hi4, sc, B[c]);
+      }
+    }
+    if constexpr (FIX) {
+      if constexpr (RB >= 8 && kH3Pairs) {
+#pragma unroll
+        for (int cp = 0; cp < RB; cp += 2) {
+          Split2h A0, A1;
+          A0.hi = tqc[(cp * 2 + 0) * 64 + lane];
+          A0.lo = tqc[(cp * 2 + 1) * 64 + lane];
+          A1.hi = tqc[(cp * 2 + 2) * 64 + lane];
+          A1.lo = tqc[(cp * 2 + 3) * 64 + lane];
+#pragma unroll
+          for (int c = 0; c < CT; ++c) {
+            acc[c][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.lo, B[c].hi, acc[c][cp], 0, 0, 0);
+            acc[c][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.lo, B[c].hi, acc[c][cp + 1], 0, 0, 0);
+          }
+#pragma unroll
+          for (int c = 0; c < CT; ++c) {
+            acc[c][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.hi, B[c].lo, acc[c][cp], 0, 0, 0);
+            acc[c][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.hi, B[c].lo, acc[c][cp + 1], 0, 0, 0);
+          }
+#pragma unroll
+          for (int c = 0; c < CT; ++c) {
+            acc[c][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0.hi, B[c].hi, acc[c][cp], 0, 0, 0);
+            acc[c][cp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1.hi, B[c].hi, acc[c][cp + 1], 0, 0, 0);
+          }
+        }
+      } else {
+        Split2h A[RB];
+#pragma unroll
+        for (int cb = 0; cb < RB; ++cb) {
+          A[cb].hi = tqc[(cb * 2 + 0) * 64 + lane];
+          A[cb].lo = tqc[(cb * 2 + 1) * 64 + lane];
+        }
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+          for (int cb = 0; cb < RB; ++cb)
+            acc[c][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].lo, B[c].hi, acc[c][cb], 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+          for (int cb = 0; cb < RB; ++cb)
+            acc[c][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].hi, B[c].lo, acc[c][cb], 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+          for (int cb = 0; cb < RB; ++cb)
+            acc[c][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[cb].hi, B[c].hi, acc[c][cb], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int cb = 0; cb < RB; ++cb) {
+        Split2h A;
+        A.hi = tqc[(cb * 2 + 0) * 64 + lane];
+        A.lo = tqc[(cb * 2 + 1) * 64 + lane];
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          const f32x4 d = mfma3h(A, B[c], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[c][cb][q] = fmaf(d[q], inv[c], acc[c][cb][q]);
+        }
+      }
+    }
+    if (s + 1 < nsteps) wait_units(min(nxt, nsteps - 1) - (s + 1));
+  }
+  };
+  if (fixed)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
+
+  const float ps = (a.tinv != nullptr ? a.tinv[b] : kPSplitInv) * (fixed ? finv : 1.f);
+  float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+      *reinterpret_cast<f32x4*>(out + static_cast<long>(col_base + CT * t + c) * R + 16 * cb + 4 * g) =
+          acc[c][cb] * ps;
+}
+
 // ---- pass A, not transposed, h3 products (fp16x3): rowproj_ef_kernel's geometry, TJ
 // line loads and line stores; the error feedback's fixed operands (P', R') carry
 // per-matrix scales, and in the projection the streamed X is the B operand (lane (t, g)
@@ -4807,6 +4997,10 @@ __global__ void __launch_bounds__(64 * NW, 1) rowproj_h3gl_kernel(const ProjArgs
     if (s < nsteps) issue(s, s);
   wait_units(min(D - 2, nsteps - 1));
 
+  // the scale mode is a template argument of the loop (colproj_h3gl_kernel: a run-time branch
+  // inside the step gave wrong per-column scales there)
+  auto run = [&](auto FIXc) {
+  constexpr bool FIX = decltype(FIXc)::value;
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s % D;
     const int nxt = s + D - 1;  // its slot (s - 1) % D was read by every wave before the last barrier
@@ -4823,7 +5017,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rowproj_h3gl_kernel(const ProjArgs
     const f16x8* tqc = tq[cur];
     Split2h Bx[kRBE];
     float invx[kRBE];
-    if (fixed) {
+    if constexpr (FIX) {
 #pragma unroll
       for (int rb = 0; rb < kRBE; ++rb) split2h(X[rb][0], X[rb][1], fs, Bx[rb]);
       if constexpr (RB >= 8 && kH3Pairs) {
@@ -4899,6 +5093,11 @@ __global__ void __launch_bounds__(64 * NW, 1) rowproj_h3gl_kernel(const ProjArgs
     }
     if (s + 1 < nsteps) wait_units(min(nxt, nsteps - 1) - (s + 1));
   }
+  };
+  if (fixed)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
 
   const float ps = (a.tinv != nullptr ? a.tinv[b] : kPSplitInv) * (fixed ? finv : 1.f);
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
@@ -5010,6 +5209,33 @@ bool pbr_gl_ok(int rows, int cols, int r) {
 // the transposed pass B's h3 geometry (launch and workspace sizing)
 Geo pbr_geo(int rows, int cols, int batch, int r);
 
+// pass B, not transposed, on LDS-DMA staging (colproj_h3gl_kernel, round 6): 1 = wherever its
+// geometry fits (r = 64 / 128, rows in 32-row steps, columns in 16 CT NW-column blocks), else
+// colproj_h3_kernel; CT columns per lane, D staging units (capped by the 160 KB of LDS)
+#ifndef DION_PBC_GL
+#define DION_PBC_GL 1
+#endif
+#ifndef DION_PBC_GL_CT
+#define DION_PBC_GL_CT 2
+#endif
+#ifndef DION_PBC_GL_D
+#define DION_PBC_GL_D 3
+#endif
+#ifndef DION_TB_PBCGL
+#define DION_TB_PBCGL 1024
+#endif
+constexpr int kPbcGlNW = 8, kPbcGlCT = DION_PBC_GL_CT;
+template <int RB>
+constexpr int pbc_gl_d() {
+  constexpr int unit = kPbcGlNW * 32 * 16 * kPbcGlCT * 4 + RB * 2 * 64 * 16;  // bytes per staging unit
+  constexpr int most = 160 * 1024 / unit;
+  return DION_PBC_GL_D < most ? DION_PBC_GL_D : most;
+}
+bool pbc_gl_ok(int rows, int cols, int r) {
+  return DION_PBC_GL && (r == 64 || r == 128) && rows % 32 == 0 && cols % (16 * kPbcGlCT * kPbcGlNW) == 0;
+}
+Geo pbc_geo(int rows, int cols, int batch, int r);
+
 // column projection: X rows x cols, reduce over rows
 Geo colproj_geo(int rows, int cols, int batch, bool panel, int kalign = 16) {
   Geo g;
@@ -5079,9 +5305,24 @@ bool colh3_ok(int rows, int cols, int r) {
   return kPbH3 && rows % 32 == 0 && cols % (16 * colh3_ct(r) * kColX6NW) == 0;
 }
 Geo colh3_geo(int rows, int cols, int batch, int r) {
+  if (pbc_gl_ok(rows, cols, r)) return pbc_geo(rows, cols, batch, r);
   Geo g;
   g.gx = static_cast<int>(ceil_div(cols, 16 * colh3_ct(r) * kColX6NW));
   long want = ceil_div(kTbPbc, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
+  long maxc = ceil_div(rows, 256);
+  long nc = want < maxc ? want : maxc;
+  if (nc < 1) nc = 1;
+  g.kchunk = round_up(ceil_div(rows, nc), 32);
+  g.nchunk = static_cast<int>(ceil_div(rows, g.kchunk));
+  g.out_rows = cols;
+  return g;
+}
+
+Geo pbc_geo(int rows, int cols, int batch, int r) {
+  (void)r;
+  Geo g;
+  g.gx = static_cast<int>(ceil_div(cols, 16 * kPbcGlCT * kPbcGlNW));
+  long want = ceil_div(DION_TB_PBCGL, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
   long maxc = ceil_div(rows, 256);
   long nc = want < maxc ? want : maxc;
   if (nc < 1) nc = 1;
@@ -5460,8 +5701,16 @@ int run_projection(bool row_mode, int rows, int cols, int r, int batch, const vo
         }
         hipLaunchKernelGGL((rowproj_h3_kernel<RB, kPbRNW>), grid, dim3(64 * kPbRNW), 0, st, a);
       }
-      else if (h3)
+      else if (h3) {
+        if constexpr (RB == 4 || RB == 8) {
+          if (pbc_gl_ok(rows, cols, r)) {
+            hipLaunchKernelGGL((colproj_h3gl_kernel<RB, kPbcGlNW, kPbcGlCT, pbc_gl_d<RB>()>), grid, dim3(64 * kPbcGlNW), 0,
+                               st, a);
+            return check_launch("colproj_h3gl");
+          }
+        }
         hipLaunchKernelGGL((colproj_h3_kernel<RB, kColX6NW, colh3_ct(16 * RB)>), grid, dim3(64 * kColX6NW), 0, st, a);
+      }
       else if (x6)
         hipLaunchKernelGGL((colproj_x6_kernel<RB, kColX6NW>), grid, dim3(64 * kColX6NW), 0, st, a);
       else if (fast && row_mode)
