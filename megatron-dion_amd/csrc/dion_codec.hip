@@ -3427,13 +3427,16 @@ __global__ void __launch_bounds__(256) presplit16_kernel(const Presplit16Args a)
     if (a.fix != nullptr) {
       // the fix-up's P half (kernels.py:185-188) with this rank's zero test: every element of
       // P is one (unit, lane, e) of the layout, so each is rewritten exactly once
+      // (only a value the fix-up changes is written back: an orthonormalised P is normally all
+      // finite and its momentum nonzero, so P is read once and nothing but the split is written)
       const bool zero = a.fix[b] == 0u;
       float* __restrict__ dst = const_cast<float*>(src);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int k = a.kmap == 0 ? 8 * g + e : 16 * (e >> 2) + 4 * g + (e & 3);
-        v[e] = zero ? 0.f : nan_to_num(v[e]);
-        dst[(blk * 32 + k) * a.r + 16 * cb + t] = v[e];
+        const float f = zero ? 0.f : nan_to_num(v[e]);
+        if (__float_as_uint(f) != __float_as_uint(v[e])) dst[(blk * 32 + k) * a.r + 16 * cb + t] = f;
+        v[e] = f;
       }
     }
   } else {

@@ -48,7 +48,7 @@ class MegatronDion(Optimizer):
                  extra_scale_factor: float = 0.2, split_qkv: bool = False, split_linear: bool = False,
                  max_concurrent_tasks: Optional[int] = None, *, codec=None, sketch_seed: int = 0,
                  coalesce_local: bool = True, local_streams: int = 3, coalesce_max_entries: int = 16,
-                 defer_error_feedback: bool = True, pipeline_lookahead: int = 2):
+                 defer_error_feedback: bool = True, pipeline_lookahead: int = 2, replicated_pipeline: bool = True):
         if isinstance(params, (list, tuple)):
             for pg in params:
                 if isinstance(pg, dict) and "wd_mult" in pg:
@@ -89,6 +89,7 @@ class MegatronDion(Optimizer):
         self._rstreams = None
         self._pstreams = None
         self._pipeline_lookahead = max(0, int(pipeline_lookahead))
+        self._replicated_pipeline = bool(replicated_pipeline)
         self._codec = codec
         self._defer_ef = bool(defer_error_feedback)
         self._profile_records: List[Tuple[str, float]] = []
@@ -278,7 +279,13 @@ class MegatronDion(Optimizer):
         if self._local_streams <= 1 or self._pipeline_lookahead <= 0 or not torch.cuda.is_available() \
                 or not batches:
             return False
-        if any(is_replicated(b) for b in batches):
+        # replicated "ddp" batches take the same schedule (round 6): the P exchange and the
+        # owner's orthonormalisation are the latency phase, the collectives waited for inline
+        # in one issue order on every rank (the reference's batch order); FS / TP batches keep
+        # the AsyncRuntime interleave
+        if any(str(getattr(b.batch_group, "kernel_kind", "ddp")) != "ddp" for b in batches):
+            return False
+        if any(is_replicated(b) for b in batches) and not self._replicated_pipeline:
             return False
         if not all(getattr(b.params[0], "is_cuda", False) for b in batches):
             return False

@@ -280,6 +280,13 @@ def reduces_p_over_fs(config) -> bool:
     return (not tr and dim == 1) or (tr and dim == 0)
 
 
+def _collective(issue):
+    """Issue an async collective, yield while it is in flight, wait."""
+    work = issue()
+    yield
+    work.wait()
+
+
 def reduce_in_state_dtype(kind, out, op, group, bf16_state, inp=None, idx=None):
     """A reduction of a P / R buffer over `group`, yielding while it is in flight.
 
@@ -332,9 +339,11 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
     `sketches` (tests only) maps an entry index to an explicit (k, m_P) sketch so
     parity runs can reuse the sketch the reference drew.  `chunks` > 1 marks a
     coalesced group of full W-entry batches (coalesce_replicated_batches).
-    `phase_marks` (world size 1 only): yield "ortho" after pass A and "stream" after
-    the orthonormalisation, so a scheduler can run the latency-bound phase on another
-    HIP stream (MegatronDion._run_local_pipelined).
+    `phase_marks` ("ddp" batches): yield "ortho" after pass A and "stream" after the
+    orthonormalisation -- at W > 1 after the P exchange and the owner's orthonormalisation,
+    every collective then waited for inline (RCCL waits are stream dependencies, not host
+    waits) -- so a scheduler can run the latency-bound phase on another HIP stream
+    (MegatronDion._run_local_pipelined).
     """
     codec = optimizer.codec
     B = len(params)
@@ -365,8 +374,17 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
                                     batch_collectives, commit_updates, use_low_rank, sketches)
         return
 
+    def xchg(gen):
+        # a collective: yielded to the AsyncRuntime, or waited for inline when a phase-marked
+        # scheduler runs the batch (MegatronDion._run_local_pipelined: every other yield is a mark)
+        if phase_marks:
+            for _ in gen:
+                pass
+            return
+        yield from gen
+
     if W > 1 and not use_low_rank and real_grads:
-        yield from dense_replica_all_reduce(optimizer, real_grads, group)
+        yield from xchg(dense_replica_all_reduce(optimizer, real_grads, group))
 
     kch = int(chunks) if (W > 1 and int(chunks) > 1 and B == real == int(chunks) * W) else 0
     if kch:
@@ -418,12 +436,14 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
 
     p_fixed = False
     r_fixed = False  # W = 1: pass B also did the fix-up and column norm (project_r_fixup)
+    if W > 1 and phase_marks:
+        yield "ortho"  # the exchange and the owner's orthonormalisation: the latency phase
     if W > 1 and kch:
         rank = dist.get_rank(group)
         mine = P[rank * kch:(rank + 1) * kch]
         P_own = torch.empty((kch, mp, r), dtype=torch.float32, device=dev)
         if use_low_rank:
-            yield from reduce_in_state_dtype("rs", P_own, dist.ReduceOp.AVG, group, bf16_state, inp=P)
+            yield from xchg(reduce_in_state_dtype("rs", P_own, dist.ReduceOp.AVG, group, bf16_state, inp=P))
         else:
             P_own.copy_(mine)
         clock.mark("p_reduce")
@@ -437,14 +457,14 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
                                      _sketch_seed(optimizer, batch_cache_key, rank * kch + c), oversample,
                                      sketch=None if S is None else S.reshape(1, *S.shape[-2:]).contiguous(),
                                      state_dtype=sdt)
-        work = dist.all_gather_into_tensor(P, P_own, group=group, async_op=True)
-        yield
-        work.wait()
+        yield from xchg(_collective(lambda: dist.all_gather_into_tensor(P, P_own, group=group, async_op=True)))
+        if phase_marks:
+            yield "stream"
         R = torch.empty((B, nq, r), dtype=torch.float32, device=dev)
         p_fixed, r_fixed = _replicated_pass_b(optimizer, codec, momentums, Qs, P, R, nonzero, real, m, n, transposed,
                                               bf16_state, use_low_rank)
         if use_low_rank:
-            yield from reduce_in_state_dtype("ar", R, dist.ReduceOp.AVG, group, bf16_state)
+            yield from xchg(reduce_in_state_dtype("ar", R, dist.ReduceOp.AVG, group, bf16_state))
     elif W > 1:
         rank = dist.get_rank(group)
         padded = (B + W - 1) // W * W
@@ -455,7 +475,8 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
             P_single = torch.empty((1, mp, r), dtype=torch.float32, device=dev)
             if use_low_rank:
                 # runtime.py:1428-1434: reduce-scatter(avg) hands entry start+rank to this rank
-                yield from reduce_in_state_dtype("rs", P_single, dist.ReduceOp.AVG, group, bf16_state, inp=chunk)
+                yield from xchg(reduce_in_state_dtype("rs", P_single, dist.ReduceOp.AVG, group, bf16_state,
+                                                      inp=chunk))
             else:
                 P_single.copy_(chunk[rank:rank + 1])
             idx = start + rank
@@ -463,15 +484,16 @@ def batch_dion_update_async(optimizer, params, momentums, Qs, configs, dist_meta
                 ortho(P_single, idx)
             else:
                 P_single.zero_()  # padded entries stay inert (runtime.py:1436-1441)
-            work = dist.all_gather_into_tensor(chunk, P_single, group=group, async_op=True)
-            yield
-            work.wait()
+            yield from xchg(_collective(lambda: dist.all_gather_into_tensor(chunk, P_single, group=group,
+                                                                            async_op=True)))
+        if phase_marks:
+            yield "stream"
         P = P[:B]
         R = torch.zeros((B, nq, r), dtype=torch.float32, device=dev)
         p_fixed, r_fixed = _replicated_pass_b(optimizer, codec, momentums, Qs, P, R, nonzero, real, m, n, transposed,
                                               bf16_state, use_low_rank)
         if use_low_rank:
-            yield from reduce_in_state_dtype("ar", R, dist.ReduceOp.AVG, group, bf16_state)
+            yield from xchg(reduce_in_state_dtype("ar", R, dist.ReduceOp.AVG, group, bf16_state))
     else:
         # W = 1, fp32 state: the last solve of the orthonormalisation also fixes P (the fix-up's
         # P half, kernels.py:185-188: an orthonormalised P is NaN only in whole columns, whose R

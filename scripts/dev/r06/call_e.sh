@@ -1,11 +1,12 @@
 # round-6 call E: pass B not transposed on LDS-DMA staging (colproj_h3gl_kernel): parity subset,
 # same-box A/B against the register column kernel (pbc0) and its staging variants, rocprof of the
-# default Llama / Mixtral steps (single stream)
+# default Llama / Mixtral steps (single stream); the replicated pipeline (W > 1 on the N = 1 stream
+# schedule) simulated at W = 8 beside this box's N = 1 line
 set -o pipefail
 mkdir -p gpurun_out/r06e
 export TMPDIR=/tmp
 O=gpurun_out/r06e
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused_tail.py tests/test_gpu_fullsize.py tests/test_gpu_configs.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "pass_b or fused_tail or project_r_fixup or config3 or config5 or twelve or explicit_sketch" > $O/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused_tail.py tests/test_gpu_fullsize.py tests/test_gpu_configs.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "pass_b or fused_tail or project_r_fixup or config3 or config4 or config5 or twelve or explicit_sketch or replicated_pipeline" > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 export DION_DEV_ALLOW_LIB_PATH=1
@@ -39,3 +40,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 echo "prof llama ok"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_mx -o run -- python bench.py --workload mixtral-8x7b-experts-r128 --streams 1 --no-cpu-baseline --steps 3 --warmup 2 > $O/prof_mx.log 2>&1 || exit 1
 echo "prof mixtral ok"
+line() { grep '^{"metric' "$1" > "$2" && python -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[1], d['value'], d['ms_per_step'], r['kernel'], r['frac'], r['step']['frac'] if 'step' in r else '')" "$2"; }
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/n1_llama.log 2>&1 || exit 1
+line $O/n1_llama.log $O/n1_llama.json || exit 1
+timeout -k 10 300 python bench.py --simulate-world 8 --steps 20 --warmup 3 --no-cpu-baseline > $O/sim8_llama.log 2>&1 || exit 1
+line $O/sim8_llama.log $O/sim8_llama.json || exit 1

@@ -221,3 +221,65 @@ def test_w2_llama_fc1_fc2_rank_major_hip_matches_oracle():
     # the first and the last matrix of each shape: the two ends of a rank-major group
     _run_and_check(LLAMA_FC, 64, 2, low_rank=True, check=[LLAMA_FC[0][0], LLAMA_FC[3][0], LLAMA_FC[4][0],
                                                           LLAMA_FC[7][0]])
+
+
+def _sched_worker(rank, world, port, out_dir, shapes, r, steps):
+    import sys
+    sys.path.insert(0, ROOT)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    import megatron_dion_amd as mda
+    from megatron_dion_amd.optimizer import attach_dp_routing
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    min_side = min(min(m, c) for _, m, c in shapes)
+    res = {}
+    for mode in (False, True):
+        named = [(n, torch.nn.Parameter((torch.randn(m, c, generator=torch.Generator().manual_seed(i)) * 0.02)
+                                        .to(dev))) for i, (n, m, c) in enumerate(shapes)]
+        opt = mda.MegatronDion([p for _, p in named], lr=0.01, mu=0.95, weight_decay=0.01,
+                               rank_fraction=r / min_side, coalesce_max_entries=16, replicated_pipeline=mode)
+        attach_dp_routing(opt, named, replicate_group=dist.group.WORLD)
+        for n, p in named:  # one Q0 for both schedules
+            opt.state[p]["Q"].copy_(torch.randn(opt.state[p]["Q"].shape,
+                                                generator=torch.Generator().manual_seed(zlib.crc32(n.encode()))))
+        for s in range(steps):
+            for i, (n, p) in enumerate(named):
+                g = torch.Generator().manual_seed(1000 * s + 10 * rank + i)
+                p.main_grad = (torch.randn(p.shape, generator=g) * 1e-3).to(torch.bfloat16).to(dev)
+            opt.step()
+        opt.flush_error_feedback()
+        torch.cuda.synchronize()
+        for n, p in named:
+            res[f"{int(mode)}_{n}_W"] = p.detach().cpu().clone()
+            res[f"{int(mode)}_{n}_Q"] = opt.state[p]["Q"].detach().cpu().clone()
+            res[f"{int(mode)}_{n}_M"] = opt.state[p]["momentum"].detach().cpu().clone()
+        del opt, named
+        torch.cuda.empty_cache()
+    torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_replicated_pipeline_is_bit_identical_to_async_runtime(world):
+    """Round 6: replicated "ddp" batches run on the software-pipelined stream schedule (the P
+    exchange and the owner's orthonormalisation as the latency phase, collectives waited for
+    inline) instead of the AsyncRuntime interleave.  Same kernels on the same data in the same
+    collective order: W, M and Q must equal the AsyncRuntime schedule's bit for bit, on every
+    rank (rank-major groups, a padded batch, deferred EF, 3 steps)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    shapes = [(f"a{i}", 896, 256) for i in range(16 + 3)] + [(f"t{i}", 256, 448) for i in range(16)]
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_sched_worker, args=(world, _port(), tmp, shapes, 64, 3), nprocs=world, join=True,
+                           start_method="spawn")
+        res = [torch.load(os.path.join(tmp, f"rank{q}.pt"), weights_only=True) for q in range(world)]
+    for R in res:
+        for key in R:
+            if key.startswith("1_"):
+                assert torch.equal(R[key], R["0_" + key[2:]]), key
+    for key in res[0]:
+        if key.endswith("_W") or key.endswith("_Q"):
+            for q in range(1, world):
+                assert torch.equal(res[0][key], res[q][key]), (q, key)
