@@ -80,7 +80,7 @@ KERNEL_OF = {("project_p", False): ("rowproj_fast_kernel<4, 2>", 1),
              ("ef_apply_w", False): ("rank_stream_kernel<4, false, 8, 2, true>", 1),
              ("ef_apply_w", True): ("rank_stream_kernel<4, false, 8, 2, true>", 1),
              ("project_r", False): ("colproj_h3_kernel<4, 4, 4>", 1),
-             ("project_r", True): ("rowproj_h3_kernel<4, 4>", 1),
+             ("project_r", True): ("rowproj_h3gl_kernel<4, 8, 3>", 1),
              ("ef_apply", False): ("rank_stream_kernel<4, false, 8, 2>", 2),
              ("ef_apply", True): ("rank_stream_kernel<4, false, 8, 2>", 2)}
 
@@ -194,6 +194,8 @@ MFMA_WORK = (("rowproj_efh3_kernel", 2 * 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("b16_col_kernel", 2, MFMA_BF16_PEAK_TFLOPS),
              ("rowproj_h3_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_h3_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),
+             ("rowproj_h3gl_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),  # the same products, LDS-DMA staging
+             ("colproj_h3gl_kernel", 2 * 3, MFMA_BF16_PEAK_TFLOPS),
              ("colproj_x6_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
              ("rank_stream_kernel@h3", 2 * 3, MFMA_BF16_PEAK_TFLOPS),  # <..., true>: the weight update
              ("rank_stream_kernel", 2 * 6, MFMA_BF16_PEAK_TFLOPS),
@@ -309,8 +311,9 @@ def kernel_names(r):
     rb = {1: 1, 2: 2, 3: 4, 4: 4}.get((r + 15) // 16, 8)
     table = KERNEL_OF_BF16 if BYTES_PER_ELEM is BYTES_PER_ELEM_BF16 else KERNEL_OF
     out = {k: (name.replace("<4", f"<{rb}", 1), n) for k, (name, n) in table.items()}
-    if r > 64 and ("project_r", False) in out:
-        out[("project_r", False)] = (f"colproj_h3_kernel<{rb}, 4, 2>", 1)
+    if r > 64 and ("project_r", False) in out and table is KERNEL_OF:
+        # r = 128: pass B on LDS-DMA staging (colproj_h3gl_kernel, 8 waves, 2 columns per lane)
+        out[("project_r", False)] = (f"colproj_h3gl_kernel<{rb}, 8, 2, 3>", 1)
     if r > 64 and ("project_p_ef", False) in out:
         # r = 128: the LDS-DMA row kernel (bf16 G, rows a multiple of 256: every bench set)
         out[("project_p_ef", False)] = ("rowproj_efgl_kernel<8, 2>", 1)

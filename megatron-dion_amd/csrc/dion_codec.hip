@@ -5190,7 +5190,9 @@ Geo rowproj_geo(int rows, int cols, int batch, int block_rows = 128, int target 
 // transposed pass B on LDS-DMA staging (rowproj_h3gl_kernel, round 6): 1 = wherever its
 // geometry fits (r = 64 / 128, rows in 32 NW-row blocks, whole 32-column steps), else
 // rowproj_h3_kernel; NW waves per block (one block per CU), D staging units (LDS
-// D (NW 4 KB + r 128 B); r = 128 keeps at most 3)
+// D (NW 4 KB + r 128 B); r = 128 keeps at most 3).  Measured (profiles/r06/d_*, one box,
+// kernel-only): Llama fc2 group 687.7 us (register) -> D 2 647.0, D 3 617.1, D 4 670.5;
+// Mixtral 1055 -> 870 us at D 3
 #ifndef DION_PBR_GL
 #define DION_PBR_GL 1
 #endif
@@ -5212,9 +5214,11 @@ bool pbr_gl_ok(int rows, int cols, int r) {
 // the transposed pass B's h3 geometry (launch and workspace sizing)
 Geo pbr_geo(int rows, int cols, int batch, int r);
 
-// pass B, not transposed, on LDS-DMA staging (colproj_h3gl_kernel, round 6): 1 = wherever its
-// geometry fits (r = 64 / 128, rows in 32-row steps, columns in 16 CT NW-column blocks), else
-// colproj_h3_kernel; CT columns per lane, D staging units (capped by the 160 KB of LDS)
+// pass B, not transposed, on LDS-DMA staging (colproj_h3gl_kernel, round 6): 1 = at r = 128
+// wherever its geometry fits (rows in 32-row steps, columns in 16 CT NW-column blocks), else
+// colproj_h3_kernel; CT columns per lane, D staging units (capped by the 160 KB of LDS).
+// Measured (profiles/r06/e_*): r = 128 Mixtral fc1 group 1636 -> 1518 us (kernel), 391.7 ->
+// 393.8 GiB/s; r = 64 slower than the register kernel (587 vs 556-580 us), so r = 64 keeps it
 #ifndef DION_PBC_GL
 #define DION_PBC_GL 1
 #endif
@@ -5235,7 +5239,7 @@ constexpr int pbc_gl_d() {
   return DION_PBC_GL_D < most ? DION_PBC_GL_D : most;
 }
 bool pbc_gl_ok(int rows, int cols, int r) {
-  return DION_PBC_GL && (r == 64 || r == 128) && rows % 32 == 0 && cols % (16 * kPbcGlCT * kPbcGlNW) == 0;
+  return DION_PBC_GL && r == 128 && rows % 32 == 0 && cols % (16 * kPbcGlCT * kPbcGlNW) == 0;
 }
 Geo pbc_geo(int rows, int cols, int batch, int r);
 

@@ -93,3 +93,47 @@ def test_fused_tail_is_the_unfused_sequence(r, transposed):
     assert (Ra - Rc).abs().max().item() <= 2e-6 * scale
     for a, c in zip(Qa, Qc):
         assert (a - c).abs().max().item() <= 2e-6
+
+
+@pytest.mark.parametrize("r,transposed", [(64, False), (128, True)])
+def test_row_sparse_p_follows_the_header_contract(r, transposed):
+    """a row-sparse P (one nonzero row) makes the Cholesky QR overflow (the oracle's
+    orthogonalize returns +-inf there; the reference's nan_to_num then feeds FLT_MAX into R and the
+    update, which is not finite either).  include/dion_codec.h (dion_pfix_split) states what the
+    fused path does instead: the fix-up makes P finite (NaN -> 0, +-inf -> +-FLT_MAX, as
+    nan_to_num), the split of an entry past the fixed scale's range is inf / NaN, so its R column
+    is fixed to 0 where the unfused pass B would rescale.  Pinned here: the fused and the W > 1
+    sequences agree bit for bit, and P, R and Q are finite."""
+    from megatron_dion_amd.codec import HipDionCodec
+
+    dev = _dev()
+    m, n = (1024, 2048) if transposed else (2048, 1024)
+    mp, nq = (n, m) if transposed else (m, n)
+    B = 2
+    gen = torch.Generator().manual_seed(5 + r)
+    Ms = [(torch.randn(m, n, generator=gen) * 1e-2).to(dev) for _ in range(B)]
+    P0 = torch.zeros(B, mp, r)
+    P0[:, 7] = torch.randn(B, r, generator=gen)  # one nonzero row
+    P0 = P0.to(dev).contiguous()
+    Q0 = [torch.randn(nq, r, generator=gen).to(dev) for _ in range(B)]
+    nz = torch.stack([M.abs().max() for M in Ms]).float().cpu().view(torch.int32).clone().to(dev)
+    codec = HipDionCodec(dev)
+    sa = codec.psplit_buffer(B, m, n, r, transposed)
+    sb = codec.psplit_buffer(B, m, n, r, transposed)
+    Pa = P0.clone()
+    codec.orthonormalize(Pa, m, n, transposed, 99, fix_nonzero=nz, p_split=sa)
+    Ra = torch.empty(B, nq, r, device=dev)
+    Qa = [q.clone() for q in Q0]
+    codec.project_r_fixup(Ms, Pa, Ra, Qa, nz, 1e-8, transposed, p_split=sa)
+    Pb = P0.clone()
+    codec.orthonormalize(Pb, m, n, transposed, 99)
+    codec.pfix_split(Pb, m, n, transposed, nz, sb)
+    Rb = torch.empty(B, nq, r, device=dev)
+    Qb = [q.clone() for q in Q0]
+    codec.project_r(Ms, Pb, Rb, transposed, nonzero=nz, p_split=sb)
+    codec.fixup_colnorm(None, Rb, Qb, nz, 1e-8, m, n, transposed)
+    torch.cuda.synchronize()
+    assert torch.equal(Pa.cpu(), Pb.cpu()) and torch.equal(sa.cpu(), sb.cpu()) and torch.equal(Ra.cpu(), Rb.cpu())
+    assert torch.isfinite(Pa).all() and torch.isfinite(Ra).all()
+    for a, b in zip(Qa, Qb):
+        assert torch.equal(a.cpu(), b.cpu()) and torch.isfinite(a).all()
