@@ -645,12 +645,23 @@ __device__ __forceinline__ void rp_compute(RowStep<GDT>& S, f32x4 (&acc)[kRB][RB
 // [x T/8, (x+1) T/8) of the logical blocks, so its resident blocks are neighbouring
 // row blocks of one matrix that read the same thin rows at the same time.
 // waves per block of the fused pass-A row kernel (rowproj_efh3_kernel; 8 measured slower)
-constexpr int kPaNW = 4;
+#ifndef DION_PA_NW
+#define DION_PA_NW 4
+#endif
+constexpr int kPaNW = DION_PA_NW;
 // r <= 64 pass-A row kernel: no register prefetch ring (PD 1) and 3 blocks per CU (166
 // VGPRs, 3 waves per SIMD, 144 KB LDS) -- the PD-2 ring needs 228 VGPRs (2 waves per SIMD;
 // at 3 it spills 113).  Measured on the Llama set: kernel 5307 vs 5165 GB/s (3-round A/B)
 constexpr int kPaPD = 1;
-constexpr int kPaMinb = 3;
+#ifndef DION_PA_MINB
+#define DION_PA_MINB 3
+#endif
+constexpr int kPaMinb = DION_PA_MINB;
+// 16-row blocks per wave of the r <= 64 pass-A row kernel (a dev build option; 2 = kRBE)
+#ifndef DION_PA_KR
+#define DION_PA_KR 2
+#endif
+constexpr int kPaKR = DION_PA_KR;
 
 constexpr int kXcdRemap = 1;
 struct BlockXYZ {
@@ -5362,7 +5373,7 @@ size_t presplit_bytes(int nq, int r, int batch) { return 2 * 16 * presplit_strid
 
 // deferred-EF pass A (rowproj_ef_kernel / colproj_ef_kernel)
 // rows per block of the fused pass A row kernel (r = 128 may run 16-row waves)
-int pa_row_block(int r) { return r > 64 ? 16 * kKR8 * kNW8 : 16 * kRBE * kPaNW; }
+int pa_row_block(int r) { return r > 64 ? 16 * kKR8 * kNW8 : 16 * kPaKR * kPaNW; }
 
 bool proj_ef_ok(int m, int n, int r, bool transposed) {
   // r = 128 (the Mixtral config) only through the h3 kernels
@@ -6372,7 +6383,7 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
           hipLaunchKernelGGL((rowproj_efgl_kernel<(RB >= kPaGlMinRB ? RB : kPaGlMinRB), GD == DION_DTYPE_F32 ? DION_DTYPE_NONE : GD>),
                              dim3(geo.gx / 2, geo.nchunk, nb), dim3(512), 0, st, e);
         else  // r = 128 without it: one-step pipeline (register budget)
-          hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, RB >= 8 ? kPD8 : kPaPD, RB >= 8 ? kKR8 : kRBE, RB >= 8 ? kNW8 : kPaNW>),
+          hipLaunchKernelGGL((rowproj_efh3_kernel<RB, GD, RB >= 8 ? kPD8 : kPaPD, RB >= 8 ? kKR8 : kPaKR, RB >= 8 ? kNW8 : kPaNW>),
                              grid, dim3(64 * (RB >= 8 ? kNW8 : kPaNW)), 0, st, e);
         return check_launch(tr ? "colproj_ef" : "rowproj_ef");
       });
