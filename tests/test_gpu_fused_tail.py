@@ -137,3 +137,31 @@ def test_row_sparse_p_follows_the_header_contract(r, transposed):
     assert torch.isfinite(Pa).all() and torch.isfinite(Ra).all()
     for a, b in zip(Qa, Qb):
         assert torch.equal(a.cpu(), b.cpu()) and torch.isfinite(a).all()
+
+
+@pytest.mark.parametrize("m,n,r", [(256, 800, 64), (544, 256, 128), (256, 544, 128), (800, 256, 128),
+                                   (256, 8224, 64), (8224, 256, 128)])
+def test_lds_dma_pass_b_ragged_k_chunks(m, n, r):
+    """Round 6's LDS-DMA pass-B kernels (rowproj_h3gl transposed at r = 64 / 128, colproj_h3gl
+    not transposed at r = 128) on contraction lengths whose split-K chunks end in short runs of
+    32-column steps (fewer steps than the staging depth, a last chunk shorter than the others),
+    against fp64, in both scale modes (pass A's max |M|: one scale per matrix; none: per-step
+    scales)."""
+    from megatron_dion_amd.codec import HipDionCodec
+
+    dev = _dev()
+    tr = m < n
+    mp, nq = (n, m) if tr else (m, n)
+    B = 3
+    gen = torch.Generator().manual_seed(m * 7 + n + r)
+    Ms = [(torch.randn(m, n, generator=gen) * 1e-2).to(dev) for _ in range(B)]
+    P = torch.linalg.qr(torch.randn(B, mp, r, generator=gen, dtype=torch.float64))[0].float().to(dev).contiguous()
+    nz = torch.stack([M.abs().max() for M in Ms]).float().cpu().view(torch.int32).clone().to(dev)
+    ref = torch.stack([(M.double().t() if tr else M.double()).t() @ P[i].double() for i, M in enumerate(Ms)])
+    codec = HipDionCodec(dev)
+    for kw in ({"nonzero": nz}, {}):
+        R = torch.zeros(B, nq, r, device=dev)
+        codec.project_r(Ms, P, R, tr, **kw)
+        torch.cuda.synchronize()
+        err = ((R.double() - ref).abs().max() / ref.abs().max()).item()
+        assert err <= 1e-6, (m, n, r, bool(kw), err)
