@@ -5213,8 +5213,11 @@ Geo rowproj_geo(int rows, int cols, int batch, int block_rows = 128, int target 
 #ifndef DION_PBR_GL_D
 #define DION_PBR_GL_D 3
 #endif
+// target blocks of its split-K geometry: 512 (one 8-wave block per CU, two rounds) measured
+// against 1024 / 2048 in call I (profiles/r06/i_ab_split_k_targets.txt): r = 128 transposed pass
+// B 0.849 -> 0.808 ms per call, r = 64 equal; half the split-K slab bytes of 1024
 #ifndef DION_TB_PBRGL
-#define DION_TB_PBRGL 1024
+#define DION_TB_PBRGL 512
 #endif
 constexpr int kPbrGlNW = DION_PBR_GL_NW;
 template <int RB>
@@ -5240,7 +5243,7 @@ Geo pbr_geo(int rows, int cols, int batch, int r);
 #define DION_PBC_GL_D 3
 #endif
 #ifndef DION_TB_PBCGL
-#define DION_TB_PBCGL 1024
+#define DION_TB_PBCGL 512  // call I: r = 128 pass B 1.542 -> 1.506 ms per call against 1024
 #endif
 constexpr int kPbcGlNW = 8, kPbcGlCT = DION_PBC_GL_CT;
 template <int RB>
