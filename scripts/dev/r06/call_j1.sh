@@ -1,4 +1,4 @@
-# round-6 call J1: the final tree's GPU suite and smoke, and the pivot record of round 5's bf16
+# round-6 call J1: the final tree's GPU suite and smoke
 set -o pipefail
 mkdir -p gpurun_out/r06j
 export TMPDIR=/tmp
