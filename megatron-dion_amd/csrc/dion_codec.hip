@@ -3486,6 +3486,11 @@ constexpr int kPD8 = 1;
 // r = 128 fused pass A row kernel: 1 = rowproj_efgl_kernel (M/G and the splits by LDS-DMA;
 // bf16 or no G, an even number of 128-row blocks), 0 = rowproj_efh3_kernel everywhere
 constexpr int kPaGl8 = 1;
+// cache policy of its bf16 G loads (64-B row pieces, the other half of the line one step later)
+#ifndef DION_PAGL_GNT
+#define DION_PAGL_GNT 0
+#endif
+constexpr int kPaGlGnt = DION_PAGL_GNT;
 constexpr int kPaGlMinRB = 8;  // the smallest rank block (r = 16 RB) that takes it (r = 64 measured slower)
 // blocks per CU the r = 128 transposed fused pass A is compiled for
 // transposed pass-A kernel (colproj_efh3_kernel) at r <= 64: 1 = the two-step SA/SB register
@@ -4175,7 +4180,7 @@ __global__ void __launch_bounds__(512, 1) rowproj_efgl_kernel(const EfProjArgs e
     if constexpr (GDT == DION_DTYPE_BF16) {
 #pragma unroll
       for (int i = 0; i < NGI; ++i)
-        glds16<false>(Gb + (static_cast<long>(16 * i) * a.ld_g + j) * 2, g_off, lds_off(&gs[slot][wave][i * 64]));
+        glds16<kPaGlGnt != 0>(Gb + (static_cast<long>(16 * i) * a.ld_g + j) * 2, g_off, lds_off(&gs[slot][wave][i * 64]));
     }
   };
 
