@@ -3491,6 +3491,14 @@ constexpr int kPaGl8 = 1;
 #define DION_PAGL_GNT 0
 #endif
 constexpr int kPaGlGnt = DION_PAGL_GNT;
+// its bf16 G in step pairs: one step's G row is 64 B, half a 128-B line, and issued a step
+// apart the two halves were fetched twice for ~1 in 6 lines (PMC: pass A 1.12x its algorithmic
+// bytes, G nt 1.21x); 1 = both halves of every line in one issue at every odd step, one step
+// ahead instead of two (split-K chunks on 64-column bounds)
+#ifndef DION_PAGL_GPAIR
+#define DION_PAGL_GPAIR 0
+#endif
+constexpr int kPaGlGpair = DION_PAGL_GPAIR;
 constexpr int kPaGlMinRB = 8;  // the smallest rank block (r = 16 RB) that takes it (r = 64 measured slower)
 // blocks per CU the r = 128 transposed fused pass A is compiled for
 // transposed pass-A kernel (colproj_efh3_kernel) at r <= 64: 1 = the two-step SA/SB register
@@ -4096,6 +4104,7 @@ __global__ void __launch_bounds__(512, 1) rowproj_efgl_kernel(const EfProjArgs e
   constexpr int GCH = GDT == DION_DTYPE_BF16 ? 4 : 0;    // 16-B chunks per G row
   constexpr int NGI = 32 * GCH / 64;
   constexpr int NMG = 4 + NGI;  // M/G LDS-DMA loads per wave and step
+  constexpr bool GP = kPaGlGpair != 0 && GCH > 0;  // G in step pairs: gs[h] = half h of the pair
   static_assert(GDT != DION_DTYPE_F32, "f32 G slots do not fit next to the splits (rowproj_efh3_kernel runs)");
   __shared__ f16x8 tq[2][NQ];
   __shared__ f16x8 rs[2][NR];
@@ -4177,25 +4186,43 @@ __global__ void __launch_bounds__(512, 1) rowproj_efgl_kernel(const EfProjArgs e
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       glds16<kNt != 0>(Mb + (static_cast<long>(8 * q) * a.ld_m + j) * 4, m_off, lds_off(&ms[slot][wave][q * 64]));
-    if constexpr (GDT == DION_DTYPE_BF16) {
+    if constexpr (GDT == DION_DTYPE_BF16 && !GP) {
 #pragma unroll
       for (int i = 0; i < NGI; ++i)
         glds16<kPaGlGnt != 0>(Gb + (static_cast<long>(16 * i) * a.ld_g + j) * 2, g_off, lds_off(&gs[slot][wave][i * 64]));
     }
   };
+  // GP: G of the even step s and of s + 1 (both halves of each 128-B line back to back) into
+  // gs[0] / gs[1]; past the chunk's end the second half loads the first again
+  auto issue_gpair = [&](int s) {
+    if constexpr (GP) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int jh = j_begin + 32 * (s + h < nsteps ? s + h : s);
+#pragma unroll
+        for (int i = 0; i < NGI; ++i)
+          glds16<kPaGlGnt != 0>(Gb + (static_cast<long>(16 * i) * a.ld_g + jh) * 2, g_off, lds_off(&gs[h][wave][i * 64]));
+      }
+    }
+  };
 
   issue_splits(0, 0);
   issue_mg(0, 0);
+  issue_gpair(0);
   if (nsteps > 1) {
     issue_mg(1, 1);
-    gl_wait_barrier<NMG>();
+    gl_wait_barrier<GP ? 4 : NMG>();
   } else {
     gl_wait_barrier<0>();
   }
+  // GP: the next pair is issued at the odd step, once gs[1] is read: a step ahead of its first
+  // use and before that step's M tiles (which stay two steps ahead), so it retires with the
+  // splits at the step's barrier
 
-  for (int s = 0; s < nsteps; ++s) {
+  // the loop runs in step pairs, so the slot and the G pair's parity are compile-time
+  auto step = [&](const int s, auto PARc) {
+    constexpr int cur = decltype(PARc)::value;  // = s & 1
     const int j = j_begin + 32 * s;
-    const int cur = s & 1;
     const bool more = s + 1 < nsteps;
     const bool ahead = s + 2 < nsteps;
     if (more) issue_splits(s + 1, cur ^ 1);
@@ -4215,6 +4242,12 @@ __global__ void __launch_bounds__(512, 1) rowproj_efgl_kernel(const EfProjArgs e
           gv[rb][c] = reinterpret_cast<const uint2*>(gs[cur][wave])[(r * GCH + p) * 2 + (g & 1)];
         }
       }
+    if constexpr (GP && cur == 1) {
+      if (more) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue_gpair(s + 1);
+      }
+    }
     if (ahead) {
       // the slot is read: refill it (the reads retire first; the DMA writes the same bytes)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -4280,13 +4313,17 @@ __global__ void __launch_bounds__(512, 1) rowproj_efgl_kernel(const EfProjArgs e
       }
     }
     if (more) {
-      // retire the next step's splits (and, in order, every older M/G load: the next step's
-      // slot); the newest M/G step and this step's 4 stores may stay in flight
+      // retire the next step's splits (and, in order, every older load: the next step's M slot
+      // and G); the newest M step and this step's 4 stores may stay in flight
       if (ahead)
-        gl_wait_barrier<NMG + 2 * KR>();
+        gl_wait_barrier<(GP ? 4 : NMG) + 2 * KR>();
       else
         gl_wait_barrier<2 * KR>();
     }
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, std::integral_constant<int, 0>{});
+    if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>{});
   }
 
   float* out = a.out + (static_cast<long>(b) * a.nchunk + kc) * a.out_rows * R;
@@ -5190,14 +5227,14 @@ constexpr int kTargetBlocks = 2048;
 constexpr int kTbPa = DION_TB_PA, kTbPbc = DION_TB_PBC, kTbPbr = DION_TB_PBR, kTbPat = DION_TB_PAT;
 
 // row projection: X rows x cols, reduce over cols (block_rows 128 generic, 256 fast)
-Geo rowproj_geo(int rows, int cols, int batch, int block_rows = 128, int target = kTargetBlocks) {
+Geo rowproj_geo(int rows, int cols, int batch, int block_rows = 128, int target = kTargetBlocks, int kalign = 32) {
   Geo g;
   g.gx = static_cast<int>(ceil_div(rows, block_rows));
   long want = ceil_div(target, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));
   long maxc = ceil_div(cols, 256);
   long nc = want < maxc ? want : maxc;
   if (nc < 1) nc = 1;
-  g.kchunk = round_up(ceil_div(cols, nc), 32);
+  g.kchunk = round_up(ceil_div(cols, nc), kalign);
   g.nchunk = static_cast<int>(ceil_div(cols, g.kchunk));
   g.out_rows = rows;
   return g;
@@ -5390,7 +5427,8 @@ bool proj_ef_ok(int m, int n, int r, bool transposed) {
 }
 
 Geo proj_ef_geo(int m, int n, int batch, bool transposed, int r) {
-  if (!transposed) return rowproj_geo(m, n, batch, pa_row_block(r), kTbPa);
+  // r = 128: K chunks on 64-column bounds (rowproj_efgl_kernel's G step pairs are whole lines)
+  if (!transposed) return rowproj_geo(m, n, batch, pa_row_block(r), kTbPa, r > 64 && kPaGlGpair ? 64 : 32);
   Geo g;
   g.gx = static_cast<int>(ceil_div(n, 128));
   long want = ceil_div(kTbPat, static_cast<long>(g.gx) * (batch > 0 ? batch : 1));

@@ -41,7 +41,8 @@ __device__ __forceinline__ f32x4 add_bf16(f32x4 x, u32x2 g) {
   return x;
 }
 
-// kind 0: mix (M += G, 10 B/elem), 1: copy (8 B/elem), 2: read (4 B/elem)
+// kind 0: mix (M += G in place, 10 B/elem), 1: copy (8 B/elem), 2: read (4 B/elem),
+// 3: mix out of place (D = M + G, 10 B/elem), 4: in-place scale (M *= 1.0001, 8 B/elem)
 template <int KIND, int U, bool NT>
 __global__ void __launch_bounds__(256) stream_kernel(f32x4* __restrict__ M, const u32x2* __restrict__ G,
                                                      f32x4* __restrict__ D, long n4, float* sink) {
@@ -54,7 +55,7 @@ __global__ void __launch_bounds__(256) stream_kernel(f32x4* __restrict__ M, cons
     for (int u = 0; u < U; ++u) {
       const long i = base + 256L * u;
       x[u] = i < n4 ? ld<NT>(M + i) : f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (KIND == 0) g[u] = i < n4 ? ld<NT>(G + i) : u32x2{0u, 0u};
+      if constexpr (KIND == 0 || KIND == 3) g[u] = i < n4 ? ld<NT>(G + i) : u32x2{0u, 0u};
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -62,6 +63,8 @@ __global__ void __launch_bounds__(256) stream_kernel(f32x4* __restrict__ M, cons
       if (i >= n4) continue;
       if constexpr (KIND == 0) st<NT>(M + i, add_bf16(x[u], g[u]));
       else if constexpr (KIND == 1) st<NT>(D + i, x[u]);
+      else if constexpr (KIND == 3) st<NT>(D + i, add_bf16(x[u], g[u]));
+      else if constexpr (KIND == 4) st<NT>(M + i, x[u] * 1.0001f);
       else s += x[u][0] + x[u][1] + x[u][2] + x[u][3];
     }
   }
@@ -69,9 +72,10 @@ __global__ void __launch_bounds__(256) stream_kernel(f32x4* __restrict__ M, cons
     if (s == 1234.5f) sink[threadIdx.x] = s;  // keeps the loads live
 }
 
-static const char* kKind[3] = {"mix (M fp32 rw + G bf16 r, 10 B/elem)", "copy (fp32 r + w, 8 B/elem)",
-                               "read (fp32 r, 4 B/elem)"};
-static const double kBytes[3] = {10.0, 8.0, 4.0};
+static const char* kKind[5] = {"mix in place (M rw, G bf16 r, 10 B/elem)", "copy (fp32 r + w, 8 B/elem)",
+                               "read (fp32 r, 4 B/elem)", "mix out of place (D = M + G, 10 B/elem)",
+                               "scale in place (M rw, 8 B/elem)"};
+static const double kBytes[5] = {10.0, 8.0, 4.0, 10.0, 8.0};
 
 template <int KIND, int U, bool NT>
 double run(f32x4* M, const u32x2* G, f32x4* D, long n4, float* sink, int blocks, int iters) {
@@ -116,7 +120,7 @@ int main() {
   CKU(hipMemset(M, 0, n * 4));
   CKU(hipMemset(D, 0, n * 4));
   CKU(hipMemset(G, 0, n * 2));
-  double best[3] = {0, 0, 0};
+  double best[5] = {0, 0, 0, 0, 0};
   sweep<0, 1, false>(M, G, D, n4, sink, best);
   sweep<0, 2, false>(M, G, D, n4, sink, best);
   sweep<0, 4, false>(M, G, D, n4, sink, best);
@@ -130,7 +134,13 @@ int main() {
   sweep<2, 2, false>(M, G, D, n4, sink, best);
   sweep<2, 4, false>(M, G, D, n4, sink, best);
   sweep<2, 4, true>(M, G, D, n4, sink, best);
-  for (int k = 0; k < 3; ++k) printf("best %-40s %8.1f GB/s = %.3f of 8 TB/s\n", kKind[k], best[k], best[k] / 8000.0);
+  sweep<3, 2, true>(M, G, D, n4, sink, best);
+  sweep<3, 4, true>(M, G, D, n4, sink, best);
+  sweep<3, 2, false>(M, G, D, n4, sink, best);
+  sweep<4, 2, true>(M, G, D, n4, sink, best);
+  sweep<4, 4, true>(M, G, D, n4, sink, best);
+  sweep<4, 2, false>(M, G, D, n4, sink, best);
+  for (int k = 0; k < 5; ++k) printf("best %-40s %8.1f GB/s = %.3f of 8 TB/s\n", kKind[k], best[k], best[k] / 8000.0);
   CKU(hipFree(M));
   CKU(hipFree(D));
   CKU(hipFree(G));

@@ -414,7 +414,11 @@ def test_llama_shape_properties(m, n):
                                        (384, 128, 128, torch.bfloat16), (256, 160, 128, torch.float32),
                                        (1152, 640, 128, torch.bfloat16), (1280, 1024, 128, torch.float32),
                                        (384, 1280, 128, torch.bfloat16), (128, 768, 128, torch.bfloat16),
-                                       (128, 640, 128, torch.bfloat16), (2048, 384, 128, torch.bfloat16)])
+                                       (128, 640, 128, torch.bfloat16), (2048, 384, 128, torch.bfloat16),
+                                       # its bf16 G in step pairs (round 6): odd step counts, a
+                                       # one-step and a three-step last K chunk
+                                       (256, 96, 128, torch.bfloat16), (1024, 800, 128, torch.bfloat16),
+                                       (1280, 1120, 128, torch.bfloat16), (512, 352, 128, torch.bfloat16)])
 def test_deferred_ef_pass_a_matches_eager_and_fp64(m, n, r, gdt):
     _deferred_ef_case(m, n, r, gdt, 0)
 
