@@ -3494,9 +3494,10 @@ constexpr int kPaGlGnt = DION_PAGL_GNT;
 // its bf16 G in step pairs: one step's G row is 64 B, half a 128-B line, and issued a step
 // apart the two halves were fetched twice for ~1 in 6 lines (PMC: pass A 1.12x its algorithmic
 // bytes, G nt 1.21x); 1 = both halves of every line in one issue at every odd step, one step
-// ahead instead of two (split-K chunks on 64-column bounds)
+// ahead instead of two (split-K chunks on 64-column bounds).  Measured (profiles/r06/l_*): the
+// launch 21.07 -> 20.04 GB (1.066x; reads 1.179x -> 1.049x), 4.78 -> 4.66 ms, Mixtral +0.6 %
 #ifndef DION_PAGL_GPAIR
-#define DION_PAGL_GPAIR 0
+#define DION_PAGL_GPAIR 1
 #endif
 constexpr int kPaGlGpair = DION_PAGL_GPAIR;
 constexpr int kPaGlMinRB = 8;  // the smallest rank block (r = 16 RB) that takes it (r = 64 measured slower)

@@ -43,9 +43,4 @@ run mx_gp1 libdion_codec_gp1.so $MX --steps 10 --warmup 2 || exit 1
 run mx_gp0 "" $MX --steps 10 --warmup 2 || exit 1
 run mx_gp1_b libdion_codec_gp1.so $MX --steps 10 --warmup 2 || exit 1
 run mx_gp0_b "" $MX --steps 10 --warmup 2 || exit 1
-# pass A's split-K block target (DION_TB_PA, both r): 2048 (default) against 1024 / 4096
 run llama "" --steps 20 --warmup 3 || exit 1
-run llama_tb1024 libdion_codec_tbpa1024.so --steps 20 --warmup 3 || exit 1
-run llama_tb4096 libdion_codec_tbpa4096.so --steps 20 --warmup 3 || exit 1
-run llama_b "" --steps 20 --warmup 3 || exit 1
-run mx_tb1024 libdion_codec_tbpa1024.so $MX --steps 10 --warmup 2 || exit 1
