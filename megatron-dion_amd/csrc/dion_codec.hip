@@ -3500,7 +3500,15 @@ constexpr int kPaGlGnt = DION_PAGL_GNT;
 #define DION_PAGL_GPAIR 1
 #endif
 constexpr int kPaGlGpair = DION_PAGL_GPAIR;
-constexpr int kPaGlMinRB = 8;  // the smallest rank block (r = 16 RB) that takes it (r = 64 measured slower)
+// the smallest rank block (r = 16 RB) that takes it, row / transposed kernel (r = 64 measured
+// slower in round 4; dev build options)
+#ifndef DION_PA_GL_MINRB
+#define DION_PA_GL_MINRB 8
+#endif
+#ifndef DION_PA_GLT_MINRB
+#define DION_PA_GLT_MINRB 8
+#endif
+constexpr int kPaGlMinRB = DION_PA_GL_MINRB, kPaGlMinRBT = DION_PA_GLT_MINRB;
 // blocks per CU the r = 128 transposed fused pass A is compiled for
 // transposed pass-A kernel (colproj_efh3_kernel) at r <= 64: 1 = the two-step SA/SB register
 // ring (234 VGPRs, 2 waves per SIMD; it spills at 3), 0 = no ring, the step's M/G loads
@@ -6421,8 +6429,8 @@ int dion_project_p_ef(const DionBatchDesc* d, const void* const* G, float* const
       return dispatch_gdt(d->g_dtype, [&](auto Gc) {
         constexpr int GD = decltype(Gc)::value;
         if (tr) {
-          if (RB >= kPaGlMinRB && GD != DION_DTYPE_F32 && kPaGl8 && geo.gx % 2 == 0)  // LDS-DMA staging
-            hipLaunchKernelGGL((colproj_efgl_kernel<(RB >= kPaGlMinRB ? RB : kPaGlMinRB), GD == DION_DTYPE_F32 ? DION_DTYPE_NONE : GD>),
+          if (RB >= kPaGlMinRBT && GD != DION_DTYPE_F32 && kPaGl8 && geo.gx % 2 == 0)  // LDS-DMA staging
+            hipLaunchKernelGGL((colproj_efgl_kernel<(RB >= kPaGlMinRBT ? RB : kPaGlMinRBT), GD == DION_DTYPE_F32 ? DION_DTYPE_NONE : GD>),
                                dim3(geo.gx / 2, geo.nchunk, nb), dim3(512), 0, st, e);
           else
             hipLaunchKernelGGL((colproj_efh3_kernel<RB, GD>), grid, dim3(256), 0, st, e);
