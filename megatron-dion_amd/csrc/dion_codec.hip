@@ -2000,6 +2000,15 @@ struct RTile<RU, true> {
 // LDS layout of a step: [u][part][lane] bf16x8 (the 32x32x16 operand run of lane
 // (t, h): factor row t, columns 16 u + 8 h .. +7), conflict-free ds_read_b128.
 // ============================================================================
+// rank_stream_kernel's tile offsets: 1 = the q-dependent part in the scalar offset (one VGPR
+// of lane offset instead of 16: r = 128 135 -> 120 VGPRs, two 8-wave blocks per CU).  Measured
+// (profiles/r06/p_ab_update_soff.txt): the r = 128 kernel alone 2.055 -> 1.977 ms, the steps
+// slower (Mixtral 398.9 -> 396.2, Llama 484.3 -> 481.7 GiB/s): the second block takes issue
+// slots from the other stream's kernel.  Kept at 0 (a dev build option)
+#ifndef DION_RS_SOFF
+#define DION_RS_SOFF 0
+#endif
+constexpr int kRsSoff = DION_RS_SOFF;
 template <int RU, bool ROWFIX, int NW, int D, bool H3 = false>
 __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_stream_kernel(const RankArgs a) {
   constexpr int R = 16 * RU;
@@ -2025,9 +2034,17 @@ __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_st
   const float* Sb = a.sptr[b] != nullptr ? a.sptr[b] : a.S + static_cast<long>(b) * a.s_stride;
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       a.x[b], static_cast<short>(0), static_cast<int>(min(static_cast<long>(rows) * ld * 4, 0x7FFFFFF0L)), 0x00020000);
-  int voff[16];
+  // lane offset of tile value q: ((q & 3) + 8 (q >> 2) + 4 h) ld + t.  kRsSoff: the lane part
+  // (4 h ld + t) in one VGPR, the q part (wave-uniform) in the scalar offset, instead of 16
+  // VGPRs of offsets
+  int voff[kRsSoff ? 1 : 16];
+  if constexpr (kRsSoff) {
+    voff[0] = (4 * h * ld + t) * 4;
+  } else {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) voff[q] = (((q & 3) + 8 * (q >> 2) + 4 * h) * ld + t) * 4;
+    for (int q = 0; q < 16; ++q) voff[q] = (((q & 3) + 8 * (q >> 2) + 4 * h) * ld + t) * 4;
+  }
+  auto qoff = [&](int q) { return ((q & 3) + 8 * (q >> 2)) * ld * 4; };
 
   Split3 F[H3 ? 1 : RU];
   Split2h FH[H3 ? RU : 1];
@@ -2087,7 +2104,9 @@ __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_st
     const int col0 = ROWFIX ? s0 : fbase;
     const int so = (row0 * ld + col0) * 4;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) T[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff[q], so, kStreamAux));
+    for (int q = 0; q < 16; ++q)
+      T[q] = __uint_as_float(kRsSoff ? __builtin_amdgcn_raw_buffer_load_b32(rx, voff[0], so + qoff(q), kStreamAux)
+                                     : __builtin_amdgcn_raw_buffer_load_b32(rx, voff[kRsSoff ? 0 : q], so, kStreamAux));
   };
   auto compute_store = [&](int s0, const f32x16& T, const bf16x8* src) {
     f32x16 acc;
@@ -2116,7 +2135,10 @@ __global__ void __launch_bounds__(64 * NW, (RU >= 7 || NW >= 8) ? 1 : 2) rank_st
     for (int q = 0; q < 16; ++q) {
       // X d rounded first (the reference's W.mul_(1 - lr wd)), then the update added
       const float v = H3 ? fmaf(acc[q], ainv, __fmul_rn(T[q], a.decay)) : __fmul_rn(T[q], a.decay) + acc[q];
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[q], so, kStreamAux);
+      if constexpr (kRsSoff)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[0], so + qoff(q), kStreamAux);
+      else
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx, voff[kRsSoff ? 0 : q], so, kStreamAux);
     }
   };
 
