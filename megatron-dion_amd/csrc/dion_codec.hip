@@ -5240,8 +5240,10 @@ struct Geo {
 };
 
 constexpr int kTargetBlocks = 2048;
+// pass A's row-kernel target: 1024 against 2048 / 512 in call Q (profiles/r06/q_ab_pass_a_targets.txt:
+// Llama 478.7 -> 481.2 GiB/s; qkv / proj in 2 K chunks instead of 3 / 4: fewer slab and P' bytes)
 #ifndef DION_TB_PA
-#define DION_TB_PA 2048
+#define DION_TB_PA 1024
 #endif
 #ifndef DION_TB_PBC
 #define DION_TB_PBC 512
