@@ -3513,6 +3513,12 @@ constexpr int kPaGl8 = 1;
 #define DION_PAGL_GNT 0
 #endif
 constexpr int kPaGlGnt = DION_PAGL_GNT;
+// the 8-wave LDS-DMA kernels (pass A at r = 128, pass B): priority 1 for waves 4-7 (the guide's
+// static form for two waves per SIMD); a dev build option
+#ifndef DION_GL_PRIO
+#define DION_GL_PRIO 0
+#endif
+constexpr int kGlPrio = DION_GL_PRIO;
 // its bf16 G in step pairs: one step's G row is 64 B, half a 128-B line, and issued a step
 // apart the two halves were fetched twice for ~1 in 6 lines (PMC: pass A 1.12x its algorithmic
 // bytes, G nt 1.21x); 1 = both halves of every line in one issue at every odd step, one step
@@ -3738,6 +3744,7 @@ __global__ void __launch_bounds__(64 * NW, 1) colproj_h3gl_kernel(const ProjArgs
   const int kc = blk.y;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (kGlPrio && wave >= 4) __builtin_amdgcn_s_setprio(1);  // the younger half of the 8 waves
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
@@ -4148,6 +4155,7 @@ __global__ void __launch_bounds__(512, 1) rowproj_efgl_kernel(const EfProjArgs e
   const int kc = blk.y;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar addressing)
+  if (kGlPrio && wave >= 4) __builtin_amdgcn_s_setprio(1);  // the younger half of the 8 waves
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
@@ -4612,6 +4620,7 @@ __global__ void __launch_bounds__(512, 1) colproj_efgl_kernel(const EfProjArgs e
   const int kc = blk.y;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (kGlPrio && wave >= 4) __builtin_amdgcn_s_setprio(1);  // the younger half of the 8 waves
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
@@ -5037,6 +5046,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rowproj_h3gl_kernel(const ProjArgs
   const int kc = blk.y;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (kGlPrio && wave >= 4) __builtin_amdgcn_s_setprio(1);  // the younger half of the 8 waves
   const int lane = tid & 63;
   const int t = lane & 15;
   const int g = lane >> 4;
